@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py -- baseband Msamples/s integrated + % HBM-read roofline.
+
+One "step" = one full 1024x1024-sample integration (README.md:2) of one
+sub-band per GPU: the HBM-resident block is unpacked, detected and
+time-integrated by the gfx950 kernel and the fp32 spectrum is emitted
+(finalize kernel).  Default workload = BASELINE.json configs[1]: 256 chans
+x 2 pols int8 (1 GiB per integration).  Inputs are synthetic (counter-based
+generator) and rotate over 4 distinct 1-GiB blocks per GPU so the
+256 MiB Infinity Cache cannot serve repeats.
+
+Multi-GPU (torchrun, one process per GPU): sub-band r on GPU r, no data-path
+collective; the K spectra of every rank are gathered to rank 0 over RCCL
+(torch.distributed "nccl") inside the timed region (configs[3]/[4]).
+value = all ranks' samples / max-over-ranks time  (weak scaling).
+
+Prints ONE JSON line on rank 0.  Options beyond the driver contract:
+  --config c2|c5|bmf|c3   workload (c3 = pinned host buffer, H2D overlapped;
+                          its value is PCIe-bound and is never the default)
+  --cpu-seconds S         bounded CPU-baseline sample (0 disables)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "paf-baseband2power_amd"))
+
+import torch  # noqa: E402  (first: one HIP runtime per process, see paf_b2p/_lib.py)
+import torch.distributed as dist  # noqa: E402
+
+import paf_b2p  # noqa: E402
+from paf_b2p.geometry import CONFIGS, samples_per_block  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+SEED = 20181105
+NBLOCKS = 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=["c2", "c5", "bmf", "c3"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def pmc_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary for this
+    config (profiles/pmc_<config>.json, written by tools/pmc_summary.py from
+    separate --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
+    p = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(p):
+        return None, None
+    try:
+        d = json.load(open(p))
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(p, REPO)
+    except Exception:
+        return None, None
+
+
+def cpu_baseline(geom, seconds: float, threads: int):
+    """The oracle's C restatement (oracle/b2p_oracle.c), OpenMP over host
+    threads, on a bounded sample of the same workload held in host RAM."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import b2p_oracle as npo  # noqa: E402
+    import oracle_c as co  # noqa: E402
+    g = npo.Geom(**geom.as_dict())
+    sample_bytes = min(g.block_bytes, 256 << 20) // g.frame_bytes * g.frame_bytes
+    buf = co.fill_synthetic(g, sample_bytes, SEED, 0, 0)
+    if threads <= 0:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    co.integrate(g, buf[: g.frame_bytes * 64], nthreads=threads)  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        co.integrate(g, buf, nthreads=threads)
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or passes >= 1000:
+            break
+    samples = passes * sample_bytes // g.word_bytes * g.npol
+    return {"value": round(samples / el / 1e6, 2), "unit": "Msamples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{passes} passes over {sample_bytes >> 20} MiB of the same synthetic "
+                      f"{g.nchan}-chan int{g.nbit} block ({el:.1f} s, host RAM, no file I/O)"}
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(world, 1)
+    cfg = CONFIGS[a.config]
+    geom = cfg["geom"]()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    it = paf_b2p.Integrator(geom, device=local)
+    nout, bb = it.nout, it.block_bytes
+    spb = samples_per_block(geom)
+
+    if world > 1:
+        # finalize writes into torch memory on torch's stream so the gather
+        # is ordered after it (one stream, no host sync inside the loop)
+        it.set_stream(torch.cuda.current_stream().cuda_stream)
+        out_t = torch.zeros((a.steps, nout), dtype=torch.float32, device="cuda")
+        out_ptr = out_t.data_ptr()
+        gather_t = torch.zeros((world, a.steps, nout), dtype=torch.float32, device="cuda")
+    else:
+        out_buf = it.alloc(max(a.steps, 1) * nout * 4)
+        out_ptr = out_buf.ptr
+
+    host_mode = a.config == "c3"
+    blocks = []
+    if host_mode:
+        import numpy as np
+        hb = np.empty(bb, dtype=np.uint8)
+        d = it.alloc(bb)
+        it.fill_synthetic(d, SEED, rank, 0)
+        hb[:] = it.download(d)
+        d.free()
+        it.register_host(hb)
+        blocks = [hb]
+    else:
+        for b in range(NBLOCKS):
+            d = it.alloc(bb)
+            it.fill_synthetic(d, SEED, rank, b)
+            blocks.append(d)
+    it.sync()
+
+    def step(k, out_row):
+        it.push(blocks[k % len(blocks)])
+        it.finish_async(out_ptr + out_row * nout * 4, True) if out_row is not None else \
+            it.finish_async(out_ptr, True)
+
+    for w in range(a.warmup):
+        step(w, None)
+    it.sync()
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+
+    it.reset_stats()
+    it.set_timing(True)
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(a.warmup + k, k)
+    if world > 1:
+        dist.all_gather_into_tensor(gather_t.view(world * a.steps, nout), out_t)
+        torch.cuda.synchronize()
+    it.sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    it.set_timing(False)
+    st = it.stats()
+
+    el_max = el
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_max = float(t.item())
+
+    kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
+    bytes_per_launch = st["bytes"] / max(st["launches"], 1)
+    achieved = bytes_per_launch / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(a.config)
+
+    if rank == 0:
+        value = n_gpus * a.steps * spb / el_max / 1e6
+        res = {
+            "metric": "baseband Msamples/s integrated + % HBM-read roofline, 1024x1024 accum",
+            "value": round(value, 1),
+            "unit": "Msamples/s",
+            "n_gpus": n_gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el_max / max(a.steps, 1) * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": f"int{geom.nbit}" + ("-be" if geom.big_endian else ""),
+            "data": "synthetic (counter-based SplitMix64 Gaussian, seed 20181105, sub-band = rank)",
+            "config": {
+                "workload": cfg["what"] + ("" if world == 1 else f"; {world} sub-bands, 1 per GPU"),
+                "baseline_config": {"c2": "configs[1]", "c5": "configs[4]", "c3": "configs[2]",
+                                    "bmf": "reference-native"}[a.config],
+                "nchan": int(geom.nchunk * geom.nchan_chunk),
+                "npol": int(geom.npol),
+                "nsamp_int": int(geom.nsamp_int),
+                "bytes_per_integration": int(bb),
+                "input": "pinned host buffer, H2D overlapped (PCIe-inclusive)" if host_mode
+                         else f"HBM-resident, {NBLOCKS} rotating blocks",
+                "parallelism": f"sub-band sharding x{n_gpus}" + (", RCCL all-gather of spectra"
+                                                                   if world > 1 else ""),
+                "launch": {"threads": it.info.threads, "columns": it.info.columns,
+                           "row_groups": it.info.row_groups, "replicas": it.info.replicas},
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "b2p_integrate_kernel",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                "avg_launch_us": round(kern_avg_s * 1e6, 2),
+                "finalize_avg_us": round(st["finalize_ms"] / max(st["finalizes"], 1) * 1e3, 2),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and a.cpu_seconds > 0 and not host_mode:
+            res["cpu_baseline"] = cpu_baseline(geom, a.cpu_seconds, a.cpu_threads)
+        print(json.dumps(res), flush=True)
+
+    for b in blocks:
+        if hasattr(b, "free"):
+            b.free()
+    if host_mode:
+        it.unregister_host(blocks[0])
+    it.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+/*
+ * include/b2p.h -- C ABI of the MI355X baseband->power integrator.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference
+ * (xinpingdeng/paf-baseband2power) declares the path but leaves it empty:
+ *   - paf_baseband2power.cu:32-93  main(): CLI, log, cudaGetDeviceCount, exit
+ *   - baseband2power.cuh:18-23     conf_t {device_id, dir, key_in, key_out}
+ *   - baseband2power.cu:1-16       host driver (includes only)
+ *   - kernel.cu:1-7, kernel.cuh    GPU kernel module (includes only)
+ *   - cudautil.cuh:10-66           CudaSafeCall -> exit(-1) error convention
+ *   - cudautil.cuh:118-125         BSWAP_64 unpack primitive
+ * Every entry point below names the reference item it replaces.  The C host
+ * (paf-baseband2power_amd/csrc/host/paf_baseband2power.c) calls only this
+ * header; hipcc-built code lives behind it (libpafb2p.so).
+ *
+ * Conventions: plain C types only, no exceptions, never exit(); every call
+ * returns B2P_OK (0) or a negative B2P_E* code (b2p_strerror()).  The caller
+ * owns every buffer.  A context is not thread-safe; use one per device /
+ * sub-band (contexts are independent).
+ */
+#ifndef B2P_H
+#define B2P_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define B2P_ABI_VERSION 1
+
+/* status codes (replace CudaSafeCall's exit(-1), cudautil.cuh:29-41) */
+#define B2P_OK 0
+#define B2P_EINVAL (-1)       /* bad argument or unsupported geometry          */
+#define B2P_ERAGGED (-2)      /* nbytes is not a whole number of frames        */
+#define B2P_EOVERFLOW (-3)    /* push would exceed nsamp_int of the integration */
+#define B2P_EPARTIAL (-4)     /* finish with != nsamp_int samples (output written) */
+#define B2P_ENODEV (-5)       /* no HIP device / device index out of range     */
+#define B2P_EHIP (-6)         /* HIP runtime error; text in b2p_last_error()    */
+#define B2P_ENOMEM (-7)       /* device or host allocation failed              */
+#define B2P_EALIGN (-8)       /* buffer not 16-byte aligned                    */
+
+/*
+ * Layout of one input ring block:
+ *   [frame][chunk nchunk][samp nsamp_df][chan nchan_chunk][pol npol][dim ndim]
+ * This is the TFTFP order of capture.c:540 ("cbuf_loc = (idf*NCHK_NIC +
+ * ifreq)*pkt_size"), payload only (capture.c:222).  Global channel =
+ * chunk*nchan_chunk + chan.  BMF-native: nbit 16, big_endian 1, nchunk 48,
+ * nsamp_df 128, nchan_chunk 7 (capture.h:20,28; paf-baseband2power.conf:2-5).
+ * The 256/1024-channel int8 configs use nchunk 1, nsamp_df 1.
+ *
+ * Supported: nbit 8 (big_endian 0) or 16; npol 2; ndim 2; npol_out 1 or 2;
+ * chunk bytes (nsamp_df*nchan_chunk*word) a multiple of 16;
+ * nchan*npol_out <= 8192; nsamp_int a multiple of nsamp_df.
+ *
+ * Word decode (16-bit BE, cudautil.cuh:118-125): lane k = bits [16k,16k+16)
+ * of BSWAP_64(word); lane0 X.re, lane1 X.im, lane2 Y.re, lane3 Y.im.
+ * Otherwise components are stored X.re, X.im, Y.re, Y.im.
+ *
+ * Output (header_baseband2power.txt:39-42, paf-baseband2power.py:77-79):
+ * one fp32 per channel (npol_out 1: |X|^2+|Y|^2), or per channel and pol
+ * ([chan][pol], npol_out 2).  Value = RNE_fp32(exact integer sum), or
+ * RNE_fp32((double)sum / nsamp_int) with mean = 1 ("average", :20).
+ */
+typedef struct b2p_geom {
+  uint32_t nbit;
+  uint32_t big_endian;
+  uint32_t nchunk;
+  uint32_t nsamp_df;
+  uint32_t nchan_chunk;
+  uint32_t npol;
+  uint32_t ndim;
+  uint32_t npol_out;
+  uint64_t nsamp_int;   /* samples per integration, README.md:2 -> 1024*1024 */
+  uint32_t mean;
+  uint32_t reserved;    /* must be 0 */
+} b2p_geom_t;
+
+/* Launch/geometry facts of an open context. */
+typedef struct b2p_info {
+  uint32_t nchan;        /* nchunk*nchan_chunk                     */
+  uint32_t nout;         /* nchan*npol_out fp32 outputs             */
+  uint64_t frame_bytes;  /* push granule                            */
+  uint64_t block_bytes;  /* one integration = nsamp_int samples     */
+  uint32_t threads;      /* active threads per workgroup            */
+  uint32_t columns;      /* workgroups across one row               */
+  uint32_t row_groups;   /* workgroups along time                   */
+  uint32_t row_vectors;  /* 16-B vectors per row                    */
+  uint32_t replicas;     /* accumulator replicas                    */
+  uint32_t device;
+} b2p_info_t;
+
+/* Kernel timing collected with HIP events on the context's stream. */
+typedef struct b2p_stats {
+  uint64_t launches;      /* integrate-kernel launches timed        */
+  uint64_t bytes;         /* algorithmic bytes read by them         */
+  double kernel_ms;       /* summed kernel time (ms)                */
+  double finalize_ms;     /* summed finalize-kernel time (ms)       */
+  uint64_t finalizes;
+} b2p_stats_t;
+
+typedef struct b2p_ctx b2p_ctx_t;
+
+/* ---- geometry helpers (no device needed) ---- */
+/* BMF-native defaults: 48 chunks x 7 chans int16 BE, 1<<20 samples.
+ * Replaces the constants of capture.h:20,28 and paf-baseband2power.conf. */
+int b2p_geom_bmf(b2p_geom_t *g);
+/* 0 if supported, else B2P_EINVAL */
+int b2p_geom_check(const b2p_geom_t *g);
+uint64_t b2p_frame_bytes(const b2p_geom_t *g);
+uint64_t b2p_block_bytes(const b2p_geom_t *g);
+const char *b2p_strerror(int code);
+int b2p_abi_version(void);
+
+/* ---- devices (paf_baseband2power.cu:86-90) ---- */
+int b2p_device_count(int *count);
+
+/* ---- context lifecycle ----
+ * b2p_open replaces the intended init of baseband2power.cu (empty) and the
+ * device selection at paf_baseband2power.cu:87-90: device < 0 is an error;
+ * if exactly one device is visible, index 0 is used whatever was asked (the
+ * reference's docker fallback). */
+int b2p_open(b2p_ctx_t **ctx, const b2p_geom_t *g, int device);
+int b2p_close(b2p_ctx_t *ctx);
+int b2p_get_info(const b2p_ctx_t *ctx, b2p_info_t *info);
+const char *b2p_last_error(const b2p_ctx_t *ctx); /* ctx may be NULL */
+/* Run on the caller's HIP stream (e.g. a framework's current stream);
+ * NULL restores the context's own stream. */
+int b2p_set_stream(b2p_ctx_t *ctx, void *hip_stream);
+
+/* ---- host memory (role of PSRDADA dada_cuda_dbregister; dada_cuda.h is
+ * included at baseband2power.cuh:9) ---- */
+int b2p_register_host(b2p_ctx_t *ctx, void *base, size_t bytes);
+int b2p_unregister_host(b2p_ctx_t *ctx, void *base);
+
+/* ---- the hot path (the intended body of kernel.cu) ----
+ * Accumulate nbytes (a whole number of frames) of baseband into the
+ * context's running integration: unpack -> |X|^2+|Y|^2 -> exact time sum.
+ * is_device = 1: buf is device memory (16-B aligned), the kernel reads it in
+ *   place; returns once enqueued.
+ * is_device = 0: buf is host memory (register it for full PCIe rate); it is
+ *   copied in frame-aligned chunks on a copy stream overlapped with the
+ *   kernel, and b2p_push returns once every byte has been copied, so the
+ *   caller may release / close the DADA block. */
+int b2p_push(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device);
+/* Emit the integration: out[nout] (host memory), blocking.  Returns B2P_OK
+ * if exactly nsamp_int samples were pushed, B2P_EPARTIAL otherwise (the
+ * output is still written).  Resets the integration. */
+int b2p_finish(b2p_ctx_t *ctx, float *out);
+/* Same, enqueued: out is device memory (out_is_device = 1) or pinned host
+ * memory; valid after b2p_sync(). */
+int b2p_finish_async(b2p_ctx_t *ctx, float *out, int out_is_device);
+int b2p_sync(b2p_ctx_t *ctx);
+/* Number of samples pushed into the current integration. */
+uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
+
+/* ---- measurement ---- */
+int b2p_set_timing(b2p_ctx_t *ctx, int enable);
+int b2p_get_stats(b2p_ctx_t *ctx, b2p_stats_t *stats); /* synchronises */
+int b2p_reset_stats(b2p_ctx_t *ctx);
+
+/* ---- synthetic baseband + device buffers (bench / tests) ----
+ * Same generator as oracle/b2p_oracle.c:orc_fill_synthetic, bit for bit. */
+int b2p_fill_synthetic(b2p_ctx_t *ctx, void *dev, size_t nbytes, uint64_t seed,
+                       uint32_t subband, uint64_t block, uint64_t elem0);
+int b2p_dev_alloc(b2p_ctx_t *ctx, void **dev, size_t bytes);
+int b2p_dev_free(b2p_ctx_t *ctx, void *dev);
+/* kind: 1 host->device, 2 device->host, 3 device->device; synchronous */
+int b2p_memcpy(b2p_ctx_t *ctx, void *dst, const void *src, size_t bytes, int kind);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* B2P_H */

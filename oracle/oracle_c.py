@@ -1,0 +1,116 @@
+"""oracle/oracle_c.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the C restatement (oracle/b2p_oracle.c) for tests/,
+``__graft_entry__.smoke()`` and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from b2p_oracle import Geom  # noqa: E402  (oracle/ is put on sys.path by callers)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "lib", "liboracle_b2p.so")
+_REF_HDR = os.path.join(_HERE, "_ref", "libhdr_ref.so")
+
+
+class OrcGeom(C.Structure):
+    _fields_ = [("nbit", C.c_uint32), ("big_endian", C.c_uint32), ("nchunk", C.c_uint32),
+                ("nsamp_df", C.c_uint32), ("nchan_chunk", C.c_uint32), ("npol", C.c_uint32),
+                ("ndim", C.c_uint32), ("npol_out", C.c_uint32), ("nsamp_int", C.c_uint64),
+                ("mean", C.c_uint32), ("reserved", C.c_uint32)]
+
+    @classmethod
+    def of(cls, g: Geom) -> "OrcGeom":
+        return cls(g.nbit, g.big_endian, g.nchunk, g.nsamp_df, g.nchan_chunk, g.npol, g.ndim,
+                   g.npol_out, g.nsamp_int, g.mean, 0)
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        P = C.c_void_p
+        L.orc_integrate.argtypes = [C.POINTER(OrcGeom), P, C.c_size_t, P]
+        L.orc_integrate_mt.argtypes = [C.POINTER(OrcGeom), P, C.c_size_t, P, C.c_int]
+        L.orc_finalize.argtypes = [C.POINTER(OrcGeom), P, P]
+        L.orc_fill_synthetic.argtypes = [C.POINTER(OrcGeom), P, C.c_size_t, C.c_uint64,
+                                         C.c_uint32, C.c_uint64, C.c_uint64]
+        L.orc_bmf_lanes.argtypes = [P, P]
+        L.orc_splitmix64.argtypes = [C.c_uint64]
+        L.orc_splitmix64.restype = C.c_uint64
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def integrate(g: Geom, buf: np.ndarray, nthreads: int = 1, acc: np.ndarray | None = None) -> np.ndarray:
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    if acc is None:
+        acc = np.zeros(g.nout, dtype=np.uint64)
+    og = OrcGeom.of(g)
+    if nthreads > 1:
+        rc = lib().orc_integrate_mt(C.byref(og), _ptr(buf), buf.size, _ptr(acc), nthreads)
+    else:
+        rc = lib().orc_integrate(C.byref(og), _ptr(buf), buf.size, _ptr(acc))
+    if rc != 0:
+        raise ValueError("oracle rejected input (ragged or unsupported geometry)")
+    return acc
+
+
+def finalize(g: Geom, acc: np.ndarray) -> np.ndarray:
+    acc = np.ascontiguousarray(acc, dtype=np.uint64)
+    out = np.zeros(g.nout, dtype=np.float32)
+    lib().orc_finalize(C.byref(OrcGeom.of(g)), _ptr(acc), _ptr(out))
+    return out
+
+
+def power(g: Geom, buf: np.ndarray, nthreads: int = 1) -> np.ndarray:
+    return finalize(g, integrate(g, buf, nthreads))
+
+
+def fill_synthetic(g: Geom, nbytes: int, seed: int, subband: int, block: int,
+                   elem0: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+    if out is None:
+        out = np.empty(nbytes, dtype=np.uint8)
+    lib().orc_fill_synthetic(C.byref(OrcGeom.of(g)), _ptr(out), nbytes, seed, subband, block, elem0)
+    return out
+
+
+def bmf_lanes(word: bytes) -> np.ndarray:
+    w = np.frombuffer(word, dtype=np.uint8).copy()
+    lanes = np.zeros(4, dtype=np.int16)
+    lib().orc_bmf_lanes(_ptr(w), _ptr(lanes))
+    return lanes
+
+
+class HdrT(C.Structure):
+    """struct hdr_t of the reference (hdr.h:6-14)."""
+    _fields_ = [("valid", C.c_int), ("idf", C.c_uint64), ("sec", C.c_uint64),
+                ("epoch", C.c_int), ("beam", C.c_int), ("freq", C.c_double)]
+
+
+def ref_hdr_lib():
+    """The reference's own hdr.c built by `make -C oracle ref` (None if absent)."""
+    if not os.path.exists(_REF_HDR):
+        return None
+    L = C.CDLL(_REF_HDR)
+    L.hdr_keys.argtypes = [C.c_void_p, C.POINTER(HdrT)]
+    L.hdr_keys.restype = C.c_int
+    return L

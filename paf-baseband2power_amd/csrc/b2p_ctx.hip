@@ -1,0 +1,569 @@
+// C ABI of the integrator (include/b2p.h): context, streams, staging, timing.
+//
+// Replaces the empty host driver of the reference (baseband2power.cu:1-16)
+// and its error convention (cudautil.cuh:29-66: print + exit(-1)) with
+// status codes.  All HIP calls go through CK() which records the HIP error
+// text in the context and returns B2P_EHIP.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "b2p.h"
+#include "b2p_internal.h"
+
+using namespace b2p;
+
+namespace {
+
+constexpr uint32_t kMaxOut = 8192;      // LDS: 64 KiB of uint64 sums
+constexpr uint32_t kTimingRing = 4096;  // event pairs kept before a drain
+
+thread_local char g_err[256];  // errors before a context exists
+
+struct EvPair {
+  hipEvent_t a, b;
+  uint64_t bytes;
+  int kind;  // 0 integrate, 1 finalize
+};
+
+}  // namespace
+
+struct b2p_ctx {
+  b2p_geom_t g;
+  int device = 0;
+  int mode = kI8;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;
+  // launch geometry
+  uint32_t VW = 0, IV = 0, FV = 0, CP = 0;
+  uint32_t B = 0, Bpad = 0, S = 0, NC = 0, G = 0;
+  uint32_t nchan = 0, nout = 0, nrep = 0;
+  uint64_t frame_bytes = 0, block_bytes = 0;
+  unsigned long long *d_rep = nullptr;
+  float *d_out = nullptr;
+  // host-buffer staging (double buffered)
+  uint8_t *d_stage[2] = {nullptr, nullptr};
+  uint64_t stage_bytes = 0;
+  hipEvent_t ev_copied[2] = {nullptr, nullptr};
+  hipEvent_t ev_consumed[2] = {nullptr, nullptr};
+  uint32_t stage_next = 0;
+  uint64_t samples = 0;
+  // timing
+  int timing = 0;
+  std::vector<EvPair> pending;
+  std::vector<hipEvent_t> ev_pool;
+  b2p_stats_t stats{};
+  char err[256] = {0};
+};
+
+static int set_err(b2p_ctx_t *c, int code, const char *fmt, ...) {
+  char *dst = c ? c->err : g_err;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(dst, 256, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define CK(c, call)                                                            \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess)                                                      \
+      return set_err((c), B2P_EHIP, "%s failed at %s:%d: %s", #call, __FILE__, \
+                     __LINE__, hipGetErrorString(e_));                         \
+  } while (0)
+
+static uint32_t gcd_u(uint32_t a, uint32_t b) {
+  while (b) {
+    uint32_t t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+static uint64_t word_bytes(const b2p_geom_t *g) {
+  return (uint64_t)g->npol * g->ndim * (g->nbit / 8);
+}
+
+extern "C" {
+
+int b2p_abi_version(void) { return B2P_ABI_VERSION; }
+
+const char *b2p_strerror(int code) {
+  switch (code) {
+    case B2P_OK: return "ok";
+    case B2P_EINVAL: return "invalid argument or unsupported geometry";
+    case B2P_ERAGGED: return "span is not a whole number of frames";
+    case B2P_EOVERFLOW: return "push exceeds nsamp_int of the integration";
+    case B2P_EPARTIAL: return "integration finished with != nsamp_int samples";
+    case B2P_ENODEV: return "no such HIP device";
+    case B2P_EHIP: return "HIP runtime error";
+    case B2P_ENOMEM: return "out of memory";
+    case B2P_EALIGN: return "buffer not 16-byte aligned";
+  }
+  return "unknown error";
+}
+
+const char *b2p_last_error(const b2p_ctx_t *c) { return c ? c->err : g_err; }
+
+int b2p_geom_bmf(b2p_geom_t *g) {
+  if (!g) return B2P_EINVAL;
+  memset(g, 0, sizeof(*g));
+  g->nbit = 16;          // BMF payload: 16-bit complex, big-endian
+  g->big_endian = 1;
+  g->nchunk = 48;        // NCHK_NIC (capture.h:20, conf:5)
+  g->nsamp_df = 128;     // NSAMP_DF (conf:2); 7168 B = 128 x 7 x 8 (capture.h:28)
+  g->nchan_chunk = 7;
+  g->npol = 2;           // NPOL_SAMP (conf:3)
+  g->ndim = 2;           // NDIM_POL (conf:4)
+  g->npol_out = 1;       // header_baseband2power.txt:41 NPOL 1
+  g->nsamp_int = 1u << 20;  // README.md:2, 1024 x 1024
+  g->mean = 0;
+  return B2P_OK;
+}
+
+uint64_t b2p_frame_bytes(const b2p_geom_t *g) {
+  return g ? (uint64_t)g->nchunk * g->nsamp_df * g->nchan_chunk * word_bytes(g) : 0;
+}
+
+uint64_t b2p_block_bytes(const b2p_geom_t *g) {
+  if (!g || !g->nsamp_df) return 0;
+  return g->nsamp_int / g->nsamp_df * b2p_frame_bytes(g);
+}
+
+int b2p_geom_check(const b2p_geom_t *g) {
+  if (!g) return B2P_EINVAL;
+  if (g->nbit != 8 && g->nbit != 16) return B2P_EINVAL;
+  if (g->nbit == 8 && g->big_endian) return B2P_EINVAL;
+  if (g->npol != 2 || g->ndim != 2) return B2P_EINVAL;
+  if (g->npol_out != 1 && g->npol_out != 2) return B2P_EINVAL;
+  if (!g->nchunk || !g->nsamp_df || !g->nchan_chunk) return B2P_EINVAL;
+  if (g->reserved) return B2P_EINVAL;
+  if (!g->nsamp_int || g->nsamp_int % g->nsamp_df) return B2P_EINVAL;
+  const uint64_t chunk_bytes = (uint64_t)g->nsamp_df * g->nchan_chunk * word_bytes(g);
+  if (chunk_bytes % 16) return B2P_EINVAL;
+  const uint64_t nout = (uint64_t)g->nchunk * g->nchan_chunk * g->npol_out;
+  if (nout > kMaxOut) return B2P_EINVAL;
+  if (chunk_bytes / 16 * g->nchunk > 0xffffffffull) return B2P_EINVAL;
+  return B2P_OK;
+}
+
+int b2p_device_count(int *count) {
+  if (!count) return B2P_EINVAL;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return set_err(nullptr, B2P_ENODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *count = n;
+  return B2P_OK;
+}
+
+// Choose the workgroup shape (DESIGN.md "integrate kernel / launch shape").
+static int plan_launch(b2p_ctx_t *c, int ncu) {
+  const b2p_geom_t *g = &c->g;
+  const uint32_t wb = (uint32_t)word_bytes(g);
+  c->VW = 16 / wb;
+  c->IV = g->nsamp_df * g->nchan_chunk / c->VW;
+  c->FV = g->nchunk * c->IV;
+  const uint32_t P = g->nchan_chunk / gcd_u(g->nchan_chunk, c->VW);
+  c->CP = g->nchunk == 1 ? P : c->FV;
+  uint32_t maxT = 1024;
+  if (const char *e = getenv("B2P_MAX_THREADS")) {
+    int v = atoi(e);
+    if (v >= 64 && v <= 1024) maxT = (uint32_t)v;
+  }
+  if (c->CP <= maxT) {
+    const uint32_t L = c->CP / gcd_u(c->CP, 64) * 64;  // lcm(CP, 64)
+    c->B = L <= maxT ? (maxT / L) * L : (maxT / c->CP) * c->CP;
+    c->S = c->B;
+    c->NC = 1;
+  } else {
+    uint32_t best = 0;
+    for (uint32_t b = maxT / 64 * 64; b >= 64; b -= 64)
+      if (c->CP % b == 0) { best = b; break; }
+    if (!best)
+      for (uint32_t b = maxT; b >= 128; --b)
+        if (c->CP % b == 0) { best = b; break; }
+    if (!best) return set_err(c, B2P_EINVAL, "no workgroup shape divides the %u-vector frame", c->CP);
+    c->B = best;
+    c->S = c->CP;
+    c->NC = c->CP / c->B;
+  }
+  c->Bpad = (c->B + 63) / 64 * 64;
+  // one resident wave of workgroups: as many per CU as registers/LDS admit
+  int occ = 0;
+  const size_t lds = (size_t)c->nout * sizeof(unsigned long long);
+  if (occupancy_integrate(c->mode, (int)g->npol_out, c->Bpad, lds, &occ) != hipSuccess || occ < 1)
+    occ = 1;
+  uint32_t per_cu = (uint32_t)occ;
+  if (const char *e = getenv("B2P_WG_PER_CU")) {
+    int v = atoi(e);
+    if (v >= 1 && v <= 32) per_cu = (uint32_t)v;
+  }
+  const uint32_t target = (uint32_t)ncu * per_cu;
+  c->G = std::max<uint32_t>(1, (target + c->NC / 2) / c->NC);
+  if (const char *e = getenv("B2P_ROW_GROUPS")) {  // test knob: long per-lane runs
+    int v = atoi(e);
+    if (v >= 1) c->G = (uint32_t)v;
+  }
+  c->nrep = 16;
+  if (const char *e = getenv("B2P_NREP")) {
+    int v = atoi(e);
+    if (v >= 1 && v <= 1024) c->nrep = (uint32_t)v;
+  }
+  return B2P_OK;
+}
+
+int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
+  if (!out || !g) return set_err(nullptr, B2P_EINVAL, "null argument");
+  *out = nullptr;
+  if (b2p_geom_check(g) != B2P_OK) return set_err(nullptr, B2P_EINVAL, "unsupported geometry");
+  if (device < 0) return set_err(nullptr, B2P_ENODEV, "device index %d < 0", device);
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return set_err(nullptr, B2P_ENODEV, "no HIP device (%s)", hipGetErrorString(e));
+  if (n == 1) device = 0;  // paf_baseband2power.cu:89-90
+  if (device >= n) return set_err(nullptr, B2P_ENODEV, "device %d of %d", device, n);
+
+  b2p_ctx_t *c = new (std::nothrow) b2p_ctx_t();
+  if (!c) return set_err(nullptr, B2P_ENOMEM, "context allocation");
+  c->g = *g;
+  c->device = device;
+  c->mode = g->nbit == 8 ? kI8 : (g->big_endian ? kI16BE : kI16LE);
+  c->nchan = g->nchunk * g->nchan_chunk;
+  c->nout = c->nchan * g->npol_out;
+  c->frame_bytes = b2p_frame_bytes(g);
+  c->block_bytes = b2p_block_bytes(g);
+  int rc;
+  int ncu = 256;
+  auto fail = [&](int code) {
+    if (code != B2P_OK) {
+      snprintf(g_err, sizeof g_err, "%s", c->err);
+      b2p_close(c);
+    }
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(set_err(c, B2P_ENODEV, "hipSetDevice(%d)", device));
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  if ((rc = plan_launch(c, ncu)) != B2P_OK) return fail(rc);
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_err(c, B2P_EHIP, "hipStreamCreate"));
+  c->stream = c->own_stream;
+  const size_t rep_bytes = (size_t)c->nrep * c->nout * sizeof(unsigned long long);
+  if (hipMalloc(&c->d_rep, rep_bytes) != hipSuccess) return fail(set_err(c, B2P_ENOMEM, "hipMalloc replicas"));
+  if (hipMalloc(&c->d_out, (size_t)c->nout * sizeof(float)) != hipSuccess)
+    return fail(set_err(c, B2P_ENOMEM, "hipMalloc out"));
+  if (hipMemsetAsync(c->d_rep, 0, rep_bytes, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return fail(set_err(c, B2P_EHIP, "zero replicas"));
+  *out = c;
+  return B2P_OK;
+}
+
+static void drain_timing(b2p_ctx_t *c) {
+  for (auto &p : c->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      if (p.kind == 0) {
+        c->stats.launches++;
+        c->stats.bytes += p.bytes;
+        c->stats.kernel_ms += ms;
+      } else {
+        c->stats.finalizes++;
+        c->stats.finalize_ms += ms;
+      }
+    }
+    c->ev_pool.push_back(p.a);
+    c->ev_pool.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+int b2p_close(b2p_ctx_t *c) {
+  if (!c) return B2P_EINVAL;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+  drain_timing(c);
+  for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i) {
+    if (c->d_stage[i]) hipFree(c->d_stage[i]);
+    if (c->ev_copied[i]) hipEventDestroy(c->ev_copied[i]);
+    if (c->ev_consumed[i]) hipEventDestroy(c->ev_consumed[i]);
+  }
+  if (c->d_rep) hipFree(c->d_rep);
+  if (c->d_out) hipFree(c->d_out);
+  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+  return B2P_OK;
+}
+
+int b2p_get_info(const b2p_ctx_t *c, b2p_info_t *info) {
+  if (!c || !info) return B2P_EINVAL;
+  info->nchan = c->nchan;
+  info->nout = c->nout;
+  info->frame_bytes = c->frame_bytes;
+  info->block_bytes = c->block_bytes;
+  info->threads = c->B;
+  info->columns = c->NC;
+  info->row_groups = c->G;
+  info->row_vectors = c->S;
+  info->replicas = c->nrep;
+  info->device = (uint32_t)c->device;
+  return B2P_OK;
+}
+
+int b2p_set_stream(b2p_ctx_t *c, void *s) {
+  if (!c) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipStreamSynchronize(c->stream));
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return B2P_OK;
+}
+
+int b2p_register_host(b2p_ctx_t *c, void *base, size_t bytes) {
+  if (!c || !base || !bytes) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipHostRegister(base, bytes, hipHostRegisterDefault));
+  return B2P_OK;
+}
+
+int b2p_unregister_host(b2p_ctx_t *c, void *base) {
+  if (!c || !base) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipHostUnregister(base));
+  return B2P_OK;
+}
+
+static hipEvent_t pool_event(b2p_ctx_t *c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Enqueue one integrate launch over a device span (frame-aligned).
+static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes) {
+  IntegrateArgs a;
+  a.data = (const uint4 *)dev;
+  a.nvec = nbytes / 16;
+  a.S = c->S;
+  a.nrows = (a.nvec + c->S - 1) / c->S;
+  a.B = c->B;
+  a.NC = c->NC;
+  a.G = c->G;
+  a.IV = c->IV;
+  a.nchunk = c->g.nchunk;
+  a.nchan_chunk = c->g.nchan_chunk;
+  a.nout = c->nout;
+  a.nrep = c->nrep;
+  a.rep = c->d_rep;
+  const uint32_t grid = c->NC * c->G;
+  EvPair p{nullptr, nullptr, nbytes, 0};
+  if (c->timing) {
+    if (c->pending.size() >= kTimingRing) drain_timing(c);
+    p.a = pool_event(c);
+    p.b = pool_event(c);
+    if (!p.a || !p.b) return set_err(c, B2P_EHIP, "hipEventCreate");
+    CK(c, hipEventRecord(p.a, c->stream));
+  }
+  CK(c, launch_integrate(a, c->mode, (int)c->g.npol_out, c->Bpad, grid, c->stream));
+  if (c->timing) {
+    CK(c, hipEventRecord(p.b, c->stream));
+    c->pending.push_back(p);
+  }
+  return B2P_OK;
+}
+
+static int ensure_staging(b2p_ctx_t *c) {
+  if (c->d_stage[0]) return B2P_OK;
+  uint64_t want = 256ull << 20;
+  if (const char *e = getenv("B2P_STAGE_MIB")) {
+    long v = atol(e);
+    if (v >= 1 && v <= 16384) want = (uint64_t)v << 20;
+  }
+  uint64_t sb = want / c->frame_bytes * c->frame_bytes;
+  if (sb == 0) sb = c->frame_bytes;
+  c->stage_bytes = sb;
+  for (int i = 0; i < 2; ++i) {
+    if (hipMalloc(&c->d_stage[i], sb) != hipSuccess) return set_err(c, B2P_ENOMEM, "hipMalloc staging");
+    CK(c, hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
+    CK(c, hipEventCreateWithFlags(&c->ev_consumed[i], hipEventDisableTiming));
+  }
+  CK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  for (int i = 0; i < 2; ++i) CK(c, hipEventRecord(c->ev_consumed[i], c->stream));
+  return B2P_OK;
+}
+
+int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
+  if (!c) return B2P_EINVAL;
+  if (nbytes == 0) return B2P_OK;
+  if (!buf) return set_err(c, B2P_EINVAL, "null buffer");
+  if (nbytes % c->frame_bytes)
+    return set_err(c, B2P_ERAGGED, "%zu bytes is not a multiple of the %llu-byte frame", nbytes,
+                   (unsigned long long)c->frame_bytes);
+  const uint64_t samples = nbytes / c->frame_bytes * c->g.nsamp_df;
+  if (c->samples + samples > c->g.nsamp_int)
+    return set_err(c, B2P_EOVERFLOW, "push of %llu samples overflows the %llu-sample integration",
+                   (unsigned long long)samples, (unsigned long long)c->g.nsamp_int);
+  CK(c, hipSetDevice(c->device));
+  int rc;
+  if (is_device) {
+    if ((uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
+    if ((rc = enqueue_span(c, buf, nbytes)) != B2P_OK) return rc;
+  } else {
+    if ((rc = ensure_staging(c)) != B2P_OK) return rc;
+    const uint8_t *h = (const uint8_t *)buf;
+    int last = -1;
+    for (uint64_t off = 0; off < nbytes; off += c->stage_bytes) {
+      const uint64_t n = std::min<uint64_t>(c->stage_bytes, nbytes - off);
+      const int i = (int)(c->stage_next++ & 1);
+      CK(c, hipStreamWaitEvent(c->copy_stream, c->ev_consumed[i], 0));
+      CK(c, hipMemcpyAsync(c->d_stage[i], h + off, n, hipMemcpyHostToDevice, c->copy_stream));
+      CK(c, hipEventRecord(c->ev_copied[i], c->copy_stream));
+      CK(c, hipStreamWaitEvent(c->stream, c->ev_copied[i], 0));
+      if ((rc = enqueue_span(c, c->d_stage[i], n)) != B2P_OK) return rc;
+      CK(c, hipEventRecord(c->ev_consumed[i], c->stream));
+      last = i;
+    }
+    // the caller may release the host span once every copy has landed
+    if (last >= 0) CK(c, hipEventSynchronize(c->ev_copied[last]));
+  }
+  c->samples += samples;
+  return B2P_OK;
+}
+
+uint64_t b2p_samples_pending(const b2p_ctx_t *c) { return c ? c->samples : 0; }
+
+int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
+  if (!c || !out) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  FinalizeArgs f;
+  f.rep = c->d_rep;
+  f.nrep = c->nrep;
+  f.nout = c->nout;
+  f.out = out_is_device ? out : c->d_out;
+  f.mean = c->g.mean;
+  f.nsamp = (double)c->g.nsamp_int;
+  EvPair p{nullptr, nullptr, 0, 1};
+  if (c->timing) {
+    if (c->pending.size() >= kTimingRing) drain_timing(c);
+    p.a = pool_event(c);
+    p.b = pool_event(c);
+    if (!p.a || !p.b) return set_err(c, B2P_EHIP, "hipEventCreate");
+    CK(c, hipEventRecord(p.a, c->stream));
+  }
+  CK(c, launch_finalize(f, c->stream));
+  if (c->timing) {
+    CK(c, hipEventRecord(p.b, c->stream));
+    c->pending.push_back(p);
+  }
+  if (!out_is_device)
+    CK(c, hipMemcpyAsync(out, c->d_out, (size_t)c->nout * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  const uint64_t got = c->samples;
+  c->samples = 0;
+  if (got != c->g.nsamp_int)
+    return set_err(c, B2P_EPARTIAL, "integration had %llu of %llu samples", (unsigned long long)got,
+                   (unsigned long long)c->g.nsamp_int);
+  return B2P_OK;
+}
+
+int b2p_sync(b2p_ctx_t *c) {
+  if (!c) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipStreamSynchronize(c->stream));
+  return B2P_OK;
+}
+
+int b2p_finish(b2p_ctx_t *c, float *out) {
+  int rc = b2p_finish_async(c, out, 0);
+  if (rc != B2P_OK && rc != B2P_EPARTIAL) return rc;
+  int rs = b2p_sync(c);
+  return rs != B2P_OK ? rs : rc;
+}
+
+int b2p_set_timing(b2p_ctx_t *c, int enable) {
+  if (!c) return B2P_EINVAL;
+  c->timing = enable ? 1 : 0;
+  return B2P_OK;
+}
+
+int b2p_get_stats(b2p_ctx_t *c, b2p_stats_t *s) {
+  if (!c || !s) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  drain_timing(c);
+  *s = c->stats;
+  return B2P_OK;
+}
+
+int b2p_reset_stats(b2p_ctx_t *c) {
+  if (!c) return B2P_EINVAL;
+  drain_timing(c);
+  memset(&c->stats, 0, sizeof c->stats);
+  return B2P_OK;
+}
+
+int b2p_fill_synthetic(b2p_ctx_t *c, void *dev, size_t nbytes, uint64_t seed, uint32_t subband,
+                       uint64_t block, uint64_t elem0) {
+  if (!c || !dev) return B2P_EINVAL;
+  if (nbytes % 16 || (uintptr_t)dev % 16) return set_err(c, B2P_EALIGN, "fill needs 16-B multiples");
+  CK(c, hipSetDevice(c->device));
+  FillArgs f;
+  const uint64_t k_sub = splitmix64_host(seed ^ (0xD1B54A32D192ED03ULL * ((uint64_t)subband + 1)));
+  f.key = splitmix64_host(k_sub ^ (0x8CB92BA72F3D8DD7ULL * (block + 1)));
+  f.elem0 = elem0;
+  f.elem_bytes = c->g.nbit / 8;
+  f.big_endian = c->g.big_endian;
+  f.comp = c->g.npol * c->g.ndim;
+  f.nchan_chunk = c->g.nchan_chunk;
+  f.wpc = (uint64_t)c->g.nsamp_df * c->g.nchan_chunk;
+  f.wpf = f.wpc * c->g.nchunk;
+  f.nchan = c->nchan;
+  f.amp = c->g.nbit == 8 ? 35 : 3464;
+  CK(c, launch_fill((uint4 *)dev, nbytes / 16, f, c->stream));
+  return B2P_OK;
+}
+
+int b2p_dev_alloc(b2p_ctx_t *c, void **dev, size_t bytes) {
+  if (!c || !dev) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  if (hipMalloc(dev, bytes ? bytes : 16) != hipSuccess) return set_err(c, B2P_ENOMEM, "hipMalloc %zu", bytes);
+  return B2P_OK;
+}
+
+int b2p_dev_free(b2p_ctx_t *c, void *dev) {
+  if (!c) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipStreamSynchronize(c->stream));
+  if (dev) CK(c, hipFree(dev));
+  return B2P_OK;
+}
+
+int b2p_memcpy(b2p_ctx_t *c, void *dst, const void *src, size_t bytes, int kind) {
+  if (!c || !dst || !src) return B2P_EINVAL;
+  hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice
+                              : (kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+  if (kind < 1 || kind > 3) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipStreamSynchronize(c->stream));
+  CK(c, hipMemcpy(dst, src, bytes, k));
+  return B2P_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// Internal interface between the C-ABI context (b2p_ctx.hip) and the gfx950
+// kernels (b2p_kernels.hip).  Not installed; include/b2p.h is the boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace b2p {
+
+enum Mode : int { kI8 = 0, kI16LE = 1, kI16BE = 2 };
+
+// One launch of the detect+integrate kernel over one pushed span.
+// The span is viewed as rows of S 16-B vectors; workgroup (col, grp) owns
+// the vectors [col*B, col*B+B) of every row in its row range, so each thread
+// sees the same channels in every row and keeps its partial sums in
+// registers (DESIGN.md "integrate kernel").
+struct IntegrateArgs {
+  const uint4 *data;            // span base, 16-B aligned, frame-aligned
+  uint64_t nvec;                // 16-B vectors in the span
+  uint64_t nrows;               // ceil(nvec / S)
+  uint32_t S;                   // vectors per row
+  uint32_t B;                   // active threads per workgroup
+  uint32_t NC;                  // workgroups across a row (S / B, or 1)
+  uint32_t G;                   // row groups
+  uint32_t IV;                  // vectors per chunk (nsamp_df*nchan_chunk/VW)
+  uint32_t nchunk;
+  uint32_t nchan_chunk;
+  uint32_t nout;                // nchan * npol_out
+  uint32_t nrep;                // accumulator replicas
+  unsigned long long *rep;      // [nrep][nout] exact sums
+};
+
+struct FinalizeArgs {
+  unsigned long long *rep;      // zeroed as it is read
+  uint32_t nrep;
+  uint32_t nout;
+  float *out;
+  uint32_t mean;
+  double nsamp;
+};
+
+struct FillArgs {
+  uint64_t key;                 // splitmix key of (seed, subband, block)
+  uint64_t elem0;
+  uint32_t elem_bytes;          // 1 or 2
+  uint32_t big_endian;
+  uint32_t comp;                // npol*ndim
+  uint32_t nchan_chunk;
+  uint64_t wpc;                 // words per chunk (nsamp_df*nchan_chunk)
+  uint64_t wpf;                 // words per frame
+  uint32_t nchan;
+  int32_t amp;
+};
+
+hipError_t launch_integrate(const IntegrateArgs &a, int mode, int npol_out,
+                            uint32_t block_threads, uint32_t grid,
+                            hipStream_t s);
+hipError_t occupancy_integrate(int mode, int npol_out, uint32_t threads,
+                               size_t lds_bytes, int *blocks_per_cu);
+hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s);
+hipError_t launch_fill(uint4 *dst, uint64_t nvec, const FillArgs &f,
+                       hipStream_t s);
+uint64_t splitmix64_host(uint64_t x);
+
+}  // namespace b2p

@@ -1,0 +1,336 @@
+// gfx950 kernels of the baseband->power integrator.
+//
+// Replaces the empty kernel module of the reference (kernel.cu:1-7,
+// kernel.cuh:1-9): unpack -> |X|^2 + |Y|^2 -> 1024x1024-sample time sum
+// (README.md:2, paf_baseband2power.cu:20).
+//
+// The path is a streaming map-reduce at ~1-2 integer ops per byte, bound by
+// HBM read bandwidth (DESIGN.md "roofline"), so the kernel is built around
+// the load stream, not arithmetic:
+//  * every lane issues 16-B global_load_dwordx4 and a wave covers 1 KiB of
+//    contiguous baseband per instruction;
+//  * a lane keeps the same 16-B position inside a row for the whole launch,
+//    so its channels are loop-invariant and its partial sums live in
+//    registers (no LDS traffic in the stream);
+//  * int8 words [X.re X.im Y.re Y.im] are detected with ONE v_dot4c_i32_i8
+//    per word (dot(w, w) = |X|^2 + |Y|^2), accumulated exactly in 32 bits and
+//    widened to 64 bits every 32768 rows;
+//  * int16 big-endian BMF words are byte-swapped per 16-bit lane with one
+//    v_perm_b32 per dword (the BSWAP_64 of cudautil.cuh:118-125, applied to
+//    the halves) and detected with v_dot2c_i32_i16, summed in 64 bits;
+//  * per-workgroup reduction through LDS 64-bit atomics, then one 64-bit
+//    global atomic per touched output into one of nrep replicas (exact
+//    integers: the result does not depend on arrival order).
+#include <hip/hip_runtime.h>
+
+#include "b2p_internal.h"
+
+namespace b2p {
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// rows a lane may accumulate in 32 bits before widening: a row adds at most
+// 4*128^2 = 2^16 per int8 word, so 2^15 rows stay below 2^31.
+constexpr uint32_t kFlushRows = 32768;
+constexpr int kUnroll = 8;
+
+__device__ __forceinline__ uint32_t pol_power16(uint32_t d, bool be) {
+  if (be) d = __builtin_amdgcn_perm(d, d, 0x02030001u);  // swap bytes in each half
+  short2_t s = __builtin_bit_cast(short2_t, d);
+  // re^2 + im^2 <= 2^31: exact as uint32 (the int32 result may read -2^31)
+  return (uint32_t)__builtin_amdgcn_sdot2(s, s, 0, false);
+}
+
+template <int MODE, int NPO>
+struct Acc;
+
+// ---- int8: 4 words per 16-B vector --------------------------------------
+template <int NPO>
+struct Acc8 {
+  unsigned long long tot[4][NPO];
+  uint32_t s[4][NPO];
+  __device__ __forceinline__ void zero_all() {
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int p = 0; p < NPO; ++p) tot[w][p] = 0, s[w][p] = 0;
+  }
+  __device__ __forceinline__ void add(const u32x4 v) {
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (NPO == 1) {
+        s[w][0] = (uint32_t)__builtin_amdgcn_sdot4((int)d[w], (int)d[w], (int)s[w][0], false);
+      } else {
+        // s[w][0] = |X|^2 (bytes 0,1), s[w][1] = |X|^2 + |Y|^2
+        s[w][0] = (uint32_t)__builtin_amdgcn_sdot4((int)(d[w] & 0xffffu), (int)d[w],
+                                                  (int)s[w][0], false);
+        s[w][1] = (uint32_t)__builtin_amdgcn_sdot4((int)d[w], (int)d[w], (int)s[w][1], false);
+      }
+    }
+  }
+  __device__ __forceinline__ void flush() {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (NPO == 1) {
+        tot[w][0] += s[w][0];
+      } else {
+        tot[w][0] += s[w][0];
+        tot[w][1] += s[w][1] - s[w][0];  // |Y|^2, exact mod 2^32
+      }
+#pragma unroll
+      for (int p = 0; p < NPO; ++p) s[w][p] = 0;
+    }
+  }
+  __device__ __forceinline__ unsigned long long get(int w, int p) const { return tot[w][p]; }
+};
+
+// ---- int16: 2 words (4 dwords) per 16-B vector -----------------------------
+template <bool BE, int NPO>
+struct Acc16 {
+  unsigned long long tot[2][NPO];
+  __device__ __forceinline__ void zero_all() {
+#pragma unroll
+    for (int w = 0; w < 2; ++w)
+#pragma unroll
+      for (int p = 0; p < NPO; ++p) tot[w][p] = 0;
+  }
+  __device__ __forceinline__ void add(const u32x4 v) {
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      // BE (BSWAP_64 convention): bytes 4-7 hold X (lanes 0,1), bytes 0-3 Y.
+      // LE: bytes 0-3 hold X, 4-7 Y.
+      const uint32_t p0 = pol_power16(d[2 * w], BE);
+      const uint32_t p1 = pol_power16(d[2 * w + 1], BE);
+      const uint32_t px = BE ? p1 : p0, py = BE ? p0 : p1;
+      if (NPO == 1) {
+        tot[w][0] += (unsigned long long)px + py;
+      } else {
+        tot[w][0] += px;
+        tot[w][1] += py;
+      }
+    }
+  }
+  __device__ __forceinline__ void flush() {}
+  __device__ __forceinline__ unsigned long long get(int w, int p) const { return tot[w][p]; }
+};
+
+template <int NPO> struct Acc<kI8, NPO> : Acc8<NPO> { static constexpr int VW = 4; };
+template <int NPO> struct Acc<kI16LE, NPO> : Acc16<false, NPO> { static constexpr int VW = 2; };
+template <int NPO> struct Acc<kI16BE, NPO> : Acc16<true, NPO> { static constexpr int VW = 2; };
+
+template <int MODE, int NPO>
+__global__ void __launch_bounds__(1024)
+b2p_integrate_kernel(IntegrateArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+  using A = Acc<MODE, NPO>;
+  constexpr int VW = A::VW;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t j = t; j < a.nout; j += blockDim.x) lds[j] = 0;
+
+  const uint32_t col = blockIdx.x % a.NC;
+  const uint32_t grp = blockIdx.x / a.NC;
+  const bool active = t < a.B;
+  const uint32_t pos = col * a.B + t;  // vector position inside a row
+
+  // channels of this lane's VW word slots (fixed for the whole launch)
+  uint32_t ch[VW];
+  {
+    const uint32_t chunk = a.nchunk == 1 ? 0u : pos / a.IV;
+    const uint32_t q = a.nchunk == 1 ? pos : pos % a.IV;
+#pragma unroll
+    for (int w = 0; w < VW; ++w)
+      ch[w] = chunk * a.nchan_chunk + (q * VW + w) % a.nchan_chunk;
+  }
+
+  const u32x4 *data = reinterpret_cast<const u32x4 *>(a.data);
+  A acc;
+  acc.zero_all();
+  const uint64_t r0 = (uint64_t)grp * a.nrows / a.G;
+  const uint64_t r1 = (uint64_t)(grp + 1) * a.nrows / a.G;
+  const uint64_t full = a.nvec / a.S;  // rows with every vector valid
+  const uint64_t rf = r1 < full ? r1 : full;
+  if (active) {
+    uint64_t r = r0;
+    while (r < rf) {
+      const uint64_t rend = (rf - r > kFlushRows) ? r + kFlushRows : rf;
+      // row base is wave-uniform (scalar), the lane offset is loop-invariant
+      for (; r + kUnroll <= rend; r += kUnroll) {
+        u32x4 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const u32x4 *row = data + (r + u) * a.S;
+          v[u] = __builtin_nontemporal_load(row + pos);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) acc.add(v[u]);
+      }
+      for (; r < rend; ++r) acc.add(__builtin_nontemporal_load(data + r * a.S + pos));
+      acc.flush();
+    }
+    // ragged last row (only when the span is not a whole number of rows)
+    for (uint64_t rr = (r0 > rf ? r0 : rf); rr < r1; ++rr) {
+      const uint64_t vi = rr * a.S + pos;
+      if (vi < a.nvec) acc.add(data[vi]);
+    }
+    acc.flush();
+  }
+  __syncthreads();
+  if (active) {
+#pragma unroll
+    for (int w = 0; w < VW; ++w)
+#pragma unroll
+      for (int p = 0; p < NPO; ++p) {
+        const unsigned long long x = acc.get(w, p);
+        if (x) atomicAdd(&lds[ch[w] * NPO + p], x);
+      }
+  }
+  __syncthreads();
+  unsigned long long *rep = a.rep + (uint64_t)(blockIdx.x % a.nrep) * a.nout;
+  for (uint32_t j = t; j < a.nout; j += blockDim.x) {
+    const unsigned long long x = lds[j];
+    if (x) atomicAdd(&rep[j], x);
+  }
+}
+
+// Sum the replicas, emit fp32 with one RNE rounding, zero the replicas.
+// 256 threads = 4 waves per 64 outputs; wave w sums replicas w, w+4, ...
+__global__ void __launch_bounds__(256) b2p_finalize_kernel(FinalizeArgs a) {
+  __shared__ unsigned long long part[4][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t j = blockIdx.x * 64 + lane;
+  unsigned long long s = 0;
+  if (j < a.nout) {
+    for (uint32_t r = w; r < a.nrep; r += 4) {
+      unsigned long long *p = a.rep + (uint64_t)r * a.nout + j;
+      s += *p;
+      *p = 0;
+    }
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && j < a.nout) {
+    const unsigned long long tot = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+    // tot < 2^53: the double is exact, the float conversion is the one RNE
+    const double d = (double)tot;
+    a.out[j] = a.mean ? (float)(d / a.nsamp) : (float)d;
+  }
+}
+
+// ---- synthetic baseband (same generator as oracle/b2p_oracle.c) -----------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int32_t synth_value(const FillArgs &f, uint64_t e) {
+  const uint64_t r = splitmix64(f.key + e);
+  const int64_t gs = (int64_t)(r & 0xffff) + (int64_t)((r >> 16) & 0xffff) +
+                     (int64_t)((r >> 32) & 0xffff) + (int64_t)(r >> 48) - 131070;
+  const uint64_t wf = (e / f.comp) % f.wpf;
+  const uint32_t ch = (uint32_t)((wf / f.wpc) * f.nchan_chunk + wf % f.nchan_chunk);
+  const int64_t amp = (ch == 0 || ch == 7 || ch == f.nchan - 1) ? 2 * f.amp : f.amp;
+  int64_t v = (gs * amp) >> 16;
+  const int64_t lo = f.elem_bytes == 1 ? -128 : -32768, hi = f.elem_bytes == 1 ? 127 : 32767;
+  v = v < lo ? lo : (v > hi ? hi : v);
+  return (int32_t)v;
+}
+
+__global__ void __launch_bounds__(256) b2p_fill_kernel(uint4 *dst, uint64_t nvec, FillArgs f) {
+  for (uint64_t vi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; vi < nvec;
+       vi += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t d[4];
+    if (f.elem_bytes == 1) {
+      const uint64_t e0 = f.elem0 + vi * 16;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          x |= ((uint32_t)(uint8_t)(int8_t)synth_value(f, e0 + 4 * k + b)) << (8 * b);
+        d[k] = x;
+      }
+    } else {
+      const uint64_t e0 = f.elem0 + vi * 8;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          uint32_t u = (uint16_t)(int16_t)synth_value(f, e0 + 2 * k + h);
+          if (f.big_endian) u = ((u & 0xff) << 8) | (u >> 8);
+          x |= u << (16 * h);
+        }
+        d[k] = x;
+      }
+    }
+    dst[vi] = make_uint4(d[0], d[1], d[2], d[3]);
+  }
+}
+
+// ---- launchers --------------------------------------------------------------
+template <int MODE, int NPO>
+static hipError_t launch_t(const IntegrateArgs &a, uint32_t threads, uint32_t grid,
+                           hipStream_t s) {
+  const size_t lds = (size_t)a.nout * sizeof(unsigned long long);
+  hipLaunchKernelGGL((b2p_integrate_kernel<MODE, NPO>), dim3(grid), dim3(threads), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_integrate(const IntegrateArgs &a, int mode, int npol_out,
+                            uint32_t threads, uint32_t grid, hipStream_t s) {
+  switch (mode * 2 + (npol_out - 1)) {
+    case kI8 * 2 + 0: return launch_t<kI8, 1>(a, threads, grid, s);
+    case kI8 * 2 + 1: return launch_t<kI8, 2>(a, threads, grid, s);
+    case kI16LE * 2 + 0: return launch_t<kI16LE, 1>(a, threads, grid, s);
+    case kI16LE * 2 + 1: return launch_t<kI16LE, 2>(a, threads, grid, s);
+    case kI16BE * 2 + 0: return launch_t<kI16BE, 1>(a, threads, grid, s);
+    case kI16BE * 2 + 1: return launch_t<kI16BE, 2>(a, threads, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int MODE, int NPO>
+static hipError_t occ_t(uint32_t threads, size_t lds, int *blocks) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, b2p_integrate_kernel<MODE, NPO>,
+                                                      (int)threads, lds);
+}
+
+hipError_t occupancy_integrate(int mode, int npol_out, uint32_t threads, size_t lds, int *blocks) {
+  switch (mode * 2 + (npol_out - 1)) {
+    case kI8 * 2 + 0: return occ_t<kI8, 1>(threads, lds, blocks);
+    case kI8 * 2 + 1: return occ_t<kI8, 2>(threads, lds, blocks);
+    case kI16LE * 2 + 0: return occ_t<kI16LE, 1>(threads, lds, blocks);
+    case kI16LE * 2 + 1: return occ_t<kI16LE, 2>(threads, lds, blocks);
+    case kI16BE * 2 + 0: return occ_t<kI16BE, 1>(threads, lds, blocks);
+    case kI16BE * 2 + 1: return occ_t<kI16BE, 2>(threads, lds, blocks);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s) {
+  const uint32_t grid = (a.nout + 63) / 64;
+  hipLaunchKernelGGL(b2p_finalize_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(uint4 *dst, uint64_t nvec, const FillArgs &f, hipStream_t s) {
+  uint64_t blocks = (nvec + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(b2p_fill_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, dst, nvec, f);
+  return hipGetLastError();
+}
+
+uint64_t splitmix64_host(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+}  // namespace b2p

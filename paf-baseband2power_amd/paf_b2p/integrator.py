@@ -1,0 +1,164 @@
+"""Python host-side mirror of the integrator's C ABI (include/b2p.h).
+
+``Integrator`` is the per-sub-band object the reference intended to build in
+baseband2power.cu (empty, baseband2power.cu:1-16) around conf_t
+(baseband2power.cuh:18-23): open on a device, push ring blocks, emit one
+power spectrum per 1024x1024-sample integration (README.md:2).  Every call
+goes through libpafb2p.so; errors raise ``B2PError`` with the library's
+status code (the reference printed and called exit(-1), cudautil.cuh:29-41).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from .geometry import make_geom
+
+
+@dataclass
+class DeviceBuffer:
+    """Device memory owned by an Integrator (hipMalloc through the C ABI)."""
+    ptr: int
+    nbytes: int
+    owner: "Integrator"
+
+    def free(self) -> None:
+        if self.ptr:
+            L.check(L.lib().b2p_dev_free(self.owner._ctx, C.c_void_p(self.ptr)), self.owner._ctx)
+            self.ptr = 0
+
+
+class Integrator:
+    def __init__(self, geom=None, device: int = 0, **geom_kw):
+        g = geom if isinstance(geom, L.Geom) else make_geom(**(geom or {}), **geom_kw)
+        self.geom = g
+        self._ctx = C.c_void_p()
+        lib = L.lib()
+        L.check(lib.b2p_open(C.byref(self._ctx), C.byref(g), device), None)
+        info = L.Info()
+        L.check(lib.b2p_get_info(self._ctx, C.byref(info)), self._ctx)
+        self.info = info
+        self.nout = info.nout
+        self.frame_bytes = info.frame_bytes
+        self.block_bytes = info.block_bytes
+
+    # ---- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            L.check(L.lib().b2p_close(self._ctx))
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- hot path ------------------------------------------------------------
+    def push(self, buf, nbytes: int | None = None, is_device: bool | None = None) -> None:
+        """Accumulate a whole number of frames.  ``buf``: numpy uint8 array
+        (host), ``DeviceBuffer`` / ``(DeviceBuffer, offset, nbytes)`` (device),
+        or a raw pointer int with ``nbytes`` and ``is_device``."""
+        ptr, n, dev = self._span(buf, nbytes, is_device)
+        L.check(L.lib().b2p_push(self._ctx, C.c_void_p(ptr), n, int(dev)), self._ctx)
+
+    def finish(self, allow_partial: bool = False) -> np.ndarray:
+        out = np.zeros(self.nout, dtype=np.float32)
+        rc = L.lib().b2p_finish(self._ctx, out.ctypes.data_as(C.c_void_p))
+        L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,) if allow_partial else ())
+        return out
+
+    def finish_async(self, out_ptr: int, out_is_device: bool) -> int:
+        rc = L.lib().b2p_finish_async(self._ctx, C.c_void_p(out_ptr), int(out_is_device))
+        return L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,))
+
+    def sync(self) -> None:
+        L.check(L.lib().b2p_sync(self._ctx), self._ctx)
+
+    def samples_pending(self) -> int:
+        return int(L.lib().b2p_samples_pending(self._ctx))
+
+    def set_stream(self, hip_stream: int | None) -> None:
+        L.check(L.lib().b2p_set_stream(self._ctx, C.c_void_p(hip_stream or 0)), self._ctx)
+
+    # ---- host memory -----------------------------------------------------------
+    def register_host(self, arr: np.ndarray) -> None:
+        L.check(L.lib().b2p_register_host(self._ctx, C.c_void_p(arr.ctypes.data), arr.nbytes),
+                self._ctx)
+
+    def unregister_host(self, arr: np.ndarray) -> None:
+        L.check(L.lib().b2p_unregister_host(self._ctx, C.c_void_p(arr.ctypes.data)), self._ctx)
+
+    # ---- device buffers / synthetic data ----------------------------------------
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        p = C.c_void_p()
+        L.check(L.lib().b2p_dev_alloc(self._ctx, C.byref(p), nbytes), self._ctx)
+        return DeviceBuffer(p.value or 0, nbytes, self)
+
+    def upload(self, arr: np.ndarray) -> DeviceBuffer:
+        arr = np.ascontiguousarray(arr)
+        d = self.alloc(max(arr.nbytes, 16))
+        if arr.nbytes:
+            L.check(L.lib().b2p_memcpy(self._ctx, C.c_void_p(d.ptr), C.c_void_p(arr.ctypes.data),
+                                       arr.nbytes, 1), self._ctx)
+        d.nbytes = arr.nbytes
+        return d
+
+    def download(self, d: DeviceBuffer, nbytes: int | None = None, offset: int = 0) -> np.ndarray:
+        n = d.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            L.check(L.lib().b2p_memcpy(self._ctx, C.c_void_p(out.ctypes.data),
+                                       C.c_void_p(d.ptr + offset), n, 2), self._ctx)
+        return out
+
+    def fill_synthetic(self, d: DeviceBuffer, seed: int, subband: int, block: int,
+                       nbytes: int | None = None, offset: int = 0, elem0: int = 0) -> None:
+        n = d.nbytes - offset if nbytes is None else nbytes
+        L.check(L.lib().b2p_fill_synthetic(self._ctx, C.c_void_p(d.ptr + offset), n, seed, subband,
+                                           block, elem0), self._ctx)
+
+    # ---- measurement -------------------------------------------------------------
+    def set_timing(self, on: bool) -> None:
+        L.check(L.lib().b2p_set_timing(self._ctx, int(on)), self._ctx)
+
+    def stats(self) -> dict:
+        s = L.Stats()
+        L.check(L.lib().b2p_get_stats(self._ctx, C.byref(s)), self._ctx)
+        return {"launches": s.launches, "bytes": s.bytes, "kernel_ms": s.kernel_ms,
+                "finalize_ms": s.finalize_ms, "finalizes": s.finalizes}
+
+    def reset_stats(self) -> None:
+        L.check(L.lib().b2p_reset_stats(self._ctx), self._ctx)
+
+    # ---- helpers -------------------------------------------------------------------
+    def _span(self, buf, nbytes, is_device):
+        if isinstance(buf, DeviceBuffer):
+            return buf.ptr, buf.nbytes if nbytes is None else nbytes, True
+        if isinstance(buf, tuple):
+            d, off, n = buf
+            return d.ptr + off, n, True
+        if isinstance(buf, np.ndarray):
+            if not buf.flags.c_contiguous:
+                raise ValueError("host span must be contiguous")
+            return buf.ctypes.data, buf.nbytes if nbytes is None else nbytes, False
+        if isinstance(buf, int):
+            if nbytes is None or is_device is None:
+                raise ValueError("raw pointer needs nbytes and is_device")
+            return buf, nbytes, is_device
+        raise TypeError(f"unsupported span type {type(buf)}")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = L.lib().b2p_device_count(C.byref(n))
+    return n.value if rc == L.B2P_OK else 0

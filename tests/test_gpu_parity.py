@@ -1,0 +1,261 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bar: bit-identical fp32 output (exact integer accumulate, one RNE rounding).
+Small cases compare with the committed fixtures and with the oracle on the
+same seeded inputs; full BASELINE sizes compare with the multi-threaded C
+oracle on the downloaded block and through size-independent properties
+(chunking/order invariance, determinism, back-to-back integrations).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+import paf_b2p
+from conftest import golden_geom, load_golden
+from paf_b2p import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+SEED = 20181105
+
+
+def to_b2p(g: npo.Geom) -> L.Geom:
+    return paf_b2p.make_geom(**g.asdict())
+
+
+def gpu_power(g: npo.Geom, buf: np.ndarray, splits=None, host=False, register=False,
+              env=None) -> np.ndarray:
+    old = {}
+    for k, v in (env or {}).items():
+        old[k] = os.environ.get(k)
+        os.environ[k] = str(v)
+    try:
+        with paf_b2p.Integrator(to_b2p(g), device=0) as it:
+            bounds = [0] + list(splits or []) + [buf.size]
+            if host:
+                hb = np.ascontiguousarray(buf)
+                if register and hb.nbytes:
+                    it.register_host(hb)
+                for a, b in zip(bounds[:-1], bounds[1:]):
+                    it.push(hb[a:b])
+                if register and hb.nbytes:
+                    it.unregister_host(hb)
+            else:
+                d = it.upload(buf)
+                for a, b in zip(bounds[:-1], bounds[1:]):
+                    it.push((d, a, b - a))
+                out = it.finish(allow_partial=True)
+                d.free()
+                return out
+            return it.finish(allow_partial=True)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def same_bits(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32),
+                          np.asarray(b, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["bmf_small", "int8_256", "int16le_48"])
+@pytest.mark.parametrize("npol_out", [1, 2])
+@pytest.mark.parametrize("mean", [0, 1])
+def test_golden_fixtures(gpu, name, npol_out, mean):
+    d = load_golden(name)
+    g = golden_geom(d, npol_out=npol_out, mean=mean)
+    out = gpu_power(g, d["input"])
+    assert same_bits(out, d[f"power_p{npol_out}_m{mean}"])
+
+
+@pytest.mark.parametrize("name", ["bmf_small", "int8_256", "int16le_48"])
+def test_golden_host_push(gpu, name):
+    d = load_golden(name)
+    g = golden_geom(d)
+    fb = g.frame_bytes
+    nf = d["input"].size // fb
+    splits = [fb * (nf // 3), fb * (2 * nf // 3)]
+    assert same_bits(gpu_power(g, d["input"], host=True), d["power_p1_m0"])
+    assert same_bits(gpu_power(g, d["input"], host=True, register=True, splits=splits),
+                     d["power_p1_m0"])
+
+
+# launch-shape branches of plan_launch(): NC=1 with whole waves, partial last
+# wave, multi-column frames, non-64-multiple workgroup
+GEOMS = {
+    "int8_256": npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=4096),
+    "int8_1024": npo.Geom(nbit=8, nchan_chunk=1024, nsamp_int=2048),
+    "int16le_336": npo.Geom(nbit=16, nchan_chunk=336, nsamp_int=1024),        # B = 1008
+    "bmf_8": npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                      nsamp_int=128 * 8),                                      # NC = 21
+    "bmf_3chunk": npo.Geom(nbit=16, big_endian=1, nchunk=3, nsamp_df=128, nchan_chunk=7,
+                           nsamp_int=128 * 40),                                # B = 448
+    "int8_odd": npo.Geom(nbit=8, nchunk=11, nsamp_df=4, nchan_chunk=99,
+                         nsamp_int=4 * 64),                                    # B = 363
+    "int8_3ch": npo.Geom(nbit=8, nchunk=1, nsamp_df=4, nchan_chunk=3, nsamp_int=4 * 999),
+    "int16be_5x3": npo.Geom(nbit=16, big_endian=1, nchunk=5, nsamp_df=16, nchan_chunk=3,
+                            nsamp_int=16 * 77),
+}
+
+
+@pytest.mark.parametrize("name", sorted(GEOMS))
+@pytest.mark.parametrize("npol_out", [1, 2])
+def test_layouts_vs_oracle(gpu, name, npol_out):
+    g = npo.Geom(**{**GEOMS[name].asdict(), "npol_out": npol_out})
+    buf = npo.fill_synthetic(g, g.block_bytes, SEED, 5, 7)
+    assert same_bits(gpu_power(g, buf), npo.power(g, buf))
+
+
+@pytest.mark.parametrize("name", sorted(GEOMS))
+def test_chunked_pushes_equal_single(gpu, name):
+    g = GEOMS[name]
+    buf = co.fill_synthetic(g, g.block_bytes, SEED, 1, 2)
+    nf = g.block_bytes // g.frame_bytes
+    rng = np.random.default_rng(nf)
+    cuts = sorted(set(int(x) * g.frame_bytes for x in rng.integers(1, nf, size=min(5, nf - 1))))
+    whole = gpu_power(g, buf)
+    assert same_bits(gpu_power(g, buf, splits=cuts), whole)
+    assert same_bits(whole, co.power(g, buf))
+
+
+@pytest.mark.parametrize("name", sorted(GEOMS))
+def test_synthetic_generator_matches_oracle(gpu, name):
+    g = GEOMS[name]
+    n = min(g.block_bytes, 1 << 20) // 16 * 16
+    eb = g.nbit // 8
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        d = it.alloc(n)
+        for elem0 in (0, 16 // eb * 12345):
+            it.fill_synthetic(d, SEED, 3, 11, elem0=elem0)
+            assert np.array_equal(it.download(d), co.fill_synthetic(g, n, SEED, 3, 11, elem0))
+        d.free()
+
+
+def test_extreme_int8_long_lane_runs(gpu):
+    # -128 everywhere, one workgroup row-group => every lane integrates all
+    # 65536 rows: exercises the 32768-row widening and uint32 wrap (2^32/lane)
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 20, npol_out=2)
+    buf = np.full(g.block_bytes, 0x80, dtype=np.uint8)
+    out = gpu_power(g, buf, env={"B2P_ROW_GROUPS": 1})
+    assert np.all(out == np.float32((1 << 20) * 2 * 16384))
+    out1 = gpu_power(npo.Geom(**{**g.asdict(), "npol_out": 1}), buf, env={"B2P_ROW_GROUPS": 2})
+    assert np.all(out1 == np.float32((1 << 20) * 4 * 16384))
+
+
+def test_extreme_int16_be_full_bmf_block(gpu):
+    # every component -32768 over a full 2.625 GiB BMF integration: 2^52/chan
+    g = npo.BMF
+    buf = np.tile(np.array([0x80, 0x00], dtype=np.uint8), g.block_bytes // 2)
+    out = gpu_power(g, buf)
+    assert np.all(out == np.float32(2.0 ** 52))
+    del buf
+
+
+def test_full_config2_block_vs_c_oracle(gpu):
+    # BASELINE configs[1]: 256 ch x 2 pol int8, 1024x1024 samples (1 GiB)
+    for npol_out in (1, 2):
+        g = npo.Geom(nbit=8, nchan_chunk=256, npol_out=npol_out)
+        with paf_b2p.Integrator(to_b2p(g)) as it:
+            d = it.alloc(g.block_bytes)
+            it.fill_synthetic(d, SEED, 0, 0)
+            it.push(d)
+            out = it.finish()
+            host = it.download(d)
+            d.free()
+        assert same_bits(out, co.power(g, host, nthreads=16))
+
+
+def test_full_bmf_block_vs_c_oracle(gpu):
+    # reference-native: 8192 DF x 48 chunks x 7168 B = 2818572288 B
+    g = npo.BMF
+    with paf_b2p.Integrator(paf_b2p.bmf_geom()) as it:
+        d = it.alloc(g.block_bytes)
+        it.fill_synthetic(d, SEED, 0, 1)
+        it.push(d)
+        out = it.finish()
+        host = it.download(d)
+        d.free()
+    assert out.shape == (336,)
+    assert same_bits(out, co.power(g, host, nthreads=16))
+
+
+def test_full_1024ch_properties(gpu):
+    # configs 3/5 layout at full size: push order / chunking invariance and
+    # run-to-run determinism (exact integer sums), plus two back-to-back
+    # integrations on one context
+    g = paf_b2p.generic_geom(1024)
+    bb = paf_b2p.block_bytes(g)
+    with paf_b2p.Integrator(g) as it:
+        d = it.alloc(bb)
+        it.fill_synthetic(d, SEED, 4, 0)
+        it.push(d)
+        whole = it.finish()
+        half = bb // 2
+        it.push((d, half, bb - half))
+        it.push((d, 0, half))
+        rev = it.finish()
+        it.push(d)
+        again = it.finish()
+        sample = it.download(d, nbytes=64 << 20)
+        d.free()
+    assert same_bits(whole, rev) and same_bits(whole, again)
+    # the first 64 MiB alone, against the oracle
+    gs = npo.Geom(nbit=8, nchan_chunk=1024, nsamp_int=(64 << 20) // 4096)
+    with paf_b2p.Integrator(to_b2p(gs)) as it2:
+        dd = it2.upload(sample)
+        it2.push(dd)
+        part = it2.finish()
+        dd.free()
+    assert same_bits(part, co.power(gs, sample, nthreads=16))
+
+
+def test_error_codes(gpu):
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=64)
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        d = it.alloc(g.block_bytes + 64)
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.push((d, 0, g.frame_bytes + 16))
+        assert e.value.code == L.B2P_ERAGGED
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.push((d, 0, g.block_bytes + g.frame_bytes))
+        assert e.value.code == L.B2P_EOVERFLOW
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.push((d, 8, g.frame_bytes))
+        assert e.value.code == L.B2P_EALIGN
+        it.push((d, 0, 0))  # empty span: no-op
+        assert it.samples_pending() == 0
+        it.fill_synthetic(d, SEED, 0, 0, nbytes=g.block_bytes)
+        it.push((d, 0, g.frame_bytes * 10))
+        assert it.samples_pending() == 10
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.finish()
+        assert e.value.code == L.B2P_EPARTIAL
+        # partial result is still emitted, and the context is reset
+        it.push((d, 0, g.frame_bytes * 10))
+        part = it.finish(allow_partial=True)
+        buf = it.download(d, nbytes=g.frame_bytes * 10)
+        gp = npo.Geom(**{**g.asdict(), "nsamp_int": 10})
+        assert same_bits(part, npo.power(gp, buf))
+        assert it.samples_pending() == 0
+        d.free()
+
+
+def test_empty_integration_is_zero(gpu):
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=64)
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        out = it.finish(allow_partial=True)
+    assert np.all(out == 0)
+
+
+def test_device_index_fallback(gpu):
+    # paf_baseband2power.cu:89-90: with one visible device any index maps to 0
+    if paf_b2p.device_count() != 1:
+        pytest.skip("more than one device visible")
+    with paf_b2p.Integrator(paf_b2p.generic_geom(256), device=5) as it:
+        assert it.info.device == 0
