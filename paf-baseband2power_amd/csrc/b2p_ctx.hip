@@ -369,6 +369,7 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes) {
   a.NC = c->NC;
   a.G = c->G;
   a.IV = c->IV;
+  a.FV = c->FV;
   a.nchunk = c->g.nchunk;
   a.nchan_chunk = c->g.nchan_chunk;
   a.nout = c->nout;

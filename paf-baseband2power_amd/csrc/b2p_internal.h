@@ -23,6 +23,7 @@ struct IntegrateArgs {
   uint32_t NC;                  // workgroups across a row (S / B, or 1)
   uint32_t G;                   // row groups
   uint32_t IV;                  // vectors per chunk (nsamp_df*nchan_chunk/VW)
+  uint32_t FV;                  // vectors per frame (nchunk*IV)
   uint32_t nchunk;
   uint32_t nchan_chunk;
   uint32_t nout;                // nchan * npol_out

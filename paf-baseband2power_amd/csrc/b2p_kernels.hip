@@ -138,8 +138,10 @@ b2p_integrate_kernel(IntegrateArgs a) {
   // channels of this lane's VW word slots (fixed for the whole launch)
   uint32_t ch[VW];
   {
-    const uint32_t chunk = a.nchunk == 1 ? 0u : pos / a.IV;
-    const uint32_t q = a.nchunk == 1 ? pos : pos % a.IV;
+    // a row may hold several frames (B a multiple of the frame): fold first
+    const uint32_t fpos = a.nchunk == 1 ? pos : pos % a.FV;
+    const uint32_t chunk = a.nchunk == 1 ? 0u : fpos / a.IV;
+    const uint32_t q = a.nchunk == 1 ? pos : fpos % a.IV;
 #pragma unroll
     for (int w = 0; w < VW; ++w)
       ch[w] = chunk * a.nchan_chunk + (q * VW + w) % a.nchan_chunk;

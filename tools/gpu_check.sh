@@ -1,0 +1,43 @@
+#!/bin/bash
+# One GPU-box session: smoke -> gpu tests -> bench -> rocprofv3 kernel trace.
+# Each GPU step has its own time limit; a fault/abort/timeout (exit other
+# than 0 or 1) ends the script at once -- nothing further touches the GPU.
+#   usage: tools/gpu_check.sh [steps...]   steps: smoke tests bench prof pmc
+cd "$(dirname "$0")/.." || exit 2
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+STEPS=${*:-smoke tests bench prof}
+
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "[$(date +%T)] $name: $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name exit $rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping: $name ended with $rc" | tee -a "$OUT/steps.log"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -q -rf ;;
+    bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
+    bench5) run bench_c5 600 python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
+    benchbmf) run bench_bmf 600 python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
+    bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
+            -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 ;;
+    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
+            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 &&
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
+            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "all steps done" | tee -a "$OUT/steps.log"

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output for the integrate kernel into profiles/.
+
+  tools/pmc_summary.py --config c2 --fetch gpurun_out/pmc_fetch/run_counter_collection.csv \
+      --write gpurun_out/pmc_write/run_counter_collection.csv \
+      --stats gpurun_out/prof/run_kernel_stats.csv --round r01
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE come from separate --pmc passes (they do not fit one TCC pass),
+are in KiB, and FETCH_SIZE reports exactly half the bytes of a wide
+coalesced streaming read on gfx950, so it is doubled.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "b2p_integrate_kernel"
+
+
+def counter(path, name):
+    vals = []
+    for row in csv.DictReader(open(path)):
+        if KERNEL in row["Kernel_Name"] and row["Counter_Name"] == name:
+            vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--stats")
+    ap.add_argument("--round", default="r01")
+    ap.add_argument("--algorithmic-bytes", type=int, default=0)
+    a = ap.parse_args()
+    f = counter(a.fetch, "FETCH_SIZE")
+    w = counter(a.write, "WRITE_SIZE")
+    fetch_kib, write_kib = statistics.median(f), statistics.median(w)
+    hbm = int(fetch_kib * 1024 * 2 + write_kib * 1024)
+    out = {
+        "kernel": KERNEL,
+        "config": a.config,
+        "launches_measured": len(f),
+        "fetch_size_kib_median": fetch_kib,
+        "write_size_kib_median": write_kib,
+        "correction": "FETCH_SIZE x2 (gfx950 wide-stream under-count, MI355X_MICROARCH.md HBM)",
+        "hbm_bytes_per_launch": hbm,
+        "algorithmic_bytes_per_launch": a.algorithmic_bytes or None,
+        "traffic_over_algorithmic": round(hbm / a.algorithmic_bytes, 4) if a.algorithmic_bytes else None,
+        "source": [os.path.relpath(a.fetch, REPO), os.path.relpath(a.write, REPO)],
+    }
+    os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
+    json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{a.config}.json"), "w"), indent=1)
+    shutil.copy(a.fetch, os.path.join(REPO, "profiles", f"{a.round}_{a.config}_pmc_fetch.csv"))
+    shutil.copy(a.write, os.path.join(REPO, "profiles", f"{a.round}_{a.config}_pmc_write.csv"))
+    if a.stats:
+        shutil.copy(a.stats, os.path.join(REPO, "profiles", f"{a.round}_{a.config}_kernel_stats.csv"))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
