@@ -34,6 +34,7 @@ import torch  # noqa: E402  (first: one HIP runtime per process, see paf_b2p/_li
 import torch.distributed as dist  # noqa: E402
 
 import paf_b2p  # noqa: E402
+from paf_b2p import distributed as D  # noqa: E402
 from paf_b2p.geometry import CONFIGS, samples_per_block  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
@@ -49,6 +50,10 @@ def parse():
     ap.add_argument("--config", default="c2", choices=["c2", "c5", "bmf", "c3"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse N ranks on one GPU (spectra gathered on the host)")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="separate finalize launch per integration (b2p_push + b2p_finish_async)")
     return ap.parse_args()
 
 
@@ -94,27 +99,24 @@ def cpu_baseline(geom, seconds: float, threads: int):
 
 def main():
     a = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = D.env_ranks()
     n_gpus = max(world, 1)
     cfg = CONFIGS[a.config]
     geom = cfg["geom"]()
+    rccl = world > 1 and a.dist_backend == "nccl"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
+        D.init(a.dist_backend, local)
+    subband = D.subband_of(rank)
+    # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
     it = paf_b2p.Integrator(geom, device=local)
     nout, bb = it.nout, it.block_bytes
     spb = samples_per_block(geom)
 
-    if world > 1:
-        # finalize writes into torch memory on torch's stream so the gather
-        # is ordered after it (one stream, no host sync inside the loop)
-        it.set_stream(torch.cuda.current_stream().cuda_stream)
+    if rccl:
+        # finalize writes the K spectra straight into torch device memory;
+        # the gather runs after one it.sync() at the end of the timed loop
         out_t = torch.zeros((a.steps, nout), dtype=torch.float32, device="cuda")
         out_ptr = out_t.data_ptr()
-        gather_t = torch.zeros((world, a.steps, nout), dtype=torch.float32, device="cuda")
     else:
         out_buf = it.alloc(max(a.steps, 1) * nout * 4)
         out_ptr = out_buf.ptr
@@ -125,7 +127,7 @@ def main():
         import numpy as np
         hb = np.empty(bb, dtype=np.uint8)
         d = it.alloc(bb)
-        it.fill_synthetic(d, SEED, rank, 0)
+        it.fill_synthetic(d, SEED, subband, 0)
         hb[:] = it.download(d)
         d.free()
         it.register_host(hb)
@@ -133,42 +135,49 @@ def main():
     else:
         for b in range(NBLOCKS):
             d = it.alloc(bb)
-            it.fill_synthetic(d, SEED, rank, b)
+            it.fill_synthetic(d, SEED, subband, b)
             blocks.append(d)
     it.sync()
 
     def step(k, out_row):
-        it.push(blocks[k % len(blocks)])
-        it.finish_async(out_ptr + out_row * nout * 4, True) if out_row is not None else \
-            it.finish_async(out_ptr, True)
+        dst = out_ptr + (out_row or 0) * nout * 4
+        if a.no_fuse or host_mode:  # push + separate finalize launch
+            it.push(blocks[k % len(blocks)])
+            it.finish_async(dst, True)
+        else:  # one launch per integration, the last workgroup emits the spectrum
+            it.integrate(blocks[k % len(blocks)], dst, True)
 
     for w in range(a.warmup):
         step(w, None)
     it.sync()
     if world > 1:
-        torch.cuda.synchronize()
+        if rccl:
+            torch.cuda.synchronize()
         dist.barrier()
 
     it.reset_stats()
-    it.set_timing(True)
+    # one event pair on the integrator's stream around the K launches (per-
+    # launch events would put a few us of event plumbing between kernels)
+    it.set_timing(2)
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(a.warmup + k, k)
-    if world > 1:
-        dist.all_gather_into_tensor(gather_t.view(world * a.steps, nout), out_t)
-        torch.cuda.synchronize()
+    it.set_timing(0)  # records the closing event right behind the last launch
     it.sync()
+    if rccl:
+        gathered = D.gather_spectra(out_t)  # RCCL all-gather of K x nout fp32
+        torch.cuda.synchronize()
+    elif world > 1:
+        host = it.download(out_buf, nbytes=a.steps * nout * 4).view("float32").reshape(a.steps, nout)
+        gathered = D.gather_spectra(torch.from_numpy(host.copy()))
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    it.set_timing(False)
     st = it.stats()
 
-    el_max = el
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_max = float(t.item())
+    el_max = D.max_over_ranks(el, "cuda" if rccl else "cpu") if world > 1 else el
+    if world > 1 and rank == 0:
+        assert len(gathered) == world and all(g.shape == (a.steps, nout) for g in gathered)
 
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
@@ -176,7 +185,7 @@ def main():
     traffic, traffic_src = pmc_traffic(a.config)
 
     if rank == 0:
-        value = n_gpus * a.steps * spb / el_max / 1e6
+        value = D.aggregate_rate(n_gpus, a.steps, spb, el_max)
         res = {
             "metric": "baseband Msamples/s integrated + % HBM-read roofline, 1024x1024 accum",
             "value": round(value, 1),
@@ -200,10 +209,12 @@ def main():
                 "bytes_per_integration": int(bb),
                 "input": "pinned host buffer, H2D overlapped (PCIe-inclusive)" if host_mode
                          else f"HBM-resident, {NBLOCKS} rotating blocks",
-                "parallelism": f"sub-band sharding x{n_gpus}" + (", RCCL all-gather of spectra"
-                                                                   if world > 1 else ""),
+                "parallelism": f"sub-band sharding x{n_gpus}" + (
+                    (", RCCL all-gather of spectra" if rccl else ", gloo gather (rehearsal)")
+                    if world > 1 else ""),
                 "launch": {"threads": it.info.threads, "columns": it.info.columns,
-                           "row_groups": it.info.row_groups, "replicas": it.info.replicas},
+                           "row_groups": it.info.row_groups, "replicas": it.info.replicas,
+                           "unroll": it.info.unroll, "nt_loads": bool(it.info.nontemporal)},
             },
             "roofline": {
                 "bound": "hbm",
@@ -216,7 +227,10 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "avg_launch_us": round(kern_avg_s * 1e6, 2),
-                "finalize_avg_us": round(st["finalize_ms"] / max(st["finalizes"], 1) * 1e3, 2),
+                "timing": "HIP events on the integrator stream bracketing the timed launches "
+                          "(region / launches: gaps and finalizes included, an upper bound)",
+                "finalize_avg_us": (round(st["finalize_ms"] / st["finalizes"] * 1e3, 2)
+                                    if st["finalizes"] else "fused into the integrate launch"),
             },
             "cpu_baseline": None,
         }

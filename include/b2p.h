@@ -89,6 +89,8 @@ typedef struct b2p_info {
   uint32_t row_vectors;  /* 16-B vectors per row                    */
   uint32_t replicas;     /* accumulator replicas                    */
   uint32_t device;
+  uint32_t unroll;       /* rows in flight per lane                 */
+  uint32_t nontemporal;  /* 1 if the stream uses nt loads           */
 } b2p_info_t;
 
 /* Kernel timing collected with HIP events on the context's stream. */
@@ -152,11 +154,27 @@ int b2p_finish(b2p_ctx_t *ctx, float *out);
  * memory; valid after b2p_sync(). */
 int b2p_finish_async(b2p_ctx_t *ctx, float *out, int out_is_device);
 int b2p_sync(b2p_ctx_t *ctx);
+/* One whole integration in one call: push exactly block_bytes and emit it,
+ * enqueued (out valid after b2p_sync()).  For a device span this is ONE
+ * kernel launch -- the last workgroup to finish writes the spectrum -- so
+ * no separate finalize launch; a host span falls back to b2p_push +
+ * b2p_finish_async.  Requires no pending push.  Same output bits as the
+ * push/finish pair. */
+int b2p_integrate(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device, float *out,
+                  int out_is_device);
 /* Number of samples pushed into the current integration. */
 uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
 
-/* ---- measurement ---- */
-int b2p_set_timing(b2p_ctx_t *ctx, int enable);
+/* ---- measurement ----
+ * mode 1: every integrate / finalize launch carries start/stop events on
+ *   its own dispatch packet (hipExtLaunchKernel) -> exact per-launch times;
+ *   the event plumbing costs a few us between launches.
+ * mode 2: one event pair on the context's stream brackets every launch
+ *   between set_timing(ctx, 2) and set_timing(ctx, 0); kernel_ms is the
+ *   region's elapsed time (inter-launch gaps and finalizes included), i.e.
+ *   an upper bound of the summed launch durations, with no per-launch cost.
+ * mode 0: off (closes a mode-2 region). */
+int b2p_set_timing(b2p_ctx_t *ctx, int mode);
 int b2p_get_stats(b2p_ctx_t *ctx, b2p_stats_t *stats); /* synchronises */
 int b2p_reset_stats(b2p_ctx_t *ctx);
 

@@ -37,6 +37,7 @@ struct b2p_ctx {
   b2p_geom_t g;
   int device = 0;
   int mode = kI8;
+  KernelChoice kc{};
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;
@@ -46,7 +47,11 @@ struct b2p_ctx {
   uint32_t nchan = 0, nout = 0, nrep = 0;
   uint64_t frame_bytes = 0, block_bytes = 0;
   unsigned long long *d_rep = nullptr;
+  uint32_t *d_ticket = nullptr;  // arrival counter of the in-launch finalize
   float *d_out = nullptr;
+  uint32_t interleave = 0;
+  int fuse = 0;  // b2p_integrate: finalize in the last workgroup (1) or a
+                 // separate launch (0, measured faster: DESIGN.md)
   // host-buffer staging (double buffered)
   uint8_t *d_stage[2] = {nullptr, nullptr};
   uint64_t stage_bytes = 0;
@@ -54,8 +59,11 @@ struct b2p_ctx {
   hipEvent_t ev_consumed[2] = {nullptr, nullptr};
   uint32_t stage_next = 0;
   uint64_t samples = 0;
-  // timing
+  // timing: 1 = per-launch dispatch-packet events, 2 = one event pair
+  // around a region of launches (no per-launch packets)
   int timing = 0;
+  hipEvent_t region_a = nullptr, region_b = nullptr;
+  uint64_t region_launches = 0, region_bytes = 0, region_finalizes = 0;
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> ev_pool;
   b2p_stats_t stats{};
@@ -176,7 +184,7 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   c->FV = g->nchunk * c->IV;
   const uint32_t P = g->nchan_chunk / gcd_u(g->nchan_chunk, c->VW);
   c->CP = g->nchunk == 1 ? P : c->FV;
-  uint32_t maxT = 1024;
+  uint32_t maxT = g->nbit == 8 ? 512 : 256;
   if (const char *e = getenv("B2P_MAX_THREADS")) {
     int v = atoi(e);
     if (v >= 64 && v <= 1024) maxT = (uint32_t)v;
@@ -199,12 +207,9 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
     c->NC = c->CP / c->B;
   }
   c->Bpad = (c->B + 63) / 64 * 64;
-  // one resident wave of workgroups: as many per CU as registers/LDS admit
-  int occ = 0;
-  const size_t lds = (size_t)c->nout * sizeof(unsigned long long);
-  if (occupancy_integrate(c->mode, (int)g->npol_out, c->Bpad, lds, &occ) != hipSuccess || occ < 1)
-    occ = 1;
-  uint32_t per_cu = (uint32_t)occ;
+  // one workgroup per CU: with ~32 KiB of loads in flight per CU more
+  // resident waves only cost bandwidth (tools/tune.py sweep)
+  uint32_t per_cu = 1;
   if (const char *e = getenv("B2P_WG_PER_CU")) {
     int v = atoi(e);
     if (v >= 1 && v <= 32) per_cu = (uint32_t)v;
@@ -243,6 +248,20 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   c->nchan = g->nchunk * g->nchan_chunk;
   c->nout = c->nchan * g->npol_out;
   c->frame_bytes = b2p_frame_bytes(g);
+  c->kc.mode = c->mode;
+  c->kc.npol_out = (int)g->npol_out;
+  // measured defaults (tools/tune.py, DESIGN.md "launch shape"): ~32 KiB of
+  // loads in flight per CU -- int8 512 threads x 4 rows, int16 256 x 8 --
+  // one workgroup per CU, contiguous row slices, non-temporal loads
+  c->kc.unroll = g->nbit == 8 ? 4 : 8;
+  c->kc.nt = true;
+  if (const char *e = getenv("B2P_UNROLL")) {
+    int v = atoi(e);
+    if (v == 4 || v == 8 || v == 16) c->kc.unroll = v;
+  }
+  if (const char *e = getenv("B2P_NT")) c->kc.nt = atoi(e) != 0;
+  if (const char *e = getenv("B2P_INTERLEAVE")) c->interleave = atoi(e) != 0;
+  if (const char *e = getenv("B2P_FUSE")) c->fuse = atoi(e) != 0;
   c->block_bytes = b2p_block_bytes(g);
   int rc;
   int ncu = 256;
@@ -260,8 +279,11 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "hipStreamCreate"));
   c->stream = c->own_stream;
-  const size_t rep_bytes = (size_t)c->nrep * c->nout * sizeof(unsigned long long);
+  // replicas, then the 4-B ticket (zeroed together; the in-launch finalize
+  // leaves both zero again)
+  const size_t rep_bytes = (size_t)c->nrep * c->nout * sizeof(unsigned long long) + 16;
   if (hipMalloc(&c->d_rep, rep_bytes) != hipSuccess) return fail(set_err(c, B2P_ENOMEM, "hipMalloc replicas"));
+  c->d_ticket = (uint32_t *)(c->d_rep + (size_t)c->nrep * c->nout);
   if (hipMalloc(&c->d_out, (size_t)c->nout * sizeof(float)) != hipSuccess)
     return fail(set_err(c, B2P_ENOMEM, "hipMalloc out"));
   if (hipMemsetAsync(c->d_rep, 0, rep_bytes, c->stream) != hipSuccess ||
@@ -305,6 +327,8 @@ int b2p_close(b2p_ctx_t *c) {
   if (c->d_rep) hipFree(c->d_rep);
   if (c->d_out) hipFree(c->d_out);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+  if (c->region_a) hipEventDestroy(c->region_a);
+  if (c->region_b) hipEventDestroy(c->region_b);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
   return B2P_OK;
@@ -322,6 +346,8 @@ int b2p_get_info(const b2p_ctx_t *c, b2p_info_t *info) {
   info->row_vectors = c->S;
   info->replicas = c->nrep;
   info->device = (uint32_t)c->device;
+  info->unroll = (uint32_t)c->kc.unroll;
+  info->nontemporal = c->kc.nt ? 1u : 0u;
   return B2P_OK;
 }
 
@@ -358,13 +384,13 @@ static hipEvent_t pool_event(b2p_ctx_t *c) {
   return e;
 }
 
-// Enqueue one integrate launch over a device span (frame-aligned).
-static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes) {
+// Enqueue one integrate launch over a device span (frame-aligned).  With
+// fused_out set, the launch also emits the integration (last workgroup).
+static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out) {
   IntegrateArgs a;
   a.data = (const uint4 *)dev;
   a.nvec = nbytes / 16;
   a.S = c->S;
-  a.nrows = (a.nvec + c->S - 1) / c->S;
   a.B = c->B;
   a.NC = c->NC;
   a.G = c->G;
@@ -374,21 +400,25 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes) {
   a.nchan_chunk = c->g.nchan_chunk;
   a.nout = c->nout;
   a.nrep = c->nrep;
+  a.interleave = c->interleave;
   a.rep = c->d_rep;
+  a.out = fused_out;
+  a.ticket = c->d_ticket;
+  a.mean = c->g.mean;
+  a.nsamp = (double)c->g.nsamp_int;
   const uint32_t grid = c->NC * c->G;
   EvPair p{nullptr, nullptr, nbytes, 0};
-  if (c->timing) {
+  if (c->timing == 2) {
+    c->region_launches++;
+    c->region_bytes += nbytes;
+  } else if (c->timing) {
     if (c->pending.size() >= kTimingRing) drain_timing(c);
     p.a = pool_event(c);
     p.b = pool_event(c);
     if (!p.a || !p.b) return set_err(c, B2P_EHIP, "hipEventCreate");
-    CK(c, hipEventRecord(p.a, c->stream));
   }
-  CK(c, launch_integrate(a, c->mode, (int)c->g.npol_out, c->Bpad, grid, c->stream));
-  if (c->timing) {
-    CK(c, hipEventRecord(p.b, c->stream));
-    c->pending.push_back(p);
-  }
+  CK(c, launch_integrate(a, c->kc, c->Bpad, grid, c->stream, p.a, p.b));
+  if (c->timing == 1) c->pending.push_back(p);
   return B2P_OK;
 }
 
@@ -427,7 +457,7 @@ int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
   int rc;
   if (is_device) {
     if ((uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
-    if ((rc = enqueue_span(c, buf, nbytes)) != B2P_OK) return rc;
+    if ((rc = enqueue_span(c, buf, nbytes, nullptr)) != B2P_OK) return rc;
   } else {
     if ((rc = ensure_staging(c)) != B2P_OK) return rc;
     const uint8_t *h = (const uint8_t *)buf;
@@ -439,7 +469,7 @@ int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
       CK(c, hipMemcpyAsync(c->d_stage[i], h + off, n, hipMemcpyHostToDevice, c->copy_stream));
       CK(c, hipEventRecord(c->ev_copied[i], c->copy_stream));
       CK(c, hipStreamWaitEvent(c->stream, c->ev_copied[i], 0));
-      if ((rc = enqueue_span(c, c->d_stage[i], n)) != B2P_OK) return rc;
+      if ((rc = enqueue_span(c, c->d_stage[i], n, nullptr)) != B2P_OK) return rc;
       CK(c, hipEventRecord(c->ev_consumed[i], c->stream));
       last = i;
     }
@@ -463,18 +493,16 @@ int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
   f.mean = c->g.mean;
   f.nsamp = (double)c->g.nsamp_int;
   EvPair p{nullptr, nullptr, 0, 1};
-  if (c->timing) {
+  if (c->timing == 2) {
+    c->region_finalizes++;
+  } else if (c->timing) {
     if (c->pending.size() >= kTimingRing) drain_timing(c);
     p.a = pool_event(c);
     p.b = pool_event(c);
     if (!p.a || !p.b) return set_err(c, B2P_EHIP, "hipEventCreate");
-    CK(c, hipEventRecord(p.a, c->stream));
   }
-  CK(c, launch_finalize(f, c->stream));
-  if (c->timing) {
-    CK(c, hipEventRecord(p.b, c->stream));
-    c->pending.push_back(p);
-  }
+  CK(c, launch_finalize(f, c->stream, p.a, p.b));
+  if (c->timing == 1) c->pending.push_back(p);
   if (!out_is_device)
     CK(c, hipMemcpyAsync(out, c->d_out, (size_t)c->nout * sizeof(float), hipMemcpyDeviceToHost, c->stream));
   const uint64_t got = c->samples;
@@ -499,9 +527,49 @@ int b2p_finish(b2p_ctx_t *c, float *out) {
   return rs != B2P_OK ? rs : rc;
 }
 
-int b2p_set_timing(b2p_ctx_t *c, int enable) {
-  if (!c) return B2P_EINVAL;
-  c->timing = enable ? 1 : 0;
+int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, float *out,
+                  int out_is_device) {
+  if (!c || !out) return B2P_EINVAL;
+  if (c->samples != 0) return set_err(c, B2P_EINVAL, "b2p_integrate with a push pending");
+  if (nbytes != c->block_bytes)
+    return set_err(c, nbytes % c->frame_bytes ? B2P_ERAGGED : B2P_EINVAL,
+                   "b2p_integrate needs exactly one integration (%llu B), got %zu",
+                   (unsigned long long)c->block_bytes, nbytes);
+  if (!is_device || !c->fuse) {  // staged / plain push, then the finalize kernel
+    int rc = b2p_push(c, buf, nbytes, 0);
+    if (rc != B2P_OK) return rc;
+    return b2p_finish_async(c, out, out_is_device);
+  }
+  if (!buf) return set_err(c, B2P_EINVAL, "null buffer");
+  if ((uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
+  CK(c, hipSetDevice(c->device));
+  int rc = enqueue_span(c, buf, nbytes, out_is_device ? out : c->d_out);
+  if (rc != B2P_OK) return rc;
+  if (!out_is_device)
+    CK(c, hipMemcpyAsync(out, c->d_out, (size_t)c->nout * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  return B2P_OK;
+}
+
+int b2p_set_timing(b2p_ctx_t *c, int mode) {
+  if (!c || mode < 0 || mode > 2) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  if (c->timing == 2 && mode != 2) {  // close the region
+    CK(c, hipEventRecord(c->region_b, c->stream));
+    CK(c, hipEventSynchronize(c->region_b));
+    float ms = 0.f;
+    CK(c, hipEventElapsedTime(&ms, c->region_a, c->region_b));
+    c->stats.launches += c->region_launches;
+    c->stats.bytes += c->region_bytes;
+    c->stats.finalizes += c->region_finalizes;
+    c->stats.kernel_ms += ms;  // the whole region, gaps and finalizes included
+    c->region_launches = c->region_bytes = c->region_finalizes = 0;
+  }
+  if (mode == 2 && c->timing != 2) {  // open a region
+    if (!c->region_a) CK(c, hipEventCreate(&c->region_a));
+    if (!c->region_b) CK(c, hipEventCreate(&c->region_b));
+    CK(c, hipEventRecord(c->region_a, c->stream));
+  }
+  c->timing = mode;
   return B2P_OK;
 }
 

@@ -17,7 +17,6 @@ enum Mode : int { kI8 = 0, kI16LE = 1, kI16BE = 2 };
 struct IntegrateArgs {
   const uint4 *data;            // span base, 16-B aligned, frame-aligned
   uint64_t nvec;                // 16-B vectors in the span
-  uint64_t nrows;               // ceil(nvec / S)
   uint32_t S;                   // vectors per row
   uint32_t B;                   // active threads per workgroup
   uint32_t NC;                  // workgroups across a row (S / B, or 1)
@@ -28,7 +27,13 @@ struct IntegrateArgs {
   uint32_t nchan_chunk;
   uint32_t nout;                // nchan * npol_out
   uint32_t nrep;                // accumulator replicas
+  uint32_t interleave;          // 1: group g owns rows g, g+G, ...; 0: a slice
   unsigned long long *rep;      // [nrep][nout] exact sums
+  // in-launch finalize (null out: the finalize kernel runs later instead)
+  float *out;                   // nout fp32, written by the last workgroup
+  uint32_t *ticket;             // arrival counter, 0 between launches
+  uint32_t mean;
+  double nsamp;
 };
 
 struct FinalizeArgs {
@@ -53,12 +58,22 @@ struct FillArgs {
   int32_t amp;
 };
 
-hipError_t launch_integrate(const IntegrateArgs &a, int mode, int npol_out,
-                            uint32_t block_threads, uint32_t grid,
-                            hipStream_t s);
-hipError_t occupancy_integrate(int mode, int npol_out, uint32_t threads,
+// which instantiation of the integrate kernel runs
+struct KernelChoice {
+  int mode;       // Mode
+  int npol_out;   // 1 or 2
+  int unroll;     // 4, 8 or 16 rows in flight per lane
+  bool nt;        // non-temporal loads
+};
+
+// ev0/ev1 may be null; when set they time the dispatch (hipExtLaunchKernel)
+hipError_t launch_integrate(const IntegrateArgs &a, const KernelChoice &k,
+                            uint32_t block_threads, uint32_t grid, hipStream_t s,
+                            hipEvent_t ev0, hipEvent_t ev1);
+hipError_t occupancy_integrate(const KernelChoice &k, uint32_t threads,
                                size_t lds_bytes, int *blocks_per_cu);
-hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s);
+hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s, hipEvent_t ev0,
+                           hipEvent_t ev1);
 hipError_t launch_fill(uint4 *dst, uint64_t nvec, const FillArgs &f,
                        hipStream_t s);
 uint64_t splitmix64_host(uint64_t x);

@@ -21,6 +21,7 @@
 //  * per-workgroup reduction through LDS 64-bit atomics, then one 64-bit
 //    global atomic per touched output into one of nrep replicas (exact
 //    integers: the result does not depend on arrival order).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "b2p_internal.h"
@@ -33,7 +34,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // rows a lane may accumulate in 32 bits before widening: a row adds at most
 // 4*128^2 = 2^16 per int8 word, so 2^15 rows stay below 2^31.
 constexpr uint32_t kFlushRows = 32768;
-constexpr int kUnroll = 8;
 
 __device__ __forceinline__ uint32_t pol_power16(uint32_t d, bool be) {
   if (be) d = __builtin_amdgcn_perm(d, d, 0x02030001u);  // swap bytes in each half
@@ -121,10 +121,31 @@ template <int NPO> struct Acc<kI8, NPO> : Acc8<NPO> { static constexpr int VW = 
 template <int NPO> struct Acc<kI16LE, NPO> : Acc16<false, NPO> { static constexpr int VW = 2; };
 template <int NPO> struct Acc<kI16BE, NPO> : Acc16<true, NPO> { static constexpr int VW = 2; };
 
-template <int MODE, int NPO>
+template <bool NT>
+__device__ __forceinline__ u32x4 stream_load(const u32x4 *p) {
+  if (NT) return __builtin_nontemporal_load(p);  // read-once stream: nt cache policy
+  return *p;
+}
+
+__device__ __forceinline__ float to_output(unsigned long long tot, uint32_t mean, double nsamp) {
+  // tot < 2^53: the double is exact, the float conversion is the one RNE
+  const double d = (double)tot;
+  return mean ? (float)(d / nsamp) : (float)d;
+}
+
+// UNROLL rows are loaded before any is consumed (UNROLL x 1 KiB in flight
+// per wave); NT selects the non-temporal load policy.  Both are tuning
+// knobs (B2P_UNROLL, B2P_NT) measured on the box, see DESIGN.md.
+//
+// Row mapping (a.interleave): 0 = row group g owns a contiguous slice of the
+// rows; 1 = group g owns rows g, g+G, g+2G, ... so that the whole grid
+// sweeps the span front to back together (the probe in tools/hbm_probe.hip
+// reads faster that way).  Either way a lane's channels never change.
+template <int MODE, int NPO, int UNROLL, bool NT>
 __global__ void __launch_bounds__(1024)
 b2p_integrate_kernel(IntegrateArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
+  __shared__ uint32_t s_last;
   using A = Acc<MODE, NPO>;
   constexpr int VW = A::VW;
   const uint32_t t = threadIdx.x;
@@ -150,34 +171,42 @@ b2p_integrate_kernel(IntegrateArgs a) {
   const u32x4 *data = reinterpret_cast<const u32x4 *>(a.data);
   A acc;
   acc.zero_all();
-  const uint64_t r0 = (uint64_t)grp * a.nrows / a.G;
-  const uint64_t r1 = (uint64_t)(grp + 1) * a.nrows / a.G;
   const uint64_t full = a.nvec / a.S;  // rows with every vector valid
-  const uint64_t rf = r1 < full ? r1 : full;
+  // this group's rows: rstart + i * rstep, i < rcount
+  uint64_t rstart, rstep, rcount;
+  if (a.interleave) {
+    rstart = grp;
+    rstep = a.G;
+    rcount = full > grp ? (full - grp + a.G - 1) / a.G : 0;
+  } else {
+    rstart = (uint64_t)grp * full / a.G;
+    rstep = 1;
+    rcount = (uint64_t)(grp + 1) * full / a.G - rstart;
+  }
   if (active) {
-    uint64_t r = r0;
-    while (r < rf) {
-      const uint64_t rend = (rf - r > kFlushRows) ? r + kFlushRows : rf;
-      // row base is wave-uniform (scalar), the lane offset is loop-invariant
-      for (; r + kUnroll <= rend; r += kUnroll) {
-        u32x4 v[kUnroll];
+    // row offsets are wave-uniform (scalar); the lane offset is invariant
+    const u32x4 *p = data + rstart * a.S + pos;
+    const uint64_t stepv = rstep * a.S;
+    uint64_t i = 0;
+    while (i < rcount) {
+      const uint64_t iend = (rcount - i > kFlushRows) ? i + kFlushRows : rcount;
+      for (; i + UNROLL <= iend; i += UNROLL) {
+        u32x4 v[UNROLL];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          const u32x4 *row = data + (r + u) * a.S;
-          v[u] = __builtin_nontemporal_load(row + pos);
-        }
+        for (int u = 0; u < UNROLL; ++u) v[u] = stream_load<NT>(p + u * stepv);
+        p += UNROLL * stepv;
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) acc.add(v[u]);
+        for (int u = 0; u < UNROLL; ++u) acc.add(v[u]);
       }
-      for (; r < rend; ++r) acc.add(__builtin_nontemporal_load(data + r * a.S + pos));
+      for (; i < iend; ++i, p += stepv) acc.add(stream_load<NT>(p));
       acc.flush();
     }
-    // ragged last row (only when the span is not a whole number of rows)
-    for (uint64_t rr = (r0 > rf ? r0 : rf); rr < r1; ++rr) {
-      const uint64_t vi = rr * a.S + pos;
-      if (vi < a.nvec) acc.add(data[vi]);
+    // ragged last row (span not a whole number of rows): the last group of
+    // every column takes it, its lanes keep their channels
+    if (grp == a.G - 1 && full * a.S + pos < a.nvec) {
+      acc.add(data[full * a.S + pos]);
+      acc.flush();
     }
-    acc.flush();
   }
   __syncthreads();
   if (active) {
@@ -195,6 +224,43 @@ b2p_integrate_kernel(IntegrateArgs a) {
     const unsigned long long x = lds[j];
     if (x) atomicAdd(&rep[j], x);
   }
+  if (!a.out) return;
+
+  // ---- in-launch finalize by the last workgroup to arrive ----------------
+  // (cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md "Valid
+  // forms"): every wave drains its replica atomics, the workgroup meets at a
+  // barrier, one lane releases at agent scope and takes a ticket; the
+  // workgroup holding the last ticket acquires and reads the replicas with
+  // agent-scope (L1-bypassing) loads.  Integer sums: arrival order is moot.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t ticket =
+        __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = ticket == gridDim.x - 1;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // every (replica, output) word read by its own lane -- all loads in flight
+  // at once -- and folded per output through LDS
+  for (uint32_t j = t; j < a.nout; j += blockDim.x) lds[j] = 0;
+  __syncthreads();
+  const uint32_t nwords = a.nrep * a.nout;
+  for (uint32_t k = t; k < nwords; k += blockDim.x) {
+    const unsigned long long x =
+        __hip_atomic_load(a.rep + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (x) atomicAdd(&lds[k % a.nout], x);
+    a.rep[k] = 0;
+  }
+  __syncthreads();
+  for (uint32_t j = t; j < a.nout; j += blockDim.x) a.out[j] = to_output(lds[j], a.mean, a.nsamp);
+  if (t == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sum the replicas, emit fp32 with one RNE rounding, zero the replicas.
@@ -215,9 +281,7 @@ __global__ void __launch_bounds__(256) b2p_finalize_kernel(FinalizeArgs a) {
   __syncthreads();
   if (w == 0 && j < a.nout) {
     const unsigned long long tot = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-    // tot < 2^53: the double is exact, the float conversion is the one RNE
-    const double d = (double)tot;
-    a.out[j] = a.mean ? (float)(d / a.nsamp) : (float)d;
+    a.out[j] = to_output(tot, a.mean, a.nsamp);
   }
 }
 
@@ -275,49 +339,58 @@ __global__ void __launch_bounds__(256) b2p_fill_kernel(uint4 *dst, uint64_t nvec
 }
 
 // ---- launchers --------------------------------------------------------------
-template <int MODE, int NPO>
-static hipError_t launch_t(const IntegrateArgs &a, uint32_t threads, uint32_t grid,
-                           hipStream_t s) {
-  const size_t lds = (size_t)a.nout * sizeof(unsigned long long);
-  hipLaunchKernelGGL((b2p_integrate_kernel<MODE, NPO>), dim3(grid), dim3(threads), lds, s, a);
-  return hipGetLastError();
-}
+typedef void (*IntegrateFn)(IntegrateArgs);
 
-hipError_t launch_integrate(const IntegrateArgs &a, int mode, int npol_out,
-                            uint32_t threads, uint32_t grid, hipStream_t s) {
-  switch (mode * 2 + (npol_out - 1)) {
-    case kI8 * 2 + 0: return launch_t<kI8, 1>(a, threads, grid, s);
-    case kI8 * 2 + 1: return launch_t<kI8, 2>(a, threads, grid, s);
-    case kI16LE * 2 + 0: return launch_t<kI16LE, 1>(a, threads, grid, s);
-    case kI16LE * 2 + 1: return launch_t<kI16LE, 2>(a, threads, grid, s);
-    case kI16BE * 2 + 0: return launch_t<kI16BE, 1>(a, threads, grid, s);
-    case kI16BE * 2 + 1: return launch_t<kI16BE, 2>(a, threads, grid, s);
+template <int MODE, int NPO>
+static IntegrateFn pick_t(int unroll, bool nt) {
+  switch (unroll * 2 + (nt ? 1 : 0)) {
+    case 4 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 4, false>;
+    case 4 * 2 + 1: return b2p_integrate_kernel<MODE, NPO, 4, true>;
+    case 16 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 16, false>;
+    case 16 * 2 + 1: return b2p_integrate_kernel<MODE, NPO, 16, true>;
+    case 8 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 8, false>;
+    default: return b2p_integrate_kernel<MODE, NPO, 8, true>;
   }
-  return hipErrorInvalidValue;
 }
 
-template <int MODE, int NPO>
-static hipError_t occ_t(uint32_t threads, size_t lds, int *blocks) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, b2p_integrate_kernel<MODE, NPO>,
+static IntegrateFn pick(int mode, int npol_out, int unroll, bool nt) {
+  switch (mode * 2 + (npol_out - 1)) {
+    case kI8 * 2 + 0: return pick_t<kI8, 1>(unroll, nt);
+    case kI8 * 2 + 1: return pick_t<kI8, 2>(unroll, nt);
+    case kI16LE * 2 + 0: return pick_t<kI16LE, 1>(unroll, nt);
+    case kI16LE * 2 + 1: return pick_t<kI16LE, 2>(unroll, nt);
+    case kI16BE * 2 + 0: return pick_t<kI16BE, 1>(unroll, nt);
+    case kI16BE * 2 + 1: return pick_t<kI16BE, 2>(unroll, nt);
+  }
+  return nullptr;
+}
+
+hipError_t launch_integrate(const IntegrateArgs &a, const KernelChoice &k, uint32_t threads,
+                            uint32_t grid, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+  IntegrateFn f = pick(k.mode, k.npol_out, k.unroll, k.nt);
+  if (!f) return hipErrorInvalidValue;
+  const size_t lds = (size_t)a.nout * sizeof(unsigned long long);
+  IntegrateArgs arg = a;
+  void *args[] = {&arg};
+  // start/stop events ride on the dispatch packet itself (no marker packets
+  // between kernels), so timing does not perturb the back-to-back stream
+  return hipExtLaunchKernel(reinterpret_cast<const void *>(f), dim3(grid), dim3(threads), args,
+                            lds, s, ev0, ev1, 0);
+}
+
+hipError_t occupancy_integrate(const KernelChoice &k, uint32_t threads, size_t lds, int *blocks) {
+  IntegrateFn f = pick(k.mode, k.npol_out, k.unroll, k.nt);
+  if (!f) return hipErrorInvalidValue;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void *>(f),
                                                       (int)threads, lds);
 }
 
-hipError_t occupancy_integrate(int mode, int npol_out, uint32_t threads, size_t lds, int *blocks) {
-  switch (mode * 2 + (npol_out - 1)) {
-    case kI8 * 2 + 0: return occ_t<kI8, 1>(threads, lds, blocks);
-    case kI8 * 2 + 1: return occ_t<kI8, 2>(threads, lds, blocks);
-    case kI16LE * 2 + 0: return occ_t<kI16LE, 1>(threads, lds, blocks);
-    case kI16LE * 2 + 1: return occ_t<kI16LE, 2>(threads, lds, blocks);
-    case kI16BE * 2 + 0: return occ_t<kI16BE, 1>(threads, lds, blocks);
-    case kI16BE * 2 + 1: return occ_t<kI16BE, 2>(threads, lds, blocks);
-  }
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s) {
+hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
   const uint32_t grid = (a.nout + 63) / 64;
-  hipLaunchKernelGGL(b2p_finalize_kernel, dim3(grid), dim3(256), 0, s, a);
-  return hipGetLastError();
+  FinalizeArgs arg = a;
+  void *args[] = {&arg};
+  return hipExtLaunchKernel(reinterpret_cast<const void *>(b2p_finalize_kernel), dim3(grid),
+                            dim3(256), args, 0, s, ev0, ev1, 0);
 }
 
 hipError_t launch_fill(uint4 *dst, uint64_t nvec, const FillArgs &f, hipStream_t s) {

@@ -1,0 +1,576 @@
+/*
+ * dada_ring.c -- SysV shared-memory rings with the PSRDADA ipcbuf / ipcio /
+ * dada_hdu call surface (include/b2p_dada.h).
+ *
+ * The reference links PSRDADA and uses its writer half (diskdb.cu:24-124,
+ * capture.c:586-642, sync.c:101-109); the reader half its baseband2power
+ * stage needed was never written.  Semantics
+ * kept from PSRDADA: data ring at key, header ring at key+1; one writer,
+ * several readers, each sees every block; a block marked filled with fewer
+ * than bufsz bytes ends the transfer; a writer that stops
+ * on a full block ends it with an empty block (ipcbuf_enable_eod).
+ */
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/ipc.h>
+#include <sys/sem.h>
+#include <sys/shm.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "b2p_dada.h"
+
+#define SYNC_MAGIC 0x50414642u /* "PAFB" */
+#define SYNC_VERSION 1u
+
+/* semaphore set layout */
+#define SEM_CLEAR 0
+#define SEM_WLOCK 1
+#define SEM_FULL(r) (2 + (r))
+#define SEM_RLOCK(r) (2 + IPCBUF_READERS + (r))
+#define NSEMS (2 + 2 * IPCBUF_READERS)
+
+struct ipcsync {
+  uint32_t magic, version;
+  uint64_t nbufs, bufsz;
+  uint32_t n_readers;
+  int32_t semid;
+  uint64_t w_count;                  /* blocks filled so far            */
+  uint64_t r_count[IPCBUF_READERS];  /* blocks cleared by each reader   */
+  uint64_t eod_count;                /* transfer ends after this many   */
+  int32_t sod;
+  int32_t pad;
+  uint64_t s_buf, s_byte;
+  /* followed by: int32 shmid[nbufs]; uint32 clear_cnt[nbufs];
+   *              uint64 nbytes[nbufs] (8-aligned)                        */
+};
+
+static int32_t *sync_shmids(ipcsync_t *s) { return (int32_t *)(s + 1); }
+static uint32_t *sync_clear(ipcsync_t *s) {
+  return (uint32_t *)(sync_shmids(s) + s->nbufs);
+}
+static uint64_t *sync_nbytes(ipcsync_t *s) {
+  uintptr_t p = (uintptr_t)(sync_clear(s) + s->nbufs);
+  return (uint64_t *)((p + 7) & ~(uintptr_t)7);
+}
+static size_t sync_size(uint64_t nbufs) {
+  return sizeof(ipcsync_t) + nbufs * (sizeof(int32_t) + sizeof(uint32_t)) + 8 +
+         nbufs * sizeof(uint64_t);
+}
+
+/* semop with EINTR retry; flags e.g. SEM_UNDO | IPC_NOWAIT */
+static int sem_do(int semid, int num, int op, int flags) {
+  struct sembuf sb;
+  sb.sem_num = (unsigned short)num;
+  sb.sem_op = (short)op;
+  sb.sem_flg = (short)flags;
+  for (;;) {
+    if (semop(semid, &sb, 1) == 0) return 0;
+    if (errno != EINTR) return -1;
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* multilog                                                            */
+
+struct multilog {
+  char name[128];
+  int use_syslog;
+  int nfp;
+  FILE *fp[8];
+};
+
+multilog_t *multilog_open(const char *program_name, char use_syslog) {
+  multilog_t *m = calloc(1, sizeof(*m));
+  if (!m) return NULL;
+  snprintf(m->name, sizeof m->name, "%s", program_name ? program_name : "");
+  m->use_syslog = use_syslog;
+  if (use_syslog) openlog(m->name, LOG_CONS | LOG_PID, LOG_USER);
+  return m;
+}
+
+int multilog_add(multilog_t *m, FILE *fptr) {
+  if (!m || !fptr || m->nfp >= 8) return -1;
+  m->fp[m->nfp++] = fptr;
+  return 0;
+}
+
+int multilog(multilog_t *m, int priority, const char *format, ...) {
+  if (!m) return -1;
+  char msg[1024];
+  va_list ap;
+  va_start(ap, format);
+  vsnprintf(msg, sizeof msg, format, ap);
+  va_end(ap);
+  char ts[64];
+  time_t now = time(NULL);
+  struct tm tmv;
+  strftime(ts, sizeof ts, "%Y-%m-%d-%H:%M:%S", localtime_r(&now, &tmv));
+  for (int i = 0; i < m->nfp; i++) {
+    fprintf(m->fp[i], "[%s] %s%s%s", ts, priority <= LOG_ERR ? "ERR " : "", msg,
+            (msg[0] && msg[strlen(msg) - 1] == '\n') ? "" : "\n");
+    fflush(m->fp[i]);
+  }
+  if (m->use_syslog) syslog(priority, "%s", msg);
+  return 0;
+}
+
+int multilog_close(multilog_t *m) {
+  if (!m) return -1;
+  for (int i = 0; i < m->nfp; i++) fflush(m->fp[i]);
+  if (m->use_syslog) closelog();
+  free(m);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* ipcbuf                                                               */
+
+int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers) {
+  if (!id || !nbufs || !bufsz || n_readers > IPCBUF_READERS || nbufs > 32767) return -1;
+  int syncid = shmget(key, sync_size(nbufs), IPC_CREAT | IPC_EXCL | 0666);
+  if (syncid < 0) return -1;
+  ipcsync_t *s = shmat(syncid, NULL, 0);
+  if (s == (void *)-1) {
+    shmctl(syncid, IPC_RMID, NULL);
+    return -1;
+  }
+  memset(s, 0, sync_size(nbufs));
+  s->nbufs = nbufs;
+  for (uint64_t i = 0; i < nbufs; i++) sync_shmids(s)[i] = -1;
+  s->bufsz = bufsz;
+  s->n_readers = n_readers;
+  s->semid = semget(IPC_PRIVATE, NSEMS, IPC_CREAT | 0666);
+  int ok = s->semid >= 0;
+  if (ok) {
+    unsigned short v[NSEMS];
+    memset(v, 0, sizeof v);
+    v[SEM_CLEAR] = (unsigned short)nbufs;
+    v[SEM_WLOCK] = 1;
+    for (int r = 0; r < IPCBUF_READERS; r++) v[SEM_RLOCK(r)] = 1;
+    union semun_u {
+      int val;
+      struct semid_ds *buf;
+      unsigned short *array;
+    } arg;
+    arg.array = v;
+    ok = semctl(s->semid, 0, SETALL, arg) == 0;
+  }
+  for (uint64_t i = 0; ok && i < nbufs; i++) {
+    int sid = shmget(IPC_PRIVATE, bufsz, IPC_CREAT | 0666);
+    sync_shmids(s)[i] = sid;
+    if (sid < 0) ok = 0;
+  }
+  if (!ok) {
+    for (uint64_t i = 0; i < nbufs; i++)
+      if (sync_shmids(s)[i] >= 0) shmctl(sync_shmids(s)[i], IPC_RMID, NULL);
+    if (s->semid >= 0) semctl(s->semid, 0, IPC_RMID);
+    shmdt(s);
+    shmctl(syncid, IPC_RMID, NULL);
+    return -1;
+  }
+  s->magic = SYNC_MAGIC; /* last: a connector never sees a half-built ring */
+  s->version = SYNC_VERSION;
+  shmdt(s);
+  return ipcbuf_connect(id, key);
+}
+
+int ipcbuf_connect(ipcbuf_t *id, key_t key) {
+  if (!id) return -1;
+  ipcbuf_t init = IPCBUF_INIT;
+  *id = init;
+  id->key = key;
+  id->syncid = shmget(key, 0, 0);
+  if (id->syncid < 0) return -1;
+  id->sync = shmat(id->syncid, NULL, 0);
+  if (id->sync == (void *)-1) {
+    id->sync = NULL;
+    return -1;
+  }
+  if (id->sync->magic != SYNC_MAGIC || id->sync->version != SYNC_VERSION) {
+    shmdt(id->sync);
+    id->sync = NULL;
+    errno = EINVAL;
+    return -1;
+  }
+  id->nbufs = id->sync->nbufs;
+  id->bufsz = id->sync->bufsz;
+  id->semid = id->sync->semid;
+  id->buffer = calloc(id->nbufs, sizeof(char *));
+  if (!id->buffer) return -1;
+  for (uint64_t i = 0; i < id->nbufs; i++) {
+    void *p = shmat(sync_shmids(id->sync)[i], NULL, 0);
+    if (p == (void *)-1) {
+      ipcbuf_disconnect(id);
+      return -1;
+    }
+    id->buffer[i] = p;
+  }
+  id->state = 1;
+  return 0;
+}
+
+int ipcbuf_disconnect(ipcbuf_t *id) {
+  if (!id) return -1;
+  if (id->state == 2) ipcbuf_unlock_write(id);
+  if (id->state == 3) ipcbuf_unlock_read(id);
+  if (id->buffer) {
+    for (uint64_t i = 0; i < id->nbufs; i++)
+      if (id->buffer[i]) shmdt(id->buffer[i]);
+    free(id->buffer);
+    id->buffer = NULL;
+  }
+  if (id->sync) shmdt(id->sync);
+  id->sync = NULL;
+  id->state = 0;
+  return 0;
+}
+
+int ipcbuf_destroy(ipcbuf_t *id) {
+  if (!id || !id->sync) return -1;
+  int semid = id->semid, syncid = id->syncid;
+  uint64_t n = id->nbufs;
+  int32_t *ids = malloc(n * sizeof(int32_t));
+  if (!ids) return -1;
+  memcpy(ids, sync_shmids(id->sync), n * sizeof(int32_t));
+  ipcbuf_disconnect(id);
+  for (uint64_t i = 0; i < n; i++) shmctl(ids[i], IPC_RMID, NULL);
+  free(ids);
+  semctl(semid, 0, IPC_RMID);
+  shmctl(syncid, IPC_RMID, NULL);
+  return 0;
+}
+
+int ipcbuf_lock_write(ipcbuf_t *id) {
+  if (!id || id->state != 1) return -1;
+  if (sem_do(id->semid, SEM_WLOCK, -1, SEM_UNDO | IPC_NOWAIT) < 0) return -1;
+  id->state = 2;
+  id->xfer_count = id->sync->w_count;
+  return 0;
+}
+
+int ipcbuf_unlock_write(ipcbuf_t *id) {
+  if (!id || id->state != 2) return -1;
+  sem_do(id->semid, SEM_WLOCK, 1, SEM_UNDO);
+  id->state = 1;
+  return 0;
+}
+
+int ipcbuf_lock_read(ipcbuf_t *id) {
+  if (!id || id->state != 1) return -1;
+  for (uint32_t r = 0; r < id->sync->n_readers; r++) {
+    if (sem_do(id->semid, SEM_RLOCK(r), -1, SEM_UNDO | IPC_NOWAIT) == 0) {
+      id->iread = (int)r;
+      id->state = 3;
+      id->xfer_count = id->sync->r_count[r];
+      return 0;
+    }
+  }
+  return -1;
+}
+
+int ipcbuf_unlock_read(ipcbuf_t *id) {
+  if (!id || id->state != 3) return -1;
+  sem_do(id->semid, SEM_RLOCK(id->iread), 1, SEM_UNDO);
+  id->iread = -1;
+  id->state = 1;
+  return 0;
+}
+
+char *ipcbuf_get_next_write(ipcbuf_t *id) {
+  if (!id || id->state != 2 || id->cur_open) return NULL;
+  if (sem_do(id->semid, SEM_CLEAR, -1, 0) < 0) return NULL;
+  id->cur_index = id->sync->w_count % id->nbufs;
+  id->cur_open = 1;
+  return id->buffer[id->cur_index];
+}
+
+int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {
+  if (!id || id->state != 2 || !id->cur_open || nbytes > id->bufsz) return -1;
+  ipcsync_t *s = id->sync;
+  sync_nbytes(s)[id->cur_index] = nbytes;
+  if (nbytes < id->bufsz) s->eod_count = s->w_count + 1; /* short block = EOD */
+  __atomic_store_n(&s->w_count, s->w_count + 1, __ATOMIC_RELEASE);
+  id->cur_open = 0;
+  id->xfer_count++;
+  for (uint32_t r = 0; r < s->n_readers; r++)
+    if (sem_do(id->semid, SEM_FULL(r), 1, 0) < 0) return -1;
+  return 0;
+}
+
+int ipcbuf_enable_eod(ipcbuf_t *id) {
+  if (!id || id->state != 2) return -1;
+  if (id->sync->eod_count && id->sync->eod_count == id->sync->w_count) return 0;
+  if (!ipcbuf_get_next_write(id)) return -1;
+  return ipcbuf_mark_filled(id, 0);
+}
+
+static int reader_at_eod(ipcbuf_t *id) {
+  uint64_t eod = __atomic_load_n(&id->sync->eod_count, __ATOMIC_ACQUIRE);
+  return eod && id->sync->r_count[id->iread] >= eod;
+}
+
+char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {
+  if (!id || id->state != 3 || id->cur_open) return NULL;
+  if (reader_at_eod(id)) return NULL;
+  if (sem_do(id->semid, SEM_FULL(id->iread), -1, 0) < 0) return NULL;
+  id->cur_index = id->sync->r_count[id->iread] % id->nbufs;
+  id->cur_open = 1;
+  if (bytes) *bytes = sync_nbytes(id->sync)[id->cur_index];
+  return id->buffer[id->cur_index];
+}
+
+int ipcbuf_mark_cleared(ipcbuf_t *id) {
+  if (!id || id->state != 3 || !id->cur_open) return -1;
+  ipcsync_t *s = id->sync;
+  const uint64_t idx = id->cur_index;
+  s->r_count[id->iread]++;
+  id->cur_open = 0;
+  id->xfer_count++;
+  if (__atomic_add_fetch(&sync_clear(s)[idx], 1, __ATOMIC_ACQ_REL) == s->n_readers) {
+    __atomic_store_n(&sync_clear(s)[idx], 0, __ATOMIC_RELEASE);
+    if (sem_do(id->semid, SEM_CLEAR, 1, 0) < 0) return -1;
+  }
+  return 0;
+}
+
+int ipcbuf_enable_sod(ipcbuf_t *id, uint64_t start_buf, uint64_t start_byte) {
+  if (!id || !id->sync) return -1;
+  id->sync->sod = 1;
+  id->sync->s_buf = start_buf;
+  id->sync->s_byte = start_byte;
+  return 0;
+}
+
+int ipcbuf_disable_sod(ipcbuf_t *id) {
+  if (!id || !id->sync) return -1;
+  id->sync->sod = 0;
+  return 0;
+}
+
+int ipcbuf_sod(ipcbuf_t *id) { return id && id->sync ? id->sync->sod : 0; }
+
+int ipcbuf_eod(ipcbuf_t *id) {
+  if (!id || !id->sync || id->iread < 0) return 0;
+  uint64_t eod = __atomic_load_n(&id->sync->eod_count, __ATOMIC_ACQUIRE);
+  return eod && id->sync->r_count[id->iread] + (uint64_t)id->cur_open >= eod;
+}
+
+uint64_t ipcbuf_get_bufsz(ipcbuf_t *id) { return id ? id->bufsz : 0; }
+uint64_t ipcbuf_get_nbufs(ipcbuf_t *id) { return id ? id->nbufs : 0; }
+uint64_t ipcbuf_get_nreaders(ipcbuf_t *id) { return id && id->sync ? id->sync->n_readers : 0; }
+char *ipcbuf_get_buffer(ipcbuf_t *id, uint64_t i) {
+  return id && id->buffer && i < id->nbufs ? id->buffer[i] : NULL;
+}
+uint64_t ipcbuf_get_write_count(ipcbuf_t *id) { return id && id->sync ? id->sync->w_count : 0; }
+uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread) {
+  return id && id->sync && iread >= 0 && iread < IPCBUF_READERS ? id->sync->r_count[iread] : 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* ipcio                                                                */
+
+int ipcio_open(ipcio_t *ipc, char rdwrt) {
+  if (!ipc) return -1;
+  ipc->rdwrt = rdwrt;
+  ipc->curbuf = NULL;
+  ipc->curbufsz = 0;
+  return rdwrt == 'W' ? ipcbuf_lock_write(&ipc->buf) : ipcbuf_lock_read(&ipc->buf);
+}
+
+int ipcio_close(ipcio_t *ipc) {
+  if (!ipc) return -1;
+  if (ipc->buf.state == 2) return ipcbuf_enable_eod(&ipc->buf);
+  return 0;
+}
+
+char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id) {
+  if (!ipc) return NULL;
+  char *p = ipcbuf_get_next_write(&ipc->buf);
+  if (p && block_id) *block_id = ipc->buf.cur_index;
+  ipc->curbuf = p;
+  ipc->curbufsz = ipc->buf.bufsz;
+  return p;
+}
+
+int ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes) {
+  if (!ipc) return -1;
+  ipc->curbuf = NULL;
+  return ipcbuf_mark_filled(&ipc->buf, bytes);
+}
+
+char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id) {
+  if (!ipc) return NULL;
+  uint64_t bytes = 0;
+  char *p = ipcbuf_get_next_read(&ipc->buf, &bytes);
+  if (!p) return NULL;
+  if (bytes == 0 && ipcbuf_eod(&ipc->buf)) { /* empty EOD marker block */
+    ipcbuf_mark_cleared(&ipc->buf);
+    return NULL;
+  }
+  if (curbufsz) *curbufsz = bytes;
+  if (block_id) *block_id = ipc->buf.cur_index;
+  ipc->curbuf = p;
+  ipc->curbufsz = bytes;
+  return p;
+}
+
+int ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes) {
+  (void)bytes;
+  if (!ipc) return -1;
+  ipc->curbuf = NULL;
+  return ipcbuf_mark_cleared(&ipc->buf);
+}
+
+/* ------------------------------------------------------------------ */
+/* dada_hdu                                                             */
+
+dada_hdu_t *dada_hdu_create(multilog_t *log) {
+  dada_hdu_t *h = calloc(1, sizeof(*h));
+  if (!h) return NULL;
+  h->log = log;
+  h->data_block_key = 0xdada;  /* PSRDADA default key */
+  h->header_block_key = 0xdadb;
+  return h;
+}
+
+void dada_hdu_set_key(dada_hdu_t *h, key_t key) {
+  if (!h) return;
+  h->data_block_key = key;
+  h->header_block_key = key + 1; /* header key = key+1 */
+}
+
+int dada_hdu_connect(dada_hdu_t *h) {
+  if (!h) return -1;
+  ipcio_t io = IPCIO_INIT;
+  ipcbuf_t hb = IPCBUF_INIT;
+  h->data_block = malloc(sizeof(ipcio_t));
+  h->header_block = malloc(sizeof(ipcbuf_t));
+  if (!h->data_block || !h->header_block) return -1;
+  *h->data_block = io;
+  *h->header_block = hb;
+  if (ipcbuf_connect(&h->data_block->buf, h->data_block_key) < 0) {
+    if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_connect: no data ring at key %x", h->data_block_key);
+    return -1;
+  }
+  if (ipcbuf_connect(h->header_block, h->header_block_key) < 0) {
+    if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_connect: no header ring at key %x", h->header_block_key);
+    ipcbuf_disconnect(&h->data_block->buf);
+    return -1;
+  }
+  return 0;
+}
+
+int dada_hdu_disconnect(dada_hdu_t *h) {
+  if (!h) return -1;
+  if (h->data_block) {
+    ipcbuf_disconnect(&h->data_block->buf);
+    free(h->data_block);
+    h->data_block = NULL;
+  }
+  if (h->header_block) {
+    ipcbuf_disconnect(h->header_block);
+    free(h->header_block);
+    h->header_block = NULL;
+  }
+  return 0;
+}
+
+void dada_hdu_destroy(dada_hdu_t *h) {
+  if (!h) return;
+  if (h->data_block || h->header_block) dada_hdu_disconnect(h);
+  free(h->header);
+  free(h);
+}
+
+int dada_hdu_lock_write(dada_hdu_t *h) {
+  if (!h || !h->data_block) return -1;
+  if (ipcbuf_lock_write(h->header_block) < 0) return -1;
+  if (ipcio_open(h->data_block, 'W') < 0) {
+    ipcbuf_unlock_write(h->header_block);
+    return -1;
+  }
+  return 0;
+}
+
+int dada_hdu_unlock_write(dada_hdu_t *h) {
+  if (!h || !h->data_block) return -1;
+  if (h->data_block->curbuf) ipcio_close_block_write(h->data_block, 0);
+  ipcio_close(h->data_block);
+  ipcbuf_unlock_write(&h->data_block->buf);
+  ipcbuf_unlock_write(h->header_block);
+  return 0;
+}
+
+int dada_hdu_lock_read(dada_hdu_t *h) {
+  if (!h || !h->data_block) return -1;
+  if (ipcbuf_lock_read(h->header_block) < 0) return -1;
+  if (ipcio_open(h->data_block, 'R') < 0) {
+    ipcbuf_unlock_read(h->header_block);
+    return -1;
+  }
+  return 0;
+}
+
+int dada_hdu_unlock_read(dada_hdu_t *h) {
+  if (!h || !h->data_block) return -1;
+  ipcbuf_unlock_read(&h->data_block->buf);
+  ipcbuf_unlock_read(h->header_block);
+  return 0;
+}
+
+int dada_hdu_open_read(dada_hdu_t *h) {
+  if (!h || !h->header_block) return -1;
+  uint64_t bytes = 0;
+  char *p = ipcbuf_get_next_read(h->header_block, &bytes);
+  if (!p) return -1;
+  uint64_t hsz = ipcbuf_get_bufsz(h->header_block);
+  if (!h->header) {
+    h->header = calloc(1, hsz + 1);
+    if (!h->header) return -1;
+  }
+  h->header_size = hsz;
+  memcpy(h->header, p, bytes < hsz ? bytes : hsz);
+  h->header[hsz] = 0;
+  return ipcbuf_mark_cleared(h->header_block);
+}
+
+int dada_db_create(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers, uint64_t hdr_nbufs,
+                   uint64_t hdr_bufsz) {
+  ipcbuf_t d = IPCBUF_INIT, hb = IPCBUF_INIT;
+  if (ipcbuf_create(&d, key, nbufs, bufsz, n_readers) < 0) return -1;
+  if (ipcbuf_create(&hb, key + 1, hdr_nbufs, hdr_bufsz, n_readers) < 0) {
+    ipcbuf_destroy(&d);
+    return -1;
+  }
+  ipcbuf_disconnect(&d);
+  ipcbuf_disconnect(&hb);
+  return 0;
+}
+
+int dada_db_destroy(key_t key) {
+  int rc = 0;
+  ipcbuf_t d = IPCBUF_INIT, hb = IPCBUF_INIT;
+  if (ipcbuf_connect(&d, key) == 0)
+    ipcbuf_destroy(&d);
+  else
+    rc = -1;
+  if (ipcbuf_connect(&hb, key + 1) == 0)
+    ipcbuf_destroy(&hb);
+  else
+    rc = -1;
+  return rc;
+}
+
+int64_t fileread(const char *filename, char *buffer, unsigned bufsz) {
+  if (!filename || !buffer || !bufsz) return -1;
+  FILE *fp = fopen(filename, "r");
+  if (!fp) return -1;
+  memset(buffer, 0, bufsz);
+  size_t n = fread(buffer, 1, bufsz - 1, fp);
+  fclose(fp);
+  return (int64_t)n;
+}

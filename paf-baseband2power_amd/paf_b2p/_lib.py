@@ -54,7 +54,7 @@ class Info(C.Structure):
     _fields_ = [("nchan", C.c_uint32), ("nout", C.c_uint32), ("frame_bytes", C.c_uint64),
                 ("block_bytes", C.c_uint64), ("threads", C.c_uint32), ("columns", C.c_uint32),
                 ("row_groups", C.c_uint32), ("row_vectors", C.c_uint32), ("replicas", C.c_uint32),
-                ("device", C.c_uint32)]
+                ("device", C.c_uint32), ("unroll", C.c_uint32), ("nontemporal", C.c_uint32)]
 
 
 class Stats(C.Structure):
@@ -83,6 +83,7 @@ PROTOTYPES = {
     "b2p_finish": (C.c_int, [_P, _P]),
     "b2p_finish_async": (C.c_int, [_P, _P, C.c_int]),
     "b2p_sync": (C.c_int, [_P]),
+    "b2p_integrate": (C.c_int, [_P, _P, C.c_size_t, C.c_int, _P, C.c_int]),
     "b2p_samples_pending": (C.c_uint64, [_P]),
     "b2p_set_timing": (C.c_int, [_P, C.c_int]),
     "b2p_get_stats": (C.c_int, [_P, C.POINTER(Stats)]),

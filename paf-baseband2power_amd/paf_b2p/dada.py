@@ -1,0 +1,216 @@
+"""ctypes binding of include/b2p_dada.h (lib/libpafdada.so): DADA ASCII
+headers and SysV ring buffers, used by the launcher and the tests.
+
+Mirrors the PSRDADA calls the reference makes (diskdb.cu:24-130,
+capture.c:590-781) plus the reader half.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from ._lib import PKG_DIR
+
+DADA_LIB = os.path.join(PKG_DIR, "lib", "libpafdada.so")
+BIN_DIR = os.path.join(PKG_DIR, "bin")
+HDR_SIZE = 4096
+
+_dl = None
+
+
+def dlib():
+    global _dl
+    if _dl is None:
+        if not os.path.exists(DADA_LIB):
+            raise ImportError(f"{DADA_LIB} not built (make -C paf-baseband2power_amd)")
+        L = C.CDLL(DADA_LIB)
+        P = C.c_void_p
+        L.ascii_header_get.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, P]
+        L.ascii_header_set.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p]
+        L.ascii_header_del.argtypes = [C.c_char_p, C.c_char_p]
+        L.dada_db_create.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint64, C.c_uint64]
+        L.dada_db_destroy.argtypes = [C.c_int]
+        L.dada_hdu_create.restype = P
+        L.dada_hdu_create.argtypes = [P]
+        L.dada_hdu_set_key.argtypes = [P, C.c_int]
+        for n in ("dada_hdu_connect", "dada_hdu_disconnect", "dada_hdu_lock_write",
+                  "dada_hdu_unlock_write", "dada_hdu_lock_read", "dada_hdu_unlock_read",
+                  "dada_hdu_open_read"):
+            getattr(L, n).argtypes = [P]
+        L.dada_hdu_destroy.argtypes = [P]
+        L.dada_hdu_destroy.restype = None
+        L.ipcio_open_block_write.restype = P
+        L.ipcio_open_block_write.argtypes = [P, C.POINTER(C.c_uint64)]
+        L.ipcio_close_block_write.argtypes = [P, C.c_uint64]
+        L.ipcio_open_block_read.restype = P
+        L.ipcio_open_block_read.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.ipcio_close_block_read.argtypes = [P, C.c_uint64]
+        L.ipcbuf_get_next_write.restype = P
+        L.ipcbuf_get_next_write.argtypes = [P]
+        L.ipcbuf_mark_filled.argtypes = [P, C.c_uint64]
+        L.ipcbuf_get_bufsz.restype = C.c_uint64
+        L.ipcbuf_get_bufsz.argtypes = [P]
+        L.ipcbuf_get_nbufs.restype = C.c_uint64
+        L.ipcbuf_get_nbufs.argtypes = [P]
+        L.ipcbuf_eod.argtypes = [P]
+        L.ipcbuf_enable_eod.argtypes = [P]
+        L.ipcbuf_get_write_count.restype = C.c_uint64
+        L.ipcbuf_get_write_count.argtypes = [P]
+        _dl = L
+    return _dl
+
+
+class HduStruct(C.Structure):
+    """struct dada_hdu (include/b2p_dada.h)"""
+    _fields_ = [("log", C.c_void_p), ("data_block", C.c_void_p), ("header_block", C.c_void_p),
+                ("header", C.c_void_p), ("header_size", C.c_uint64), ("data_block_key", C.c_int),
+                ("header_block_key", C.c_int)]
+
+
+# ---- ASCII header -------------------------------------------------------------
+
+def header_get(header: bytes | str, key: str, fmt: str = "%1023s"):
+    """Value of `key` (string by default), or None when absent."""
+    h = header.encode() if isinstance(header, str) else header
+    if fmt in ("%d", "%i"):
+        v = C.c_int()
+    elif fmt in ("%lf", "%f"):
+        v, fmt = C.c_double(), "%lf"
+    elif fmt in ("%lu", "%llu", "%" "lu"):
+        v = C.c_uint64()
+    else:
+        v = C.create_string_buffer(1024)
+    rc = dlib().ascii_header_get(h, key.encode(), fmt.encode(), C.byref(v))
+    if rc < 1:
+        return None
+    return v.value.decode() if isinstance(v, C.Array) else v.value
+
+
+def header_set(header: bytes | str, key: str, value, size: int = HDR_SIZE) -> bytes:
+    h = header.encode() if isinstance(header, str) else header
+    buf = C.create_string_buffer(h, max(size, len(h) + 256))
+    rc = dlib().ascii_header_set(buf, key.encode(), b"%s", str(value).encode())
+    if rc != 0:
+        raise ValueError(f"ascii_header_set {key}")
+    return buf.value
+
+
+def header_del(header: bytes | str, key: str) -> bytes:
+    h = header.encode() if isinstance(header, str) else header
+    buf = C.create_string_buffer(h, len(h) + 1)
+    dlib().ascii_header_del(buf, key.encode())
+    return buf.value
+
+
+def header_block(text: bytes | str, size: int = HDR_SIZE) -> bytes:
+    """NUL-padded fixed-size header block."""
+    t = text.encode() if isinstance(text, str) else text
+    if len(t) >= size:
+        raise ValueError("header longer than the header block")
+    return t + b"\0" * (size - len(t))
+
+
+# ---- rings --------------------------------------------------------------------------
+
+def create_ring(key: int, nbufs: int, bufsz: int, nreaders: int = 1, hdr_nbufs: int = 8,
+                hdr_bufsz: int = HDR_SIZE) -> None:
+    if dlib().dada_db_create(key, nbufs, bufsz, nreaders, hdr_nbufs, hdr_bufsz) != 0:
+        raise OSError(C.get_errno(), f"dada_db_create {key:x}")
+
+
+def destroy_ring(key: int) -> bool:
+    return dlib().dada_db_destroy(key) == 0
+
+
+class Hdu:
+    """A dada_hdu_t as writer ('W') or reader ('R')."""
+
+    def __init__(self, key: int, mode: str):
+        L = dlib()
+        self.mode = mode
+        self.h = L.dada_hdu_create(None)
+        L.dada_hdu_set_key(self.h, key)
+        if L.dada_hdu_connect(self.h) != 0:
+            L.dada_hdu_destroy(self.h)
+            raise OSError(f"no ring at key {key:x}")
+        lock = L.dada_hdu_lock_write if mode == "W" else L.dada_hdu_lock_read
+        if lock(self.h) != 0:
+            L.dada_hdu_destroy(self.h)
+            raise OSError(f"cannot lock ring {key:x} for {mode}")
+        s = HduStruct.from_address(self.h)
+        self.data = s.data_block        # ipcio_t* (its first member is the ipcbuf_t)
+        self.hdr = s.header_block       # ipcbuf_t*
+        self.bufsz = L.ipcbuf_get_bufsz(self.data)
+
+    # writer ----------------------------------------------------------------------
+    def write_header(self, text: bytes | str) -> None:
+        L = dlib()
+        p = L.ipcbuf_get_next_write(self.hdr)
+        hsz = L.ipcbuf_get_bufsz(self.hdr)
+        blk = header_block(text, hsz)
+        C.memmove(p, blk, hsz)
+        if L.ipcbuf_mark_filled(self.hdr, hsz) != 0:
+            raise OSError("mark_filled header")
+
+    def write_block(self, data: bytes | memoryview) -> None:
+        L = dlib()
+        bid = C.c_uint64()
+        p = L.ipcio_open_block_write(self.data, C.byref(bid))
+        if not p:
+            raise OSError("open_block_write")
+        n = len(data)
+        if n > self.bufsz:
+            raise ValueError("block too large")
+        C.memmove(p, bytes(data), n)
+        L.ipcio_close_block_write(self.data, n)
+
+    # reader ----------------------------------------------------------------------
+    def read_header(self) -> bytes:
+        L = dlib()
+        if L.dada_hdu_open_read(self.h) != 0:
+            raise OSError("open_read header")
+        s = HduStruct.from_address(self.h)
+        return C.string_at(s.header)
+
+    def read_block(self):
+        """bytes of the next block, or None at end of data"""
+        L = dlib()
+        n, bid = C.c_uint64(), C.c_uint64()
+        p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
+        if not p:
+            return None
+        out = C.string_at(p, n.value)
+        L.ipcio_close_block_read(self.data, n.value)
+        return out
+
+    def eod(self) -> bool:
+        return bool(dlib().ipcbuf_eod(self.data))
+
+    def close(self) -> None:
+        if self.h:
+            L = dlib()
+            (L.dada_hdu_unlock_write if self.mode == "W" else L.dada_hdu_unlock_read)(self.h)
+            L.dada_hdu_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def write_dada_file(path: str, header: bytes | str, payload) -> None:
+    """A DADA file: 4096-B ASCII header then the payload (the files paf_diskdb
+    reads, diskdb.cu:17,69)."""
+    with open(path, "wb") as f:
+        f.write(header_block(header))
+        f.write(memoryview(payload))
+
+
+def read_dada_file(path: str):
+    import numpy as np
+    with open(path, "rb") as f:
+        hdr = f.read(HDR_SIZE)
+        data = np.frombuffer(f.read(), dtype=np.uint8)
+    return hdr.split(b"\0", 1)[0], data

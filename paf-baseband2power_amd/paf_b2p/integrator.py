@@ -81,6 +81,20 @@ class Integrator:
         rc = L.lib().b2p_finish_async(self._ctx, C.c_void_p(out_ptr), int(out_is_device))
         return L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,))
 
+    def integrate(self, buf, out_ptr: int | None = None, out_is_device: bool = False):
+        """One whole integration in one call (fused finalize for device spans).
+        With out_ptr None the spectrum is returned (blocking)."""
+        ptr, n, dev = self._span(buf, None, None)
+        if out_ptr is None:
+            out = np.zeros(self.nout, dtype=np.float32)
+            L.check(L.lib().b2p_integrate(self._ctx, C.c_void_p(ptr), n, int(dev),
+                                          out.ctypes.data_as(C.c_void_p), 0), self._ctx)
+            self.sync()
+            return out
+        L.check(L.lib().b2p_integrate(self._ctx, C.c_void_p(ptr), n, int(dev), C.c_void_p(out_ptr),
+                                      int(out_is_device)), self._ctx)
+        return None
+
     def sync(self) -> None:
         L.check(L.lib().b2p_sync(self._ctx), self._ctx)
 
@@ -128,8 +142,9 @@ class Integrator:
                                            block, elem0), self._ctx)
 
     # ---- measurement -------------------------------------------------------------
-    def set_timing(self, on: bool) -> None:
-        L.check(L.lib().b2p_set_timing(self._ctx, int(on)), self._ctx)
+    def set_timing(self, mode: int | bool) -> None:
+        """0 off, 1 per-launch events, 2 one event pair around a region."""
+        L.check(L.lib().b2p_set_timing(self._ctx, int(mode)), self._ctx)
 
     def stats(self) -> dict:
         s = L.Stats()

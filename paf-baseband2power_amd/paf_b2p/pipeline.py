@@ -1,0 +1,145 @@
+"""Pipeline launcher: the role of the reference's paf-baseband2power.py.
+
+    python -m paf_b2p.pipeline -a paf-baseband2power.conf -b DIR -c GPU -f DATAFILE
+           [-d VISIBLEGPU] [-e MEMCHECK] [-s NSUB] [-g LAYOUT] [-p NPOL_OUT] [-m]
+
+Reads the same INI sections/keys (paf-baseband2power.py:49-80), writes the key
+files (:98-112), creates the two rings with dada_db (:114-115), runs the three
+stages as separate processes -- paf_diskdb, paf_baseband2power, paf_dbdisk
+(:85-95, :117-127) -- and destroys the rings (:129-130).  Differences: it
+parses (the reference's launcher is a SyntaxError at :90 and reads undefined
+args.psrname / args.dfname at :37-38), stops the other stages if one fails,
+and with -s N runs N independent sub-band chains, chain r on GPU r with ring
+keys KEY + 0x10*r (one GPU, one stream, one ring per sub-band).
+"""
+from __future__ import annotations
+
+import argparse
+import configparser
+import os
+import subprocess
+import sys
+import time
+
+from . import dada
+
+CONF_DIR = os.path.join(os.path.dirname(dada.BIN_DIR), "conf")
+
+
+def read_conf(path: str) -> dict:
+    cp = configparser.ConfigParser(inline_comment_prefixes=(";", "#"))
+    cp.read(path)
+    b, d, o = cp["BasicConf"], cp["DiskdbConf"], cp["Baseband2powerConf"]
+    c = {
+        "nsamp_df": int(b["nsamp_df"]), "npol_samp": int(b["npol_samp"]),
+        "ndim_pol": int(b["ndim_pol"]), "nchk_nic": int(b["nchk_nic"]),
+        "diskdb_ndf": int(d["ndf"]), "diskdb_nbuf": int(d["nblk"]),
+        "diskdb_key": int(d["key"], 16), "diskdb_kfname": f"{d['kfname_prefix']}.key",
+        "diskdb_hfname": d["hfname"], "diskdb_nreader": int(d["nreader"]),
+        "diskdb_sod": int(d["sod"]),
+        "b2p_key": int(o["key"], 16), "b2p_kfname": f"{o['kfname_prefix']}.key",
+        "b2p_nreader": int(o["nreader"]), "b2p_nbuf": int(o["nblk"]),
+        "b2p_nchan": int(o["nchan"]), "b2p_nbyte": int(o["nbyte"]),
+    }
+    # ring block sizes (paf-baseband2power.py:67, :79)
+    c["diskdb_rbufsz"] = c["diskdb_ndf"] * c["nchk_nic"] * 7168
+    c["b2p_rbufsz"] = c["b2p_nchan"] * c["b2p_nbyte"]
+    if "bytes_per_df" in b:
+        c["diskdb_rbufsz"] = c["diskdb_ndf"] * c["nchk_nic"] * int(b["bytes_per_df"])
+    return c
+
+
+def _bin(name: str) -> str:
+    return os.path.join(dada.BIN_DIR, name)
+
+
+def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
+        layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
+        hfname: str | None = None, outfiles: list | None = None) -> list:
+    """Run the chains; returns the output file path of every sub-band."""
+    c = read_conf(conf_path)
+    hdr = hfname or c["diskdb_hfname"]
+    if not os.path.isabs(hdr):
+        cand = [os.path.join(os.path.dirname(os.path.abspath(conf_path)), hdr),
+                os.path.join(CONF_DIR, hdr)]
+        hdr = next((p for p in cand if os.path.exists(p)), cand[0])
+    os.makedirs(directory, exist_ok=True)
+    outs, procs, keys = [], [], []
+    try:
+        for r in range(nsub):
+            kin, kout = c["diskdb_key"] + 0x10 * r, c["b2p_key"] + 0x10 * r
+            for kf, k in ((c["diskdb_kfname"], kin), (c["b2p_kfname"], kout)):
+                with open(os.path.join(directory, kf if nsub == 1 else f"{r}_{kf}"), "w") as f:
+                    f.write("DADA INFO:\n")
+                    f.write(f"key {k:x}\n")
+            dada.destroy_ring(kin)
+            dada.destroy_ring(kout)
+            dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"])
+            keys.append(kin)
+            obytes = c["b2p_rbufsz"] * npol_out
+            dada.create_ring(kout, c["b2p_nbuf"], obytes, c["b2p_nreader"])
+            keys.append(kout)
+            sub_dir = directory if nsub == 1 else os.path.join(directory, f"subband{r}")
+            os.makedirs(sub_dir, exist_ok=True)
+            out = (outfiles[r] if outfiles else os.path.join(sub_dir, "power.dada"))
+            outs.append(out)
+            dfile = datafile if isinstance(datafile, str) else datafile[r]
+            b2p_cmd = [_bin("paf_baseband2power"), "-a", f"{kin:x}", "-b", f"{kout:x}",
+                       "-c", sub_dir, "-d", str(gpu + r), "-p", str(npol_out)]
+            if layout:
+                b2p_cmd += ["-f", layout]
+            if mean:
+                b2p_cmd.append("-m")
+            procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
+                                          stderr=subprocess.PIPE))
+            procs.append(subprocess.Popen(b2p_cmd, stderr=subprocess.PIPE))
+            procs.append(subprocess.Popen(
+                [_bin("paf_diskdb"), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
+                 "-c", os.path.basename(dfile), "-d", hdr, "-e", str(c["diskdb_sod"])],
+                stderr=subprocess.PIPE))
+        t_end = time.time() + timeout
+        failed = None
+        while any(p.poll() is None for p in procs):
+            for p in procs:
+                if p.poll() not in (None, 0):
+                    failed = p
+            if failed or time.time() > t_end:
+                break
+            time.sleep(0.05)
+        if failed is None:
+            failed = next((p for p in procs if p.poll() not in (None, 0)), None)
+        if failed is not None or any(p.poll() is None for p in procs):
+            for p in procs:  # stop the rest (exact PIDs we started)
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+            msgs = [f"{p.args[0]}: rc={p.returncode} {p.stderr.read().decode(errors='replace')[-400:]}"
+                    for p in procs]
+            raise RuntimeError("pipeline failed:\n" + "\n".join(msgs))
+        return outs
+    finally:
+        for k in keys:  # paf-baseband2power.py:129-130
+            dada.destroy_ring(k)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="baseband -> power pipeline (DADA rings)")
+    ap.add_argument("-a", "--cfname", required=True, help="configuration file")
+    ap.add_argument("-b", "--directory", required=True, help="output / log directory")
+    ap.add_argument("-c", "--gpu", type=int, default=0, help="index of the first GPU")
+    ap.add_argument("-d", "--visiblegpu", default="", help="accepted for compatibility")
+    ap.add_argument("-e", "--memcheck", type=int, default=0, help="accepted (no cuda-memcheck)")
+    ap.add_argument("-f", "--dfname", required=True, nargs="+", help="DADA data file(s)")
+    ap.add_argument("-s", "--subbands", type=int, default=1)
+    ap.add_argument("-g", "--layout", default="")
+    ap.add_argument("-p", "--npol-out", type=int, default=1)
+    ap.add_argument("-m", "--mean", action="store_true")
+    a = ap.parse_args(argv)
+    files = a.dfname if a.subbands > 1 else a.dfname[0]
+    outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean)
+    print("\n".join(outs))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

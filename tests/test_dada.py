@@ -1,0 +1,283 @@
+"""DADA layer (CPU): ASCII headers, SysV rings, the diskdb / dbdisk / dada_db
+executables, and the configs[0] plumbing (diskdb file -> ring -> CPU path).
+
+The ring contract follows PSRDADA as the reference uses it (SURVEY.md 3.1,
+3.2, Appendix A): header ring at key+1, one writer, N readers each seeing
+every block, a short block ends the transfer.
+"""
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+from conftest import REPO
+from paf_b2p import dada
+
+BIN = dada.BIN_DIR
+TEMPLATE = """HEADER       DADA                # Distributed aquisition and data analysis
+HDR_VERSION  1.0                 # Version of this ASCII header
+HDR_SIZE     4096                # Size of the header in bytes
+UTC_START    2018-11-05-00:00:00 # yyyy-mm-dd-hh:mm:ss
+OBS_OFFSET   0                   # bytes offset from the start MJD/UTC
+TELESCOPE    Effelsberg       # telescope name
+TSAMP        88473.6               # sampling interval in microseconds
+NBIT         32                      # number of bits per sample, here record float
+NDIM         1                   # dimension of samples (2=complex, 1=real)
+NPOL         1                   # number of polarizations observed
+NCHAN        336                    # number of channels here
+"""
+
+_key_lock = threading.Lock()
+_next_key = [0x5a00 + (os.getpid() % 64) * 16]
+
+
+def fresh_key() -> int:
+    with _key_lock:
+        k = _next_key[0]
+        _next_key[0] += 2
+    dada.destroy_ring(k)  # leftovers of an aborted run
+    return k
+
+
+@pytest.fixture
+def ring():
+    made = []
+
+    def make(nbufs, bufsz, nreaders=1):
+        k = fresh_key()
+        dada.create_ring(k, nbufs, bufsz, nreaders)
+        made.append(k)
+        return k
+
+    yield make
+    for k in made:
+        dada.destroy_ring(k)
+
+
+# ---- ASCII header (capture.c:758-778 usage) ---------------------------------------
+
+def test_header_get_values():
+    assert dada.header_get(TEMPLATE, "NCHAN", "%d") == 336
+    assert dada.header_get(TEMPLATE, "TSAMP", "%lf") == 88473.6
+    assert dada.header_get(TEMPLATE, "TELESCOPE") == "Effelsberg"
+    assert dada.header_get(TEMPLATE, "NOPE") is None
+    # whole-word, line-start match only
+    assert dada.header_get("XNCHAN 5\nNCHAN 7\n", "NCHAN", "%d") == 7
+    assert dada.header_get("NCHANX 5\n", "NCHAN", "%d") is None
+
+
+def test_header_set_replaces_keeps_comment_and_appends():
+    h = dada.header_set(TEMPLATE, "NCHAN", 1024)
+    assert dada.header_get(h, "NCHAN", "%d") == 1024
+    line = [ln for ln in h.decode().splitlines() if ln.startswith("NCHAN")][0]
+    assert "# number of channels here" in line
+    h2 = dada.header_set(h, "FREQ", "1340.5")
+    assert dada.header_get(h2, "FREQ", "%lf") == 1340.5
+    assert h2.decode().count("\n") == h.decode().count("\n") + 1
+    h3 = dada.header_del(h2, "FREQ")
+    assert dada.header_get(h3, "FREQ") is None
+    # every other key untouched
+    for k in ("HEADER", "TSAMP", "UTC_START", "NBIT"):
+        assert dada.header_get(h3, k) == dada.header_get(TEMPLATE, k)
+
+
+def test_reference_template_parses():
+    path = os.path.join(REPO, "paf-baseband2power_amd", "conf", "header_baseband2power.txt")
+    text = open(path).read()
+    assert dada.header_get(text, "NCHAN", "%d") == 336
+    assert dada.header_get(text, "NBIT", "%d") == 32
+    assert dada.header_get(text, "HDR_SIZE", "%d") == 4096
+
+
+# ---- rings -----------------------------------------------------------------------------
+
+def test_ring_roundtrip_and_short_block_eod(ring):
+    k = ring(3, 4096)
+    rng = np.random.default_rng(1)
+    blocks = [rng.integers(0, 256, 4096, dtype=np.uint8).tobytes() for _ in range(7)] + [b"x" * 100]
+    got = []
+
+    def reader():
+        with dada.Hdu(k, "R") as r:
+            got.append(r.read_header())
+            while True:
+                b = r.read_block()
+                if b is None:
+                    break
+                got.append(b)
+
+    t = threading.Thread(target=reader)
+    t.start()
+    with dada.Hdu(k, "W") as w:
+        w.write_header(TEMPLATE)
+        for b in blocks:  # 8 blocks through a 3-block ring: flow control
+            w.write_block(b)
+    t.join(30)
+    assert not t.is_alive()
+    assert got[0].decode() == TEMPLATE
+    assert got[1:] == blocks
+
+
+def test_ring_full_last_block_then_empty_eod(ring):
+    k = ring(2, 1024)
+    out = []
+
+    def reader():
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            while (b := r.read_block()) is not None:
+                out.append(len(b))
+            out.append("eod" if r.eod() else "no-eod")
+
+    t = threading.Thread(target=reader)
+    t.start()
+    with dada.Hdu(k, "W") as w:
+        w.write_header("HDR 1\n")
+        for _ in range(3):
+            w.write_block(b"\1" * 1024)
+    # unlock_write (close) ends the transfer with an empty block
+    t.join(30)
+    assert out == [1024, 1024, 1024, "eod"]
+
+
+def test_two_readers_each_see_every_block(ring):
+    k = ring(2, 512, nreaders=2)
+    res = {0: [], 1: []}
+
+    def reader(i):
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            while (b := r.read_block()) is not None:
+                res[i].append(b[0])
+
+    ts = [threading.Thread(target=reader, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    with dada.Hdu(k, "W") as w:
+        w.write_header("HDR 1\n")
+        for i in range(9):
+            w.write_block(bytes([i]) * 512)
+    for t in ts:
+        t.join(30)
+    assert res[0] == list(range(9)) and res[1] == list(range(9))
+
+
+def test_single_writer_lock(ring):
+    k = ring(2, 512)
+    with dada.Hdu(k, "W"):
+        with pytest.raises(OSError):
+            dada.Hdu(k, "W")
+    with dada.Hdu(k, "W"):  # released by close
+        pass
+
+
+def test_connect_missing_ring_fails():
+    k = fresh_key()
+    with pytest.raises(OSError):
+        dada.Hdu(k, "R")
+
+
+def test_dada_db_tool_create_destroy():
+    k = fresh_key()
+    r = subprocess.run([f"{BIN}/dada_db", "-k", f"{k:x}", "-b", "8192", "-n", "4", "-r", "1",
+                        "-l", "-p"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    with dada.Hdu(k, "W") as w:
+        assert w.bufsz == 8192
+    assert subprocess.run([f"{BIN}/dada_db", "-k", f"{k:x}", "-d"]).returncode == 0
+    assert subprocess.run([f"{BIN}/dada_db", "-k", f"{k:x}", "-d"],
+                          capture_output=True).returncode != 0
+
+
+# ---- executables: diskdb -> ring -> dbdisk (byte-exact) -------------------------------
+
+def run_diskdb(key, path, hdr_path, sod=1):
+    return subprocess.Popen([f"{BIN}/paf_diskdb", "-a", f"{key:x}", "-b", os.path.dirname(path),
+                             "-c", os.path.basename(path), "-d", hdr_path, "-e", str(sod)],
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+
+
+@pytest.mark.parametrize("payload_blocks", [3.0, 2.5])
+def test_diskdb_to_dbdisk_bytes(tmp_path, ring, payload_blocks):
+    bufsz = 64 * 1024
+    k = ring(4, bufsz)
+    payload = np.random.default_rng(3).integers(0, 256, int(bufsz * payload_blocks),
+                                                dtype=np.uint8)
+    src = tmp_path / "obs.dada"
+    dada.write_dada_file(str(src), "FILE_HEADER_IS_SKIPPED 1\n", payload)
+    hdr = tmp_path / "header.txt"
+    hdr.write_text(TEMPLATE)
+    out = tmp_path / "out.dada"
+    sink = subprocess.Popen([f"{BIN}/paf_dbdisk", "-k", f"{k:x}", "-o", str(out), "-W"],
+                            stderr=subprocess.PIPE)
+    src_p = run_diskdb(k, str(src), str(hdr))
+    assert src_p.wait(60) == 0, src_p.stderr.read()
+    assert sink.wait(60) == 0, sink.stderr.read()
+    h, data = dada.read_dada_file(str(out))
+    assert h.decode() == TEMPLATE                # diskdb.cu:79-93: the template header
+    assert np.array_equal(data, payload)         # diskdb.cu:69,103-121: payload only
+
+
+def test_dbdisk_default_file_name(tmp_path, ring):
+    k = ring(2, 1024)
+    sink = subprocess.Popen([f"{BIN}/paf_dbdisk", "-k", f"{k:x}", "-D", str(tmp_path)])
+    with dada.Hdu(k, "W") as w:
+        w.write_header(TEMPLATE)
+        w.write_block(b"\7" * 1024)
+    assert sink.wait(30) == 0
+    assert os.listdir(tmp_path) == ["2018-11-05-00:00:00_0000000000000000.000000.dada"]
+
+
+# ---- configs[0]: 256 ch x 2 pol, 1024x1024 integrate from a diskdb file, CPU path ---
+
+def test_config1_diskdb_plumbing_cpu(tmp_path, ring):
+    """paf_diskdb feeds one full 1 GiB integration through a ring; a CPU
+    consumer (the oracle, as the reference has no CPU path) integrates every
+    block it receives; the spectrum equals the oracle run on the file."""
+    g = npo.Geom(nbit=8, nchan_chunk=256)  # configs[0]: 256 x 2 pol, 1<<20 samples
+    nblk = 4
+    bufsz = g.block_bytes // nblk
+    k = ring(3, bufsz)
+    payload = co.fill_synthetic(g, g.block_bytes, 20181105, 0, 0)
+    src = tmp_path / "c1.dada"
+    dada.write_dada_file(str(src), "NBIT 8\nNCHAN 256\n", payload)
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text(TEMPLATE)
+    acc = np.zeros(g.nout, dtype=np.uint64)
+    seen = []
+
+    def consumer():
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            while (b := r.read_block()) is not None:
+                seen.append(len(b))
+                co.integrate(g, np.frombuffer(b, dtype=np.uint8), nthreads=4, acc=acc)
+
+    t = threading.Thread(target=consumer)
+    t.start()
+    p = run_diskdb(k, str(src), str(hdr))
+    assert p.wait(300) == 0
+    t.join(300)
+    assert seen == [bufsz] * nblk
+    direct = co.power(g, payload, nthreads=8)
+    assert np.array_equal(co.finalize(g, acc).view(np.uint32), direct.view(np.uint32))
+    del payload
+
+
+def test_paf_baseband2power_cli_help_and_no_gpu(tmp_path, have_gpu):
+    exe = f"{BIN}/paf_baseband2power"
+    r = subprocess.run([exe, "-h"], capture_output=True, text=True)
+    assert r.returncode == 1 and "-a  Hexacdecimal shared memory key" in r.stdout
+    r = subprocess.run([exe, "-a", "zz", "-b", "adad"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Could not parse key" in r.stderr
+    if have_gpu:
+        return
+    r = subprocess.run([exe, "-a", "dada", "-b", "adad", "-c", str(tmp_path), "-d", "0"],
+                       capture_output=True, text=True)
+    assert r.returncode == 1
+    log = (tmp_path / "paf_baseband2power.log").read_text()
+    assert "START PAF_PROCESS" in log and "no HIP device" in log

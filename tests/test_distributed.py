@@ -1,0 +1,81 @@
+"""N>1 path on CPU: world_size-2 gloo processes, one sub-band each, spectra
+gathered to rank 0 in sub-band order, max-over-ranks timing (the same
+functions bench.py uses with RCCL)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ORACLE, PKG
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    import b2p_oracle as npo
+    from paf_b2p import distributed as D
+
+    r, w, _ = D.env_ranks()
+    D.init("gloo", r)
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=64)
+    steps = 3
+    spec = []
+    for k in range(steps):  # this rank's sub-band, 3 integrations
+        buf = npo.fill_synthetic(g, g.block_bytes, 20181105, D.subband_of(r), k)
+        spec.append(npo.power(g, buf))
+    local = torch.from_numpy(np.stack(spec))
+    got = D.gather_spectra(local)
+    el = D.max_over_ranks(0.5 + r)
+    if r == 0:
+        q.put(("gather", [t.numpy() for t in got], el))
+    else:
+        q.put(("peer", got, el))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_gather_and_max(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    sys.path.insert(0, ORACLE)
+    import b2p_oracle as npo
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=64)
+    root = [x for x in res if x[0] == "gather"][0]
+    assert all(x[2] == world - 0.5 for x in res)          # max over ranks
+    assert [x[1] for x in res if x[0] == "peer"] == [None] * (world - 1)
+    for sb, arr in enumerate(root[1]):                    # rank order == sub-band order
+        for k in range(3):
+            buf = npo.fill_synthetic(g, g.block_bytes, 20181105, sb, k)
+            assert np.array_equal(arr[k], npo.power(g, buf))
+
+
+def test_aggregate_rate_formula():
+    sys.path.insert(0, PKG)
+    from paf_b2p import distributed as D
+    # 8 ranks x 10 steps x 2^29 samples in 1 s
+    assert D.aggregate_rate(8, 10, 1 << 29, 1.0) == 8 * 10 * (1 << 29) / 1e6

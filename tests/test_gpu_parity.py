@@ -259,3 +259,82 @@ def test_device_index_fallback(gpu):
         pytest.skip("more than one device visible")
     with paf_b2p.Integrator(paf_b2p.generic_geom(256), device=5) as it:
         assert it.info.device == 0
+
+
+@pytest.mark.parametrize("name", sorted(GEOMS))
+@pytest.mark.parametrize("npol_out,mean", [(1, 0), (2, 1)])
+def test_integrate_fused_equals_push_finish(gpu, name, npol_out, mean):
+    # b2p_integrate: one launch, last workgroup finalizes; three back-to-back
+    # integrations on one context (the arrival ticket must re-arm) and both
+    # row mappings
+    g = npo.Geom(**{**GEOMS[name].asdict(), "npol_out": npol_out, "mean": mean})
+    bufs = [npo.fill_synthetic(g, g.block_bytes, SEED, 2, k) for k in range(3)]
+    for inter in (0, 1):
+        os.environ["B2P_INTERLEAVE"] = str(inter)
+        try:
+            with paf_b2p.Integrator(to_b2p(g)) as it:
+                for b in bufs:
+                    d = it.upload(b)
+                    fused = it.integrate(d)
+                    it.push(d)
+                    pf = it.finish()
+                    d.free()
+                    assert same_bits(fused, pf)
+                    assert same_bits(fused, npo.power(g, b))
+        finally:
+            os.environ.pop("B2P_INTERLEAVE", None)
+
+
+def test_integrate_host_span_and_errors(gpu):
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=4096)
+    buf = co.fill_synthetic(g, g.block_bytes, SEED, 0, 0)
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        assert same_bits(it.integrate(buf), co.power(g, buf))   # host span
+        d = it.upload(buf)
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.integrate((d, 0, g.block_bytes - g.frame_bytes))
+        assert e.value.code == L.B2P_EINVAL
+        it.push((d, 0, g.frame_bytes))
+        with pytest.raises(paf_b2p.B2PError):
+            it.integrate(d)                                      # a push is pending
+        it.finish(allow_partial=True)
+        assert same_bits(it.integrate(d), co.power(g, buf))
+        d.free()
+
+
+def test_full_size_fused_vs_oracle(gpu):
+    # configs[1] and the BMF block through the one-launch path
+    for g, pg in ((npo.Geom(nbit=8, nchan_chunk=256), paf_b2p.generic_geom(256)),
+                  (npo.BMF, paf_b2p.bmf_geom())):
+        with paf_b2p.Integrator(pg) as it:
+            d = it.alloc(g.block_bytes)
+            it.fill_synthetic(d, SEED, 7, 7)
+            out = it.integrate(d)
+            host = it.download(d)
+            d.free()
+        assert same_bits(out, co.power(g, host, nthreads=16))
+
+
+def test_timing_modes(gpu):
+    g = paf_b2p.generic_geom(256)
+    with paf_b2p.Integrator(g) as it:
+        d = it.alloc(it.block_bytes)
+        it.fill_synthetic(d, SEED, 0, 0)
+        it.set_timing(1)
+        for _ in range(3):
+            it.push(d)
+            it.finish()
+        s1 = it.stats()
+        assert s1["launches"] == 3 and s1["finalizes"] == 3 and s1["bytes"] == 3 * it.block_bytes
+        per = s1["kernel_ms"] / 3
+        assert 0.05 < per < 5.0  # ms; 1 GiB at 0.2-20 TB/s
+        it.set_timing(0)
+        it.reset_stats()
+        it.set_timing(2)
+        for _ in range(4):
+            it.integrate(d, None)
+        it.set_timing(0)
+        s2 = it.stats()
+        assert s2["launches"] == 4 and s2["finalizes"] == 0
+        assert s2["kernel_ms"] / 4 > 0.5 * per
+        d.free()

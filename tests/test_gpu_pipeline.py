@@ -1,0 +1,102 @@
+"""End-to-end drop-in test on the GPU: the three-process DADA pipeline
+(paf_diskdb -> paf_baseband2power -> paf_dbdisk, launched like
+paf-baseband2power.py) against the oracle run on the input file.
+"""
+import os
+import textwrap
+
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+from paf_b2p import dada, pipeline
+
+pytestmark = pytest.mark.gpu
+SEED = 20181105
+
+
+def write_conf(path, ndf, nchk, bytes_per_df, nchan_out, key_in, key_out, hfname):
+    path.write_text(textwrap.dedent(f"""\
+        [BasicConf]
+        NSAMP_DF: 128
+        NPOL_SAMP: 2
+        NDIM_POL: 2
+        NCHK_NIC: {nchk}
+        BYTES_PER_DF: {bytes_per_df}
+        [DiskdbConf]
+        NDF: {ndf}
+        NBLK: 3
+        KEY: {key_in:x}
+        KFNAME_PREFIX: diskdb
+        NREADER: 1
+        SOD: 1
+        HFNAME: {hfname}
+        [Baseband2powerConf]
+        KEY: {key_out:x}
+        KFNAME_PREFIX: baseband2power
+        NREADER: 1
+        SOD: 1
+        NCHAN: {nchan_out}
+        NBYTE: 4
+        NBLK: 4
+        """))
+
+
+def spectra(path, nout):
+    hdr, data = dada.read_dada_file(path)
+    return hdr.decode(), data.view(np.float32).reshape(-1, nout)
+
+
+@pytest.mark.parametrize("npol_out,mean", [(1, 0), (2, 1)])
+def test_bmf_pipeline(gpu, tmp_path, npol_out, mean):
+    # BMF-native TFTFP int16 BE, 64 DFs per block (8192 samples per integration),
+    # 3 whole integrations + a partial one that must be skipped
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=64 * 128, npol_out=npol_out, mean=mean)
+    nblk = 3
+    payload = co.fill_synthetic(g, g.block_bytes * nblk + g.block_bytes // 2, SEED, 0, 9)
+    src = tmp_path / "bmf.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 64, 48, 7168, 336, 0x6a10, 0x6b10, "header_baseband2power.txt")
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, str(src), npol_out=npol_out,
+                        mean=bool(mean), layout="bmf", timeout=600)
+    hdr, sp = spectra(outs[0], g.nout)
+    assert sp.shape == (nblk, g.nout)
+    for i in range(nblk):
+        blk = payload[i * g.block_bytes:(i + 1) * g.block_bytes]
+        assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk, nthreads=8).view(np.uint32))
+    assert dada.header_get(hdr, "NBIT", "%d") == 32
+    assert dada.header_get(hdr, "NPOL", "%d") == npol_out
+    assert dada.header_get(hdr, "NCHAN", "%d") == 336
+    assert abs(dada.header_get(hdr, "TSAMP", "%lf") - 8192 * 27 / 32) < 1e-6
+    log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
+    assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log
+
+
+def test_int8_header_layout_two_subbands(gpu, tmp_path):
+    # generic 256-chan int8 described by the input header; two sub-band
+    # chains (rings KEY and KEY+0x10), both on the one visible GPU
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 16)
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nUTC_START 2018-11-05-00:00:00\n"
+                     "NBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\nTSAMP 0.84375\n")
+    files, payloads = [], []
+    for r in range(2):
+        p = co.fill_synthetic(g, g.block_bytes * 2, SEED, r, 0)
+        f = tmp_path / f"sb{r}.dada"
+        dada.write_dada_file(str(f), "x 1\n", p)
+        files.append(str(f))
+        payloads.append(p)
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 16, 1, 1024, 256, 0x6c10, 0x6d10, str(hfile))
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, files, nsub=2, timeout=600)
+    for r in range(2):
+        hdr, sp = spectra(outs[r], 256)
+        assert sp.shape == (2, 256)
+        for i in range(2):
+            blk = payloads[r][i * g.block_bytes:(i + 1) * g.block_bytes]
+            assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk).view(np.uint32))
+        assert abs(dada.header_get(hdr, "TSAMP", "%lf") - 0.84375 * (1 << 16)) < 1e-6
+        assert dada.header_get(hdr, "NCHAN", "%d") == 256

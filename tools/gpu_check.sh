@@ -28,9 +28,17 @@ for s in $STEPS; do
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -q -rf ;;
     bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
+    benchnf) run bench_nofuse 600 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-fuse ;;
     bench5) run bench_c5 600 python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
     benchbmf) run bench_bmf 600 python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
+    bench2gloo) run bench_2gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 2 \
+            --dist-backend gloo ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
+    probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
+    tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
+          run tune_c5 600 python3 tools/tune.py --config c5 --quick &&
+          run tune_bmf 600 python3 tools/tune.py --config bmf --quick ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
             -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Launch-shape sweep for the integrate kernel, interleaved in ONE process
+(cdna_hip_programming.md §5.4 rule 24): every variant is opened as its own
+context (the knobs are read at b2p_open) and timed with dispatch-packet
+events over the same rotating HBM blocks, round after round.
+
+    python3 tools/tune.py --config c2 --rounds 3 > gpurun_out/tune_c2.json
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "paf-baseband2power_amd"))
+
+import paf_b2p  # noqa: E402
+from paf_b2p.geometry import CONFIGS  # noqa: E402
+
+KNOBS = ("B2P_MAX_THREADS", "B2P_UNROLL", "B2P_NT", "B2P_WG_PER_CU", "B2P_INTERLEAVE", "FUSE")
+
+
+def variants(quick: bool):
+    threads = [256, 512, 1024]
+    unroll = [4, 8, 16]
+    per_cu = [None, 1, 2, 4]
+    for t, u, p, il, fu in itertools.product(threads, unroll, per_cu, [0, 1], [0, 1]):
+        if quick and (p not in (None, 1) or u == 16):
+            continue
+        yield {"B2P_MAX_THREADS": t, "B2P_UNROLL": u, "B2P_NT": 1, "B2P_WG_PER_CU": p,
+               "B2P_INTERLEAVE": il, "FUSE": fu}
+
+
+def open_variant(geom, v):
+    for k in KNOBS:
+        os.environ.pop(k, None)
+        if v.get(k) is not None and k.startswith("B2P_"):
+            os.environ[k] = str(v[k])
+    it = paf_b2p.Integrator(geom)
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    return it
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--launches", type=int, default=12)
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    geom = CONFIGS[a.config]["geom"]()
+    base = paf_b2p.Integrator(geom)
+    bb = base.block_bytes
+    blocks = []
+    for b in range(4):
+        d = base.alloc(bb)
+        base.fill_synthetic(d, 20181105, 0, b)
+        blocks.append(d)
+    base.sync()
+    ref = None
+    vs = list(variants(a.quick))
+    res = {i: [] for i in range(len(vs))}
+    info = {}
+    for _ in range(a.rounds):
+        for i, v in enumerate(vs):
+            it = open_variant(geom, v)
+            info[i] = {"threads": it.info.threads, "grid": it.info.columns * it.info.row_groups}
+            dout = it.alloc(it.nout * 4)
+
+            def one(k):
+                if v["FUSE"]:
+                    it.integrate(blocks[k % 4], dout.ptr, True)
+                else:
+                    it.push(blocks[k % 4])
+                    it.finish_async(dout.ptr, True)
+            for k in range(2):
+                one(k)
+            it.sync()
+            it.set_timing(2)  # region timing: end-to-end time per integration
+            for k in range(a.launches):
+                one(k)
+            it.set_timing(0)
+            it.sync()
+            out = it.download(dout).view("float32")
+            dout.free()
+            st = it.stats()
+            if ref is None:
+                ref = out
+            assert (out.view("uint32") == ref.view("uint32")).all(), f"variant {v} differs"
+            res[i].append(st["kernel_ms"] / st["launches"])
+            it.close()
+    rows = []
+    for i, v in enumerate(vs):
+        ms = statistics.median(res[i])
+        rows.append({**{k: v[k] for k in KNOBS}, **info[i], "median_us": round(ms * 1e3, 2),
+                     "min_us": round(min(res[i]) * 1e3, 2), "GBps": round(bb / (ms * 1e-3) / 1e9, 1)})
+    rows.sort(key=lambda r: r["median_us"])
+    print(json.dumps({"config": a.config, "block_bytes": bb, "rounds": a.rounds, "variants": rows},
+                     indent=1))
+    for d in blocks:
+        d.free()
+    base.close()
+
+
+if __name__ == "__main__":
+    main()
