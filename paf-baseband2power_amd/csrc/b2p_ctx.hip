@@ -536,7 +536,7 @@ int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, f
                    "b2p_integrate needs exactly one integration (%llu B), got %zu",
                    (unsigned long long)c->block_bytes, nbytes);
   if (!is_device || !c->fuse) {  // staged / plain push, then the finalize kernel
-    int rc = b2p_push(c, buf, nbytes, 0);
+    int rc = b2p_push(c, buf, nbytes, is_device);
     if (rc != B2P_OK) return rc;
     return b2p_finish_async(c, out, out_is_device);
   }
