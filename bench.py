@@ -52,8 +52,11 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on one GPU (spectra gathered on the host)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed even at world size 1 (rehearses the "
+                         "RCCL gather path on one GPU)")
     ap.add_argument("--no-fuse", action="store_true",
-                    help="separate finalize launch per integration (b2p_push + b2p_finish_async)")
+                    help="use b2p_push + b2p_finish_async instead of b2p_integrate")
     return ap.parse_args()
 
 
@@ -103,8 +106,9 @@ def main():
     n_gpus = max(world, 1)
     cfg = CONFIGS[a.config]
     geom = cfg["geom"]()
-    rccl = world > 1 and a.dist_backend == "nccl"
-    if world > 1:
+    dist_on = world > 1 or a.force_dist
+    rccl = dist_on and a.dist_backend == "nccl"
+    if dist_on:
         D.init(a.dist_backend, local)
     subband = D.subband_of(rank)
     # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
@@ -141,16 +145,17 @@ def main():
 
     def step(k, out_row):
         dst = out_ptr + (out_row or 0) * nout * 4
-        if a.no_fuse or host_mode:  # push + separate finalize launch
+        if a.no_fuse or host_mode:  # the push / finish_async pair
             it.push(blocks[k % len(blocks)])
             it.finish_async(dst, True)
-        else:  # one launch per integration, the last workgroup emits the spectrum
+        else:  # b2p_integrate: one integrate launch per integration (its
+            # finalize rides on the next launch)
             it.integrate(blocks[k % len(blocks)], dst, True)
 
     for w in range(a.warmup):
         step(w, None)
     it.sync()
-    if world > 1:
+    if dist_on:
         if rccl:
             torch.cuda.synchronize()
         dist.barrier()
@@ -167,16 +172,16 @@ def main():
     if rccl:
         gathered = D.gather_spectra(out_t)  # RCCL all-gather of K x nout fp32
         torch.cuda.synchronize()
-    elif world > 1:
+    elif dist_on:
         host = it.download(out_buf, nbytes=a.steps * nout * 4).view("float32").reshape(a.steps, nout)
         gathered = D.gather_spectra(torch.from_numpy(host.copy()))
-    if world > 1:
+    if dist_on:
         dist.barrier()
     el = time.perf_counter() - t0
     st = it.stats()
 
-    el_max = D.max_over_ranks(el, "cuda" if rccl else "cpu") if world > 1 else el
-    if world > 1 and rank == 0:
+    el_max = D.max_over_ranks(el, "cuda" if rccl else "cpu") if dist_on else el
+    if dist_on and rank == 0:
         assert len(gathered) == world and all(g.shape == (a.steps, nout) for g in gathered)
 
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
@@ -211,7 +216,7 @@ def main():
                          else f"HBM-resident, {NBLOCKS} rotating blocks",
                 "parallelism": f"sub-band sharding x{n_gpus}" + (
                     (", RCCL all-gather of spectra" if rccl else ", gloo gather (rehearsal)")
-                    if world > 1 else ""),
+                    if dist_on else ""),
                 "launch": {"threads": it.info.threads, "columns": it.info.columns,
                            "row_groups": it.info.row_groups, "replicas": it.info.replicas,
                            "unroll": it.info.unroll, "nt_loads": bool(it.info.nontemporal)},
@@ -244,7 +249,7 @@ def main():
     if host_mode:
         it.unregister_host(blocks[0])
     it.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -46,9 +46,21 @@ struct b2p_ctx {
   uint32_t B = 0, Bpad = 0, S = 0, NC = 0, G = 0;
   uint32_t nchan = 0, nout = 0, nrep = 0;
   uint64_t frame_bytes = 0, block_bytes = 0;
+  // two replica sets: integration k sums into set k&1.  Its finalize is
+  // deferred and carried by ONE extra workgroup of the next integrate launch
+  // (which sums into the other set), so no finalize launch and no
+  // cross-stream dependency sits between two integrations; b2p_sync /
+  // b2p_finish flush a finalize that found no launch to ride on.
   unsigned long long *d_rep = nullptr;
-  uint32_t *d_ticket = nullptr;  // arrival counter of the in-launch finalize
+  uint32_t *d_ticket = nullptr;  // arrival counters of the in-launch finalize [2]
   float *d_out = nullptr;
+  int cur = 0;                   // replica set of the running integration
+  struct {
+    int valid;
+    int set;
+    float *dev_out;              // where the kernel writes the spectrum
+    float *host_out;             // non-null: D2H copy after it
+  } pend = {0, 0, nullptr, nullptr};
   uint32_t interleave = 0;
   int fuse = 0;  // b2p_integrate: finalize in the last workgroup (1) or a
                  // separate launch (0, measured faster: DESIGN.md)
@@ -279,16 +291,19 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "hipStreamCreate"));
   c->stream = c->own_stream;
-  // replicas, then the 4-B ticket (zeroed together; the in-launch finalize
-  // leaves both zero again)
-  const size_t rep_bytes = (size_t)c->nrep * c->nout * sizeof(unsigned long long) + 16;
+  // two replica sets, then the two 4-B tickets (zeroed together; every
+  // finalize leaves its set and ticket zero again)
+  const size_t set_words = (size_t)c->nrep * c->nout;
+  const size_t rep_bytes = 2 * set_words * sizeof(unsigned long long) + 16;
   if (hipMalloc(&c->d_rep, rep_bytes) != hipSuccess) return fail(set_err(c, B2P_ENOMEM, "hipMalloc replicas"));
-  c->d_ticket = (uint32_t *)(c->d_rep + (size_t)c->nrep * c->nout);
+  c->d_ticket = (uint32_t *)(c->d_rep + 2 * set_words);
+
   if (hipMalloc(&c->d_out, (size_t)c->nout * sizeof(float)) != hipSuccess)
     return fail(set_err(c, B2P_ENOMEM, "hipMalloc out"));
   if (hipMemsetAsync(c->d_rep, 0, rep_bytes, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "zero replicas"));
+
   *out = c;
   return B2P_OK;
 }
@@ -401,12 +416,22 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   a.nout = c->nout;
   a.nrep = c->nrep;
   a.interleave = c->interleave;
-  a.rep = c->d_rep;
+  a.rep = c->d_rep + (size_t)c->cur * c->nrep * c->nout;
   a.out = fused_out;
-  a.ticket = c->d_ticket;
+  a.ticket = c->d_ticket + c->cur;
   a.mean = c->g.mean;
   a.nsamp = (double)c->g.nsamp_int;
-  const uint32_t grid = c->NC * c->G;
+  uint32_t grid = c->NC * c->G;
+  a.nwork = grid;
+  // the previous integration's finalize rides on this launch (extra block)
+  a.fin_rep = nullptr;
+  a.fin_out = nullptr;
+  const bool carry = c->pend.valid;
+  if (carry) {
+    a.fin_rep = c->d_rep + (size_t)c->pend.set * c->nrep * c->nout;
+    a.fin_out = c->pend.dev_out;
+    grid += 1;
+  }
   EvPair p{nullptr, nullptr, nbytes, 0};
   if (c->timing == 2) {
     c->region_launches++;
@@ -419,6 +444,40 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   }
   CK(c, launch_integrate(a, c->kc, c->Bpad, grid, c->stream, p.a, p.b));
   if (c->timing == 1) c->pending.push_back(p);
+  if (carry) {
+    if (c->pend.host_out)
+      CK(c, hipMemcpyAsync(c->pend.host_out, c->pend.dev_out, (size_t)c->nout * sizeof(float),
+                           hipMemcpyDeviceToHost, c->stream));
+    c->pend.valid = 0;
+  }
+  return B2P_OK;
+}
+
+// A deferred finalize with no integrate launch to ride on: run it alone.
+static int flush_pending(b2p_ctx_t *c) {
+  if (!c->pend.valid) return B2P_OK;
+  FinalizeArgs f;
+  f.rep = c->d_rep + (size_t)c->pend.set * c->nrep * c->nout;
+  f.nrep = c->nrep;
+  f.nout = c->nout;
+  f.out = c->pend.dev_out;
+  f.mean = c->g.mean;
+  f.nsamp = (double)c->g.nsamp_int;
+  EvPair p{nullptr, nullptr, 0, 1};
+  if (c->timing == 2) {
+    c->region_finalizes++;
+  } else if (c->timing) {
+    if (c->pending.size() >= kTimingRing) drain_timing(c);
+    p.a = pool_event(c);
+    p.b = pool_event(c);
+    if (!p.a || !p.b) return set_err(c, B2P_EHIP, "hipEventCreate");
+  }
+  CK(c, launch_finalize(f, c->stream, p.a, p.b));
+  if (c->timing == 1) c->pending.push_back(p);
+  if (c->pend.host_out)
+    CK(c, hipMemcpyAsync(c->pend.host_out, c->pend.dev_out, (size_t)c->nout * sizeof(float),
+                         hipMemcpyDeviceToHost, c->stream));
+  c->pend.valid = 0;
   return B2P_OK;
 }
 
@@ -455,8 +514,8 @@ int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
                    (unsigned long long)samples, (unsigned long long)c->g.nsamp_int);
   CK(c, hipSetDevice(c->device));
   int rc;
+  if (is_device && (uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
   if (is_device) {
-    if ((uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
     if ((rc = enqueue_span(c, buf, nbytes, nullptr)) != B2P_OK) return rc;
   } else {
     if ((rc = ensure_staging(c)) != B2P_OK) return rc;
@@ -485,26 +544,14 @@ uint64_t b2p_samples_pending(const b2p_ctx_t *c) { return c ? c->samples : 0; }
 int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
   if (!c || !out) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));
-  FinalizeArgs f;
-  f.rep = c->d_rep;
-  f.nrep = c->nrep;
-  f.nout = c->nout;
-  f.out = out_is_device ? out : c->d_out;
-  f.mean = c->g.mean;
-  f.nsamp = (double)c->g.nsamp_int;
-  EvPair p{nullptr, nullptr, 0, 1};
-  if (c->timing == 2) {
-    c->region_finalizes++;
-  } else if (c->timing) {
-    if (c->pending.size() >= kTimingRing) drain_timing(c);
-    p.a = pool_event(c);
-    p.b = pool_event(c);
-    if (!p.a || !p.b) return set_err(c, B2P_EHIP, "hipEventCreate");
-  }
-  CK(c, launch_finalize(f, c->stream, p.a, p.b));
-  if (c->timing == 1) c->pending.push_back(p);
-  if (!out_is_device)
-    CK(c, hipMemcpyAsync(out, c->d_out, (size_t)c->nout * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  int rc = flush_pending(c);  // two finishes in a row: the first runs alone
+  if (rc != B2P_OK) return rc;
+  // defer: the next integrate launch (or b2p_sync) emits this integration
+  c->pend.valid = 1;
+  c->pend.set = c->cur;
+  c->pend.dev_out = out_is_device ? out : c->d_out;
+  c->pend.host_out = out_is_device ? nullptr : out;
+  c->cur ^= 1;
   const uint64_t got = c->samples;
   c->samples = 0;
   if (got != c->g.nsamp_int)
@@ -516,6 +563,8 @@ int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
 int b2p_sync(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));
+  int rc = flush_pending(c);
+  if (rc != B2P_OK) return rc;
   CK(c, hipStreamSynchronize(c->stream));
   return B2P_OK;
 }
@@ -543,17 +592,22 @@ int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, f
   if (!buf) return set_err(c, B2P_EINVAL, "null buffer");
   if ((uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
   CK(c, hipSetDevice(c->device));
+  // the launch finalizes its own set in its last workgroup; a deferred
+  // finalize of the previous integration rides on it as well
   int rc = enqueue_span(c, buf, nbytes, out_is_device ? out : c->d_out);
   if (rc != B2P_OK) return rc;
   if (!out_is_device)
     CK(c, hipMemcpyAsync(out, c->d_out, (size_t)c->nout * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  c->cur ^= 1;
   return B2P_OK;
 }
 
 int b2p_set_timing(b2p_ctx_t *c, int mode) {
   if (!c || mode < 0 || mode > 2) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));
-  if (c->timing == 2 && mode != 2) {  // close the region
+  if (c->timing == 2 && mode != 2) {  // close the region, last finalize included
+    int rc = flush_pending(c);
+    if (rc != B2P_OK) return rc;
     CK(c, hipEventRecord(c->region_b, c->stream));
     CK(c, hipEventSynchronize(c->region_b));
     float ms = 0.f;

@@ -34,6 +34,11 @@ struct IntegrateArgs {
   uint32_t *ticket;             // arrival counter, 0 between launches
   uint32_t mean;
   double nsamp;
+  // deferred finalize of the previous integration, done by the LAST
+  // workgroup of this launch (grid = NC*G + 1) when fin_out is set
+  unsigned long long *fin_rep;  // its replica set (re-zeroed)
+  float *fin_out;
+  uint32_t nwork;               // streaming workgroups (NC*G)
 };
 
 struct FinalizeArgs {

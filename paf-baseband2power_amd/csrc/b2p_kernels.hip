@@ -151,6 +151,20 @@ b2p_integrate_kernel(IntegrateArgs a) {
   const uint32_t t = threadIdx.x;
   for (uint32_t j = t; j < a.nout; j += blockDim.x) lds[j] = 0;
 
+  if (a.fin_out && blockIdx.x == gridDim.x - 1) {
+    // the previous integration's finalize (its set was completed by the
+    // previous launch on this stream; this launch sums into the other set)
+    __syncthreads();
+    const uint32_t nwords = a.nrep * a.nout;
+    for (uint32_t k = t; k < nwords; k += blockDim.x) {
+      const unsigned long long x = a.fin_rep[k];
+      if (x) atomicAdd(&lds[k % a.nout], x);
+      a.fin_rep[k] = 0;
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < a.nout; j += blockDim.x) a.fin_out[j] = to_output(lds[j], a.mean, a.nsamp);
+    return;
+  }
   const uint32_t col = blockIdx.x % a.NC;
   const uint32_t grp = blockIdx.x / a.NC;
   const bool active = t < a.B;
@@ -239,7 +253,7 @@ b2p_integrate_kernel(IntegrateArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t ticket =
         __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = ticket == gridDim.x - 1;
+    s_last = ticket == a.nwork - 1;  // the carried-finalize block takes no ticket
     if (s_last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -352,3 +352,39 @@ def test_integrate_device_span_is_one_launch(gpu):
         s = it.stats()
         assert s["launches"] == 1 and s["bytes"] == it.block_bytes
         d.free()
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_back_to_back_async_integrations(gpu, fuse):
+    # 7 integrations enqueued without a host sync: the two replica sets
+    # alternate and every finalize overlaps the next integrate (or runs in
+    # the last workgroup with B2P_FUSE=1); each spectrum must be exact
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 16)
+    os.environ["B2P_FUSE"] = str(fuse)
+    try:
+        with paf_b2p.Integrator(to_b2p(g)) as it:
+            blocks = []
+            for k in range(3):
+                d = it.alloc(g.block_bytes)
+                it.fill_synthetic(d, SEED, 9, k)
+                blocks.append(d)
+            out = it.alloc(7 * g.nout * 4)
+            for k in range(7):
+                it.integrate(blocks[k % 3], out.ptr + k * g.nout * 4, True)
+            it.sync()
+            got = it.download(out).view(np.float32).reshape(7, g.nout).copy()
+            # the push / finish_async form, also unsynchronised
+            for k in range(7):
+                it.push(blocks[k % 3])
+                it.finish_async(out.ptr + k * g.nout * 4, True)
+            it.sync()
+            got2 = it.download(out).view(np.float32).reshape(7, g.nout)
+            assert same_bits(got, got2)
+            hosts = [it.download(b) for b in blocks]
+            for b in blocks:
+                b.free()
+            out.free()
+    finally:
+        os.environ.pop("B2P_FUSE", None)
+    for k in range(7):
+        assert same_bits(got[k], co.power(g, hosts[k % 3])), k

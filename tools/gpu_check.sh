@@ -34,6 +34,9 @@ for s in $STEPS; do
     bench2gloo) run bench_2gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
             --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 2 \
             --dist-backend gloo ;;
+    benchdist1) run bench_dist1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+            --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 2 \
+            --cpu-seconds 0 --force-dist ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
