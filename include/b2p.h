@@ -165,6 +165,23 @@ int b2p_integrate(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device,
 /* Number of samples pushed into the current integration. */
 uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
 
+/* ---- multi-GPU gather ----
+ * N contexts in one process, one per GPU / sub-band (one host thread, one
+ * stream, one ring each).  Sub-bands never exchange data while they
+ * integrate; b2p_group_gather collects each member's finished spectrum
+ * (nout fp32 in that member's device memory) into root_out (n*nout fp32,
+ * sub-band-major, device memory of ctxs[0]) with RCCL over xGMI:
+ * ncclCommInitAll + ncclGather (rccl.h:236,745), enqueued on every member's
+ * stream behind its finalize; valid on ctxs[0] after b2p_group_sync().
+ * mode 0 = RCCL; mode 1 = peer copies (test rigs where members share a
+ * device, which RCCL refuses).  All members need the same nout. */
+typedef struct b2p_group b2p_group_t;
+int b2p_group_open(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode);
+int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);
+int b2p_group_sync(b2p_group_t *grp);
+const char *b2p_group_last_error(const b2p_group_t *grp); /* grp may be NULL */
+int b2p_group_close(b2p_group_t *grp);
+
 /* ---- measurement ----
  * mode 1: every integrate / finalize launch carries start/stop events on
  *   its own dispatch packet (hipExtLaunchKernel) -> exact per-launch times;

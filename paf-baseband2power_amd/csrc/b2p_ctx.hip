@@ -541,6 +541,18 @@ int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
 
 uint64_t b2p_samples_pending(const b2p_ctx_t *c) { return c ? c->samples : 0; }
 
+}  // extern "C"
+
+void *b2p_internal_stream(b2p_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
+
+int b2p_internal_flush(b2p_ctx_t *c) {
+  if (!c) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  return flush_pending(c);
+}
+
+extern "C" {
+
 int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
   if (!c || !out) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));

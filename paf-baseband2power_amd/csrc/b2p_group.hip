@@ -1,0 +1,146 @@
+// Multi-GPU gather of per-channel spectra (include/b2p.h "b2p_group").
+//
+// sub-bands shard with no exchange during the integrate; the
+// only collective is the final gather of each sub-band's spectrum to the
+// root device -- RCCL over xGMI (ncclCommInitAll + ncclGather,
+// /opt/rocm/include/rccl/rccl.h:236,745), issued on each context's own
+// stream so it is ordered behind that context's finalize.  Mode 1 replaces
+// RCCL with peer copies for rigs where several contexts share one device
+// (RCCL refuses duplicate devices in a communicator).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "b2p.h"
+#include "b2p_internal.h"
+
+struct b2p_group {
+  int n = 0;
+  int mode = 0;  // 0 RCCL, 1 device copies
+  std::vector<b2p_ctx_t *> ctx;
+  std::vector<int> dev;
+  std::vector<hipStream_t> stream;
+  std::vector<ncclComm_t> comm;
+  std::vector<hipEvent_t> done;  // mode 1: member r's spectrum is final
+  uint32_t nout = 0;
+  char err[256] = {0};
+};
+
+namespace {
+thread_local char g_gerr[256];
+int gerr(b2p_group_t *g, int code, const char *what, const char *detail) {
+  snprintf(g ? g->err : g_gerr, 256, "%s: %s", what, detail ? detail : "");
+  return code;
+}
+}  // namespace
+
+extern "C" {
+
+int b2p_group_open(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int mode) {
+  if (!out || !ctxs || n < 1 || (mode != 0 && mode != 1)) return B2P_EINVAL;
+  *out = nullptr;
+  b2p_group_t *g = new (std::nothrow) b2p_group_t();
+  if (!g) return B2P_ENOMEM;
+  g->n = n;
+  g->mode = mode;
+  for (int r = 0; r < n; ++r) {
+    b2p_info_t info;
+    if (!ctxs[r] || b2p_get_info(ctxs[r], &info) != B2P_OK) {
+      delete g;
+      return gerr(nullptr, B2P_EINVAL, "b2p_group_open", "null context");
+    }
+    if (r == 0) g->nout = info.nout;
+    if (info.nout != g->nout) {
+      delete g;
+      return gerr(nullptr, B2P_EINVAL, "b2p_group_open", "members differ in nout");
+    }
+    g->ctx.push_back(ctxs[r]);
+    g->dev.push_back((int)info.device);
+    g->stream.push_back((hipStream_t)b2p_internal_stream(ctxs[r]));
+  }
+  if (mode == 0) {
+    g->comm.resize(n);
+    ncclResult_t nr = ncclCommInitAll(g->comm.data(), n, g->dev.data());
+    if (nr != ncclSuccess) {
+      int rc = gerr(nullptr, B2P_EHIP, "ncclCommInitAll", ncclGetErrorString(nr));
+      delete g;
+      return rc;
+    }
+  } else {
+    g->done.resize(n, nullptr);
+    for (int r = 0; r < n; ++r) {
+      hipSetDevice(g->dev[r]);
+      if (hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming) != hipSuccess) {
+        b2p_group_close(g);
+        return gerr(nullptr, B2P_EHIP, "b2p_group_open", "hipEventCreate");
+      }
+    }
+  }
+  *out = g;
+  return B2P_OK;
+}
+
+int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
+  if (!g || !spectra || !root_out) return B2P_EINVAL;
+  // every member's deferred finalize must be enqueued before the gather
+  for (int r = 0; r < g->n; ++r) {
+    int rc = b2p_internal_flush(g->ctx[r]);
+    if (rc != B2P_OK) return gerr(g, rc, "flush", b2p_last_error(g->ctx[r]));
+  }
+  const size_t bytes = (size_t)g->nout * sizeof(float);
+  if (g->mode == 0) {
+    ncclResult_t nr = ncclGroupStart();
+    for (int r = 0; r < g->n && nr == ncclSuccess; ++r) {
+      hipSetDevice(g->dev[r]);
+      nr = ncclGather(spectra[r], r == 0 ? root_out : nullptr, g->nout, ncclFloat32, 0, g->comm[r],
+                      g->stream[r]);
+    }
+    ncclResult_t ne = ncclGroupEnd();
+    if (nr != ncclSuccess || ne != ncclSuccess)
+      return gerr(g, B2P_EHIP, "ncclGather", ncclGetErrorString(nr != ncclSuccess ? nr : ne));
+    return B2P_OK;
+  }
+  for (int r = 0; r < g->n; ++r) {
+    hipSetDevice(g->dev[r]);
+    if (hipEventRecord(g->done[r], g->stream[r]) != hipSuccess)
+      return gerr(g, B2P_EHIP, "hipEventRecord", "");
+  }
+  hipSetDevice(g->dev[0]);
+  for (int r = 0; r < g->n; ++r) {
+    if (hipStreamWaitEvent(g->stream[0], g->done[r], 0) != hipSuccess ||
+        hipMemcpyPeerAsync(root_out + (size_t)r * g->nout, g->dev[0], spectra[r], g->dev[r], bytes,
+                           g->stream[0]) != hipSuccess)
+      return gerr(g, B2P_EHIP, "hipMemcpyPeerAsync", "");
+  }
+  return B2P_OK;
+}
+
+int b2p_group_sync(b2p_group_t *g) {
+  if (!g) return B2P_EINVAL;
+  for (int r = 0; r < g->n; ++r) {
+    int rc = b2p_sync(g->ctx[r]);
+    if (rc != B2P_OK) return rc;
+  }
+  return B2P_OK;
+}
+
+const char *b2p_group_last_error(const b2p_group_t *g) { return g ? g->err : g_gerr; }
+
+int b2p_group_close(b2p_group_t *g) {
+  if (!g) return B2P_EINVAL;
+  for (auto c : g->comm)
+    if (c) ncclCommDestroy(c);
+  for (size_t r = 0; r < g->done.size(); ++r)
+    if (g->done[r]) {
+      hipSetDevice(g->dev[r]);
+      hipEventDestroy(g->done[r]);
+    }
+  delete g;
+  return B2P_OK;
+}
+
+}  // extern "C"

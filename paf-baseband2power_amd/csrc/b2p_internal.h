@@ -84,3 +84,8 @@ hipError_t launch_fill(uint4 *dst, uint64_t nvec, const FillArgs &f,
 uint64_t splitmix64_host(uint64_t x);
 
 }  // namespace b2p
+
+// library-internal hooks for b2p_group.hip (not part of include/b2p.h)
+struct b2p_ctx;
+void *b2p_internal_stream(struct b2p_ctx *ctx);  // the context's current stream
+int b2p_internal_flush(struct b2p_ctx *ctx);     // enqueue a deferred finalize

@@ -12,9 +12,15 @@
  * One input ring block is one integration (the ring is sized so:
  * paf-baseband2power.py:67 / conf:9, NDF 8192 x 48 x 7168 B = 1024x1024
  * samples).  A short final block (EOD) is skipped and logged.
+ *
+ * -n N (extension): N sub-bands in one process, sub-band r on
+ * ring key_in + 0x10*r and GPU d + r, one host thread + one stream each; after
+ * every integration the N spectra are gathered to GPU d over RCCL
+ * (b2p_group_gather) and written as one N*NCHAN block to key_out.
  */
 #include <getopt.h>
 #include <inttypes.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -26,15 +32,30 @@
 
 #define MSTR_LEN 512 /* paf_baseband2power.cuh:4 */
 #define TSAMP_BMF_US (27.0 / 32.0) /* README.md:2 */
+#define MAX_SUB 64
 
-typedef struct conf_t { /* baseband2power.cuh:18-23, plus layout options */
+typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
   int device_id;
   char dir[MSTR_LEN];
   key_t key_in, key_out;
   char layout[64];
   int npol_out;
   int mean;
+  int nsub;
 } conf_t;
+
+typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
+  int r;
+  key_t key;
+  int device;
+  dada_hdu_t *in;
+  b2p_ctx_t *ctx;
+  b2p_geom_t g;
+  double tsamp_us;
+  float *spec_dev; /* this sub-band's spectrum (device) */
+  uint64_t rbufsz;
+  int locked;
+} sub_t;
 
 static void usage(void) {
   fprintf(stdout,
@@ -50,6 +71,7 @@ static void usage(void) {
           "keys if they describe 8/16-bit baseband, else bmf)\n"
           " -p  Output pols: 1 = |X|^2+|Y|^2 (default), 2 = X and Y\n"
           " -m  Write the time average instead of the sum\n"
+          " -n  Number of sub-bands (rings key_in + 0x10*r, GPUs d + r), gathered to GPU d\n"
           " -h  show help\n");
 }
 
@@ -130,15 +152,108 @@ static int pick_geometry(const conf_t *conf, const char *hdr, uint64_t rbufsz, b
   return 0;
 }
 
+/* ---- the integration loop, one thread per sub-band ---------------------- */
+
+typedef struct shared_t {
+  conf_t *conf;
+  sub_t *sub;
+  int nsub;
+  multilog_t *log;
+  dada_hdu_t *out;
+  b2p_group_t *grp;
+  float *root_dev;  /* nsub*nout on sub[0]'s device */
+  float *spec_host; /* nsub*nout, pinned */
+  uint64_t nout, obytes;
+  pthread_barrier_t bar;
+  int have[MAX_SUB]; /* this round: 1 whole block, 0 partial, -1 end of data */
+  int failed;
+  uint64_t nblocks, nskipped;
+} shared_t;
+
+typedef struct worker_t {
+  shared_t *sh;
+  int r;
+} worker_t;
+
+static void *worker(void *arg) {
+  worker_t *w = (worker_t *)arg;
+  shared_t *sh = w->sh;
+  sub_t *s = &sh->sub[w->r];
+  for (;;) {
+    uint64_t bytes = 0, bid = 0;
+    char *blk = ipcio_open_block_read(s->in->data_block, &bytes, &bid);
+    sh->have[w->r] = !blk ? -1 : (bytes == s->rbufsz ? 1 : 0);
+    pthread_barrier_wait(&sh->bar); /* all sub-bands agree on this round */
+    int stop = sh->failed, skip = 0;
+    for (int r = 0; r < sh->nsub; r++) {
+      if (sh->have[r] < 0) stop = 1;
+      if (sh->have[r] == 0) skip = 1;
+    }
+    if (stop || skip) {
+      if (blk) ipcio_close_block_read(s->in->data_block, bytes);
+      if (w->r == 0 && skip && !stop) {
+        sh->nskipped++;
+        multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band block held %" PRIu64
+                 " of %" PRIu64 " B)", bytes, s->rbufsz);
+      }
+      pthread_barrier_wait(&sh->bar);
+      if (stop) break;
+      continue;
+    }
+    const double t0 = now_s();
+    int rc = b2p_push(s->ctx, blk, bytes, 0); /* returns once the block is copied */
+    ipcio_close_block_read(s->in->data_block, bytes);
+    if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
+                                            sh->nsub == 1 ? 0 : 1);
+    if (rc == B2P_OK && sh->nsub == 1) rc = b2p_sync(s->ctx);
+    if (rc != B2P_OK) {
+      multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", w->r, b2p_strerror(rc), b2p_last_error(s->ctx));
+      sh->failed = 1;
+    }
+    pthread_barrier_wait(&sh->bar); /* every spectrum of this round is enqueued */
+    if (w->r == 0 && !sh->failed) {
+      if (sh->nsub > 1) {
+        float *specs[MAX_SUB];
+        for (int r = 0; r < sh->nsub; r++) specs[r] = sh->sub[r].spec_dev;
+        rc = b2p_group_gather(sh->grp, specs, sh->root_dev);
+        if (rc == B2P_OK) rc = b2p_group_sync(sh->grp);
+        if (rc == B2P_OK) rc = b2p_memcpy(s->ctx, sh->spec_host, sh->root_dev, sh->obytes, 2);
+        if (rc != B2P_OK) {
+          multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
+          sh->failed = 1;
+        }
+      }
+      if (!sh->failed) {
+        char *o = ipcio_open_block_write(sh->out->data_block, &bid);
+        if (!o) {
+          sh->failed = 1;
+        } else {
+          memcpy(o, sh->spec_host, sh->obytes);
+          ipcio_close_block_write(sh->out->data_block, sh->obytes);
+          sh->nblocks++;
+          const double dt = now_s() - t0;
+          multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s per sub-band, "
+                   "%.1f Msamples/s in all", sh->nblocks, dt * 1e3, bytes / dt / 1e9,
+                   (double)sh->nsub * (sh->nout / s->g.npol_out) * s->g.npol * s->g.nsamp_int / dt / 1e6);
+        }
+      }
+    }
+    pthread_barrier_wait(&sh->bar);
+    if (sh->failed) break;
+  }
+  return NULL;
+}
+
 int main(int argc, char *argv[]) {
   int arg;
   conf_t conf;
   memset(&conf, 0, sizeof conf);
   conf.npol_out = 1;
+  conf.nsub = 1;
   strcpy(conf.dir, ".");
   int have_in = 0, have_out = 0;
 
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:mh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:mh")) != -1) {
     switch (arg) {
       case 'h':
         usage();
@@ -157,27 +272,16 @@ int main(int argc, char *argv[]) {
         }
         have_out = 1;
         break;
-      case 'c':
-        snprintf(conf.dir, sizeof conf.dir, "%s", optarg);
-        break;
-      case 'd':
-        sscanf(optarg, "%d", &conf.device_id);
-        break;
-      case 'f':
-        snprintf(conf.layout, sizeof conf.layout, "%s", optarg);
-        break;
-      case 'p':
-        conf.npol_out = atoi(optarg);
-        break;
-      case 'm':
-        conf.mean = 1;
-        break;
-      default:
-        usage();
-        return EXIT_FAILURE;
+      case 'c': snprintf(conf.dir, sizeof conf.dir, "%s", optarg); break;
+      case 'd': sscanf(optarg, "%d", &conf.device_id); break;
+      case 'f': snprintf(conf.layout, sizeof conf.layout, "%s", optarg); break;
+      case 'p': conf.npol_out = atoi(optarg); break;
+      case 'n': conf.nsub = atoi(optarg); break;
+      case 'm': conf.mean = 1; break;
+      default: usage(); return EXIT_FAILURE;
     }
   }
-  if (!have_in || !have_out) {
+  if (!have_in || !have_out || conf.nsub < 1 || conf.nsub > MAX_SUB) {
     usage();
     return EXIT_FAILURE;
   }
@@ -203,57 +307,72 @@ int main(int argc, char *argv[]) {
   }
   if (ndev == 1) conf.device_id = 0;
 
-  int status = EXIT_FAILURE;
-  b2p_ctx_t *ctx = NULL;
-  float *spec = NULL;
-  dada_hdu_t *in = dada_hdu_create(log), *out = dada_hdu_create(log);
-  dada_hdu_set_key(in, conf.key_in);
+  int status = EXIT_FAILURE, out_locked = 0;
+  shared_t sh;
+  memset(&sh, 0, sizeof sh);
+  sh.conf = &conf;
+  sh.nsub = conf.nsub;
+  sh.log = log;
+  sub_t sub[MAX_SUB];
+  memset(sub, 0, sizeof sub);
+  sh.sub = sub;
+  dada_hdu_t *out = dada_hdu_create(log);
   dada_hdu_set_key(out, conf.key_out);
-  int in_locked = 0, out_locked = 0;
-  uint64_t nblocks = 0, nskipped = 0;
+  sh.out = out;
+  int dup_dev = 0;
 
-  if (dada_hdu_connect(in) < 0 || dada_hdu_lock_read(in) < 0) {
-    multilog(log, LOG_ERR, "cannot attach/lock input ring %x", conf.key_in);
-    goto done;
-  }
-  in_locked = 1;
-  if (dada_hdu_open_read(in) < 0) {
-    multilog(log, LOG_ERR, "no header on input ring");
-    goto done;
-  }
-  const uint64_t rbufsz = ipcbuf_get_bufsz(&in->data_block->buf);
-  b2p_geom_t g;
-  double tsamp_us = TSAMP_BMF_US;
-  if (pick_geometry(&conf, in->header, rbufsz, &g, &tsamp_us, log) < 0) goto done;
-
-  int rc = b2p_open(&ctx, &g, conf.device_id);
-  if (rc != B2P_OK) {
-    multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
-    goto done;
+  for (int r = 0; r < conf.nsub; r++) {
+    sub_t *s = &sub[r];
+    s->r = r;
+    s->key = conf.key_in + 0x10 * r;
+    s->device = ndev == 1 ? 0 : (conf.device_id + r) % ndev;
+    if (r && s->device == sub[0].device) dup_dev = 1;
+    s->in = dada_hdu_create(log);
+    dada_hdu_set_key(s->in, s->key);
+    if (dada_hdu_connect(s->in) < 0 || dada_hdu_lock_read(s->in) < 0) {
+      multilog(log, LOG_ERR, "cannot attach/lock input ring %x", (unsigned)s->key);
+      goto done;
+    }
+    s->locked = 1;
+    if (dada_hdu_open_read(s->in) < 0) {
+      multilog(log, LOG_ERR, "no header on input ring %x", (unsigned)s->key);
+      goto done;
+    }
+    s->rbufsz = ipcbuf_get_bufsz(&s->in->data_block->buf);
+    if (pick_geometry(&conf, s->in->header, s->rbufsz, &s->g, &s->tsamp_us, log) < 0) goto done;
+    if (r && memcmp(&s->g, &sub[0].g, sizeof s->g)) {
+      multilog(log, LOG_ERR, "sub-band %d layout differs from sub-band 0", r);
+      goto done;
+    }
+    int rc = b2p_open(&s->ctx, &s->g, s->device);
+    if (rc != B2P_OK) {
+      multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
+      goto done;
+    }
+    /* pin the input ring's blocks for DMA (dada_cuda_dbregister role) */
+    for (uint64_t i = 0; i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
+      if (b2p_register_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i), s->rbufsz) != B2P_OK)
+        multilog(log, LOG_INFO, "register block %" PRIu64 ": %s", i, b2p_last_error(s->ctx));
   }
   b2p_info_t info;
-  b2p_get_info(ctx, &info);
+  b2p_get_info(sub[0].ctx, &info);
+  sh.nout = info.nout;
+  sh.obytes = (uint64_t)conf.nsub * info.nout * sizeof(float);
   multilog(log, LOG_INFO,
-           "layout nbit %u %s, %u chunks x %u chans x %u samp/DF, %u outputs, %" PRIu64
-           " samples per integration, GPU %d",
-           g.nbit, g.big_endian ? "BE" : "LE", g.nchunk, g.nchan_chunk, g.nsamp_df, info.nout,
-           g.nsamp_int, (int)info.device);
-  /* pin the input ring's blocks for DMA (dada_cuda_dbregister role) */
-  for (uint64_t i = 0; i < ipcbuf_get_nbufs(&in->data_block->buf); i++) {
-    rc = b2p_register_host(ctx, ipcbuf_get_buffer(&in->data_block->buf, i), rbufsz);
-    if (rc != B2P_OK) multilog(log, LOG_INFO, "register block %" PRIu64 ": %s", i, b2p_last_error(ctx));
-  }
+           "%d sub-band(s): nbit %u %s, %u chunks x %u chans x %u samp/DF, %u outputs each, "
+           "%" PRIu64 " samples per integration, first GPU %d",
+           conf.nsub, sub[0].g.nbit, sub[0].g.big_endian ? "BE" : "LE", sub[0].g.nchunk,
+           sub[0].g.nchan_chunk, sub[0].g.nsamp_df, info.nout, sub[0].g.nsamp_int, (int)info.device);
 
   if (dada_hdu_connect(out) < 0 || dada_hdu_lock_write(out) < 0) {
-    multilog(log, LOG_ERR, "cannot attach/lock output ring %x", conf.key_out);
+    multilog(log, LOG_ERR, "cannot attach/lock output ring %x", (unsigned)conf.key_out);
     goto done;
   }
   out_locked = 1;
-  const uint64_t obytes = (uint64_t)info.nout * sizeof(float);
-  if (ipcbuf_get_bufsz(&out->data_block->buf) != obytes) {
+  if (ipcbuf_get_bufsz(&out->data_block->buf) != sh.obytes) {
     /* same check as diskdb.cu:36-42, for the output ring (py:77-79) */
-    multilog(log, LOG_ERR, "output ring block %" PRIu64 " B != NCHAN x NPOL x 4 = %" PRIu64 " B",
-             ipcbuf_get_bufsz(&out->data_block->buf), obytes);
+    multilog(log, LOG_ERR, "output ring block %" PRIu64 " B != NSUB x NCHAN x NPOL x 4 = %" PRIu64 " B",
+             ipcbuf_get_bufsz(&out->data_block->buf), sh.obytes);
     goto done;
   }
 
@@ -263,21 +382,22 @@ int main(int argc, char *argv[]) {
     uint64_t ohsz = ipcbuf_get_bufsz(out->header_block);
     if (!ohdr) goto done;
     memset(ohdr, 0, ohsz);
-    memcpy(ohdr, in->header, in->header_size < ohsz ? in->header_size : ohsz);
+    memcpy(ohdr, sub[0].in->header, sub[0].in->header_size < ohsz ? sub[0].in->header_size : ohsz);
     ohdr[ohsz - 1] = 0;
-    const double tsamp_out = tsamp_us * (double)g.nsamp_int;
+    const double tsamp_out = sub[0].tsamp_us * (double)sub[0].g.nsamp_int;
     double tmpl = 0;
     if (ascii_header_get(ohdr, "TSAMP", "%lf", &tmpl) == 1 && tmpl != tsamp_out)
       multilog(log, LOG_INFO, "TSAMP %.6g us in the input header replaced by %.6f us "
-               "(= %.6f us x %" PRIu64 ")", tmpl, tsamp_out, tsamp_us, g.nsamp_int);
+               "(= %.6f us x %" PRIu64 ")", tmpl, tsamp_out, sub[0].tsamp_us, sub[0].g.nsamp_int);
     ascii_header_set(ohdr, "NBIT", "%d", 32);
     ascii_header_set(ohdr, "NDIM", "%d", 1);
-    ascii_header_set(ohdr, "NPOL", "%u", g.npol_out);
-    ascii_header_set(ohdr, "NCHAN", "%u", info.nchan);
+    ascii_header_set(ohdr, "NPOL", "%u", sub[0].g.npol_out);
+    ascii_header_set(ohdr, "NCHAN", "%u", conf.nsub * info.nchan);
     ascii_header_set(ohdr, "TSAMP", "%.6f", tsamp_out);
-    ascii_header_set(ohdr, "BYTES_PER_SECOND", "%.6f", obytes / (tsamp_out * 1e-6));
-    ascii_header_set(ohdr, "NSAMP_INT", "%" PRIu64, g.nsamp_int);
-    ascii_header_set(ohdr, "POWER_MODE", "%s", g.mean ? "MEAN" : "SUM");
+    ascii_header_set(ohdr, "BYTES_PER_SECOND", "%.6f", sh.obytes / (tsamp_out * 1e-6));
+    ascii_header_set(ohdr, "NSAMP_INT", "%" PRIu64, sub[0].g.nsamp_int);
+    ascii_header_set(ohdr, "POWER_MODE", "%s", sub[0].g.mean ? "MEAN" : "SUM");
+    if (conf.nsub > 1) ascii_header_set(ohdr, "NSUBBAND", "%d", conf.nsub);
     ascii_header_del(ohdr, "NCHUNK");
     ascii_header_del(ohdr, "NCHAN_CHUNK");
     ascii_header_del(ohdr, "NSAMP_DF");
@@ -285,59 +405,65 @@ int main(int argc, char *argv[]) {
     if (ipcbuf_mark_filled(out->header_block, ohsz) < 0) goto done;
   }
 
-  spec = aligned_alloc(4096, (obytes + 4095) / 4096 * 4096);
-  if (!spec) goto done;
-  b2p_register_host(ctx, spec, (obytes + 4095) / 4096 * 4096);
-
-  for (;;) {
-    uint64_t bytes = 0, bid = 0;
-    char *blk = ipcio_open_block_read(in->data_block, &bytes, &bid);
-    if (!blk) break; /* end of data */
-    if (bytes != rbufsz) {
-      multilog(log, LOG_INFO, "partial integration skipped: block %" PRIu64 " holds %" PRIu64
-               " of %" PRIu64 " B", bid, bytes, rbufsz);
-      ipcio_close_block_read(in->data_block, bytes);
-      nskipped++;
-      continue;
-    }
-    const double t0 = now_s();
-    rc = b2p_push(ctx, blk, bytes, 0); /* returns once the block is copied */
-    ipcio_close_block_read(in->data_block, bytes);
-    if (rc != B2P_OK) {
-      multilog(log, LOG_ERR, "b2p_push: %s (%s)", b2p_strerror(rc), b2p_last_error(ctx));
-      goto done;
-    }
-    rc = b2p_finish(ctx, spec);
-    if (rc != B2P_OK) {
-      multilog(log, LOG_ERR, "b2p_finish: %s (%s)", b2p_strerror(rc), b2p_last_error(ctx));
-      goto done;
-    }
-    char *o = ipcio_open_block_write(out->data_block, &bid);
-    if (!o) goto done;
-    memcpy(o, spec, obytes);
-    ipcio_close_block_write(out->data_block, obytes);
-    const double dt = now_s() - t0;
-    nblocks++;
-    multilog(log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s, %.1f Msamples/s",
-             nblocks, dt * 1e3, bytes / dt / 1e9,
-             (double)info.nchan * g.npol * g.nsamp_int / dt / 1e6);
+  {
+    const size_t hb = (sh.obytes + 4095) / 4096 * 4096;
+    sh.spec_host = aligned_alloc(4096, hb);
+    if (!sh.spec_host) goto done;
+    b2p_register_host(sub[0].ctx, sh.spec_host, hb);
   }
-  status = EXIT_SUCCESS;
+  if (conf.nsub > 1) {
+    for (int r = 0; r < conf.nsub; r++)
+      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, info.nout * sizeof(float)) != B2P_OK)
+        goto done;
+    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, sh.obytes) != B2P_OK) goto done;
+    b2p_ctx_t *ctxs[MAX_SUB];
+    for (int r = 0; r < conf.nsub; r++) ctxs[r] = sub[r].ctx;
+    /* RCCL needs distinct devices; members sharing one GPU use peer copies */
+    const char *gm = getenv("B2P_GATHER");
+    int mode = dup_dev || (gm && !strcmp(gm, "copy")) ? 1 : 0;
+    int rc = b2p_group_open(&sh.grp, ctxs, conf.nsub, mode);
+    if (rc != B2P_OK) {
+      multilog(log, LOG_ERR, "b2p_group_open: %s", b2p_group_last_error(NULL));
+      goto done;
+    }
+    multilog(log, LOG_INFO, "gather of %d sub-bands to GPU %d via %s", conf.nsub, sub[0].device,
+             mode ? "peer copies (shared device)" : "RCCL ncclGather");
+  }
+
+  {
+    pthread_barrier_init(&sh.bar, NULL, (unsigned)conf.nsub);
+    pthread_t th[MAX_SUB];
+    worker_t wk[MAX_SUB];
+    for (int r = 0; r < conf.nsub; r++) {
+      wk[r].sh = &sh;
+      wk[r].r = r;
+      pthread_create(&th[r], NULL, worker, &wk[r]);
+    }
+    for (int r = 0; r < conf.nsub; r++) pthread_join(th[r], NULL);
+    pthread_barrier_destroy(&sh.bar);
+  }
+  status = sh.failed ? EXIT_FAILURE : EXIT_SUCCESS;
 
 done:
   if (out_locked) dada_hdu_unlock_write(out); /* ends the output transfer (EOD) */
-  if (in_locked) dada_hdu_unlock_read(in);
-  if (ctx) {
-    for (uint64_t i = 0; in->data_block && i < ipcbuf_get_nbufs(&in->data_block->buf); i++)
-      b2p_unregister_host(ctx, ipcbuf_get_buffer(&in->data_block->buf, i));
-    if (spec) b2p_unregister_host(ctx, spec);
-    b2p_close(ctx);
+  if (sh.grp) b2p_group_close(sh.grp);
+  for (int r = 0; r < conf.nsub; r++) {
+    sub_t *s = &sub[r];
+    if (s->ctx) {
+      for (uint64_t i = 0; s->in && s->in->data_block && i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
+        b2p_unregister_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i));
+      if (r == 0 && sh.spec_host) b2p_unregister_host(s->ctx, sh.spec_host);
+      if (s->spec_dev) b2p_dev_free(s->ctx, s->spec_dev);
+      if (r == 0 && sh.root_dev) b2p_dev_free(s->ctx, sh.root_dev);
+      b2p_close(s->ctx);
+    }
+    if (s->locked) dada_hdu_unlock_read(s->in);
+    if (s->in) dada_hdu_destroy(s->in);
   }
-  free(spec);
-  dada_hdu_destroy(in);
+  free(sh.spec_host);
   dada_hdu_destroy(out);
   multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s",
-           nblocks, nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED");
+           sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED");
   multilog_close(log);
   fclose(fp_log);
   return status;

@@ -8,7 +8,7 @@ library is missing every entry point raises.
 from ._lib import B2PError, Geom, lib  # noqa: F401
 from .geometry import (CONFIGS, NSAMP_INT, TSAMP_US, bmf_geom, block_bytes,  # noqa: F401
                        frame_bytes, generic_geom, make_geom, nchan, samples_per_block)
-from .integrator import DeviceBuffer, Integrator, device_count  # noqa: F401
+from .integrator import DeviceBuffer, Group, Integrator, device_count  # noqa: F401
 
 __all__ = ["B2PError", "Geom", "Integrator", "DeviceBuffer", "CONFIGS", "bmf_geom",
            "generic_geom", "make_geom", "device_count", "lib"]

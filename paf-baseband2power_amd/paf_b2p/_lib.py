@@ -93,6 +93,11 @@ PROTOTYPES = {
     "b2p_dev_alloc": (C.c_int, [_P, C.POINTER(_P), C.c_size_t]),
     "b2p_dev_free": (C.c_int, [_P, _P]),
     "b2p_memcpy": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_int]),
+    "b2p_group_open": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int]),
+    "b2p_group_gather": (C.c_int, [_P, C.POINTER(_P), _P]),
+    "b2p_group_sync": (C.c_int, [_P]),
+    "b2p_group_last_error": (C.c_char_p, [_P]),
+    "b2p_group_close": (C.c_int, [_P]),
 }
 
 _lib = None

@@ -177,3 +177,35 @@ def device_count() -> int:
     n = C.c_int(0)
     rc = L.lib().b2p_device_count(C.byref(n))
     return n.value if rc == L.B2P_OK else 0
+
+
+class Group:
+    """b2p_group: gather the spectra of N Integrators (one per GPU /
+    sub-band) to the first one's device -- RCCL (mode 0) or peer copies
+    (mode 1, members sharing a device)."""
+
+    def __init__(self, members: list[Integrator], mode: int = 0):
+        self.members = members
+        arr = (C.c_void_p * len(members))(*[m._ctx.value for m in members])
+        self._g = C.c_void_p()
+        rc = L.lib().b2p_group_open(C.byref(self._g), arr, len(members), mode)
+        if rc != L.B2P_OK:
+            raise L.B2PError(rc, L.lib().b2p_group_last_error(None).decode(errors="replace"))
+
+    def gather(self, spectra_ptrs: list[int], root_out_ptr: int) -> None:
+        arr = (C.c_void_p * len(spectra_ptrs))(*spectra_ptrs)
+        rc = L.lib().b2p_group_gather(self._g, arr, C.c_void_p(root_out_ptr))
+        if rc != L.B2P_OK:
+            raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
+        L.check(L.lib().b2p_group_sync(self._g))
+
+    def close(self) -> None:
+        if self._g:
+            L.lib().b2p_group_close(self._g)
+            self._g = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -55,8 +55,13 @@ def _bin(name: str) -> str:
 
 def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
-        hfname: str | None = None, outfiles: list | None = None) -> list:
-    """Run the chains; returns the output file path of every sub-band."""
+        hfname: str | None = None, outfiles: list | None = None, gather: bool = False) -> list:
+    """Run the chains; returns the output file path of every sub-band (one
+    combined file with gather=True: one paf_baseband2power process serves all
+    sub-bands and gathers their spectra to its first GPU)."""
+    if gather:
+        return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
+                             timeout, hfname)
     c = read_conf(conf_path)
     hdr = hfname or c["diskdb_hfname"]
     if not os.path.isabs(hdr):
@@ -122,6 +127,73 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
             dada.destroy_ring(k)
 
 
+def _resolve_header(c, conf_path, hfname):
+    hdr = hfname or c["diskdb_hfname"]
+    if not os.path.isabs(hdr):
+        cand = [os.path.join(os.path.dirname(os.path.abspath(conf_path)), hdr),
+                os.path.join(CONF_DIR, hdr)]
+        hdr = next((p for p in cand if os.path.exists(p)), cand[0])
+    return hdr
+
+
+def _wait_all(procs, timeout):
+    t_end = time.time() + timeout
+    failed = None
+    while any(p.poll() is None for p in procs):
+        failed = next((p for p in procs if p.poll() not in (None, 0)), None)
+        if failed or time.time() > t_end:
+            break
+        time.sleep(0.05)
+    failed = failed or next((p for p in procs if p.poll() not in (None, 0)), None)
+    if failed is not None or any(p.poll() is None for p in procs):
+        for p in procs:  # stop the rest (exact PIDs we started)
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        msgs = [f"{p.args[0]}: rc={p.returncode} {p.stderr.read().decode(errors='replace')[-400:]}"
+                for p in procs]
+        raise RuntimeError("pipeline failed:\n" + "\n".join(msgs))
+
+
+def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, mean, timeout,
+                  hfname):
+    c = read_conf(conf_path)
+    hdr = _resolve_header(c, conf_path, hfname)
+    os.makedirs(directory, exist_ok=True)
+    kout = c["b2p_key"]
+    procs, keys = [], []
+    try:
+        dada.destroy_ring(kout)
+        dada.create_ring(kout, c["b2p_nbuf"], nsub * c["b2p_rbufsz"] * npol_out, c["b2p_nreader"])
+        keys.append(kout)
+        for r in range(nsub):
+            kin = c["diskdb_key"] + 0x10 * r
+            dada.destroy_ring(kin)
+            dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"])
+            keys.append(kin)
+        out = os.path.join(directory, "power.dada")
+        procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
+                                      stderr=subprocess.PIPE))
+        cmd = [_bin("paf_baseband2power"), "-a", f"{c['diskdb_key']:x}", "-b", f"{kout:x}",
+               "-c", directory, "-d", str(gpu), "-p", str(npol_out), "-n", str(nsub)]
+        if layout:
+            cmd += ["-f", layout]
+        if mean:
+            cmd.append("-m")
+        procs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE))
+        for r in range(nsub):
+            dfile = datafiles[r]
+            procs.append(subprocess.Popen(
+                [_bin("paf_diskdb"), "-a", f"{c['diskdb_key'] + 0x10 * r:x}",
+                 "-b", os.path.dirname(os.path.abspath(dfile)), "-c", os.path.basename(dfile),
+                 "-d", hdr, "-e", str(c["diskdb_sod"])], stderr=subprocess.PIPE))
+        _wait_all(procs, timeout)
+        return [out]
+    finally:
+        for k in keys:
+            dada.destroy_ring(k)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="baseband -> power pipeline (DADA rings)")
     ap.add_argument("-a", "--cfname", required=True, help="configuration file")
@@ -134,9 +206,12 @@ def main(argv=None) -> int:
     ap.add_argument("-g", "--layout", default="")
     ap.add_argument("-p", "--npol-out", type=int, default=1)
     ap.add_argument("-m", "--mean", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="one process for all sub-bands, spectra gathered to the first GPU")
     a = ap.parse_args(argv)
-    files = a.dfname if a.subbands > 1 else a.dfname[0]
-    outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean)
+    files = a.dfname if a.subbands > 1 or a.gather else a.dfname[0]
+    outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean,
+               gather=a.gather)
     print("\n".join(outs))
     return 0
 
