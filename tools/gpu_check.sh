@@ -39,6 +39,7 @@ for s in $STEPS; do
             --cpu-seconds 0 --force-dist ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
+    skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
           run tune_c5 600 python3 tools/tune.py --config c5 --quick &&
           run tune_bmf 600 python3 tools/tune.py --config bmf --quick ;;
