@@ -196,7 +196,7 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   c->FV = g->nchunk * c->IV;
   const uint32_t P = g->nchan_chunk / gcd_u(g->nchan_chunk, c->VW);
   c->CP = g->nchunk == 1 ? P : c->FV;
-  uint32_t maxT = g->nbit == 8 ? 512 : 256;
+  uint32_t maxT = g->nbit == 8 ? 512 : 448;
   if (const char *e = getenv("B2P_MAX_THREADS")) {
     int v = atoi(e);
     if (v >= 64 && v <= 1024) maxT = (uint32_t)v;
@@ -207,6 +207,9 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
     c->S = c->B;
     c->NC = 1;
   } else {
+    // the frame is split into NC = CP / B columns: the largest whole-wave B
+    // (multiple of 64) that divides the frame -- partial waves straddle
+    // 1-KiB lines and measured 10-15 % slower (BMF: 168 or 336 threads)
     uint32_t best = 0;
     for (uint32_t b = maxT / 64 * 64; b >= 64; b -= 64)
       if (c->CP % b == 0) { best = b; break; }
@@ -214,6 +217,10 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
       for (uint32_t b = maxT; b >= 128; --b)
         if (c->CP % b == 0) { best = b; break; }
     if (!best) return set_err(c, B2P_EINVAL, "no workgroup shape divides the %u-vector frame", c->CP);
+    if (const char *e = getenv("B2P_THREADS")) {  // tuning knob: exact divisor
+      int v = atoi(e);
+      if (v >= 64 && v <= 1024 && c->CP % (uint32_t)v == 0) best = (uint32_t)v;
+    }
     c->B = best;
     c->S = c->CP;
     c->NC = c->CP / c->B;
@@ -262,16 +269,18 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   c->frame_bytes = b2p_frame_bytes(g);
   c->kc.mode = c->mode;
   c->kc.npol_out = (int)g->npol_out;
-  // measured defaults (tools/tune.py, DESIGN.md "launch shape"): ~32 KiB of
-  // loads in flight per CU -- int8 512 threads x 4 rows, int16 256 x 8 --
-  // one workgroup per CU, contiguous row slices, non-temporal loads
-  c->kc.unroll = g->nbit == 8 ? 4 : 8;
+  // measured defaults (tools/tune.py, DESIGN.md "launch shape"): 28-32 KiB
+  // of loads in flight per CU -- 4 rows per lane; int8 512 threads with
+  // contiguous row slices, int16 (BMF) 448 threads with interleaved rows --
+  // one workgroup per CU, non-temporal loads
+  c->kc.unroll = 4;
   c->kc.nt = true;
   if (const char *e = getenv("B2P_UNROLL")) {
     int v = atoi(e);
     if (v == 4 || v == 8 || v == 16) c->kc.unroll = v;
   }
   if (const char *e = getenv("B2P_NT")) c->kc.nt = atoi(e) != 0;
+  c->interleave = g->nbit == 16 ? 1 : 0;
   if (const char *e = getenv("B2P_INTERLEAVE")) c->interleave = atoi(e) != 0;
   if (const char *e = getenv("B2P_FUSE")) c->fuse = atoi(e) != 0;
   c->block_bytes = b2p_block_bytes(g);

@@ -43,6 +43,7 @@ for s in $STEPS; do
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
           run tune_c5 600 python3 tools/tune.py --config c5 --quick &&
           run tune_bmf 600 python3 tools/tune.py --config bmf --quick ;;
+    tunebmf) run tune_bmf2 600 python3 tools/tune.py --config bmf --threads 168,256,336,448,512 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
             -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \

@@ -21,7 +21,15 @@ sys.path.insert(0, os.path.join(REPO, "paf-baseband2power_amd"))
 import paf_b2p  # noqa: E402
 from paf_b2p.geometry import CONFIGS  # noqa: E402
 
-KNOBS = ("B2P_MAX_THREADS", "B2P_UNROLL", "B2P_NT", "B2P_WG_PER_CU", "B2P_INTERLEAVE", "FUSE")
+KNOBS = ("B2P_MAX_THREADS", "B2P_UNROLL", "B2P_NT", "B2P_WG_PER_CU", "B2P_INTERLEAVE", "FUSE",
+         "B2P_THREADS")
+
+
+def frame_variants(threads):
+    """multi-column frames (BMF): exact workgroup sizes"""
+    for t, u, il in itertools.product(threads, [4, 8, 16], [0, 1]):
+        yield {"B2P_MAX_THREADS": 1024, "B2P_THREADS": t, "B2P_UNROLL": u, "B2P_NT": 1,
+               "B2P_WG_PER_CU": None, "B2P_INTERLEAVE": il, "FUSE": 0}
 
 
 def variants(quick: bool):
@@ -52,6 +60,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--launches", type=int, default=12)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--threads", default="", help="comma list of exact B2P_THREADS (BMF)")
     a = ap.parse_args()
     geom = CONFIGS[a.config]["geom"]()
     base = paf_b2p.Integrator(geom)
@@ -63,7 +72,8 @@ def main():
         blocks.append(d)
     base.sync()
     ref = None
-    vs = list(variants(a.quick))
+    vs = (list(frame_variants([int(x) for x in a.threads.split(",")])) if a.threads
+          else list(variants(a.quick)))
     res = {i: [] for i in range(len(vs))}
     info = {}
     for _ in range(a.rounds):
@@ -97,7 +107,7 @@ def main():
     rows = []
     for i, v in enumerate(vs):
         ms = statistics.median(res[i])
-        rows.append({**{k: v[k] for k in KNOBS}, **info[i], "median_us": round(ms * 1e3, 2),
+        rows.append({**{k: v.get(k) for k in KNOBS}, **info[i], "median_us": round(ms * 1e3, 2),
                      "min_us": round(min(res[i]) * 1e3, 2), "GBps": round(bb / (ms * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda r: r["median_us"])
     print(json.dumps({"config": a.config, "block_bytes": bb, "rounds": a.rounds, "variants": rows},
