@@ -200,6 +200,23 @@ int b2p_reset_stats(b2p_ctx_t *ctx);
 int b2p_fill_synthetic(b2p_ctx_t *ctx, void *dev, size_t nbytes, uint64_t seed,
                        uint32_t subband, uint64_t block, uint64_t elem0);
 int b2p_dev_alloc(b2p_ctx_t *ctx, void **dev, size_t bytes);
+
+/* ---- TFTFP assembly on the GPU (capture.c:527-547; include/b2p_df.h) ----
+ * Scatter a stream of ndf raw 7232-B data frames (64-B header + 7168-B
+ * payload, as received; device memory) into a payload-only TFTFP block of
+ * block_ndf x nchunk x 7168 B (device memory) at
+ * (idf_rel * nchunk + chunk) * 7168, idf_rel computed from each header
+ * relative to the reference frame (ref_idf, ref_sec) exactly as
+ * capture.c:566 does, chunk = chunk_of_df[i] (device, capture.c:571-584).
+ * Frames outside [0, block_ndf) or with chunk >= nchunk are not placed.
+ * counts (device, nchunk + 3 uint64, accumulated): frames placed per
+ * chunk, then frames before the block, after it, with a bad chunk.  Slots
+ * no frame reaches keep their previous bytes (as in the capture ring).
+ * Enqueued on the context's stream, so a b2p_push of the block is ordered
+ * after it. */
+int b2p_assemble(b2p_ctx_t *ctx, const void *dfs, uint64_t ndf, uint32_t df_bytes,
+                 const uint8_t *chunk_of_df, uint64_t ref_idf, uint64_t ref_sec, void *block,
+                 uint64_t block_ndf, uint32_t nchunk, unsigned long long *counts);
 int b2p_dev_free(b2p_ctx_t *ctx, void *dev);
 /* kind: 1 host->device, 2 device->host, 3 device->device; synchronous */
 int b2p_memcpy(b2p_ctx_t *ctx, void *dst, const void *src, size_t bytes, int kind);

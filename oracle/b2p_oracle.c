@@ -189,3 +189,45 @@ void orc_fill_synthetic(const orc_geom_t *g, uint8_t *buf, size_t nbytes,
     }
   }
 }
+
+/* ---------------------------------------------------------------------- */
+/* data frames: hdr.c:10-28, capture.c:527-568                              */
+
+static uint64_t be64_at(const uint8_t *p) {
+  uint64_t w = 0;
+  for (int k = 0; k < 8; k++) w |= (uint64_t)p[k] << (8 * k); /* host LE load */
+  return bswap64_restated(w);                                 /* bswap_64 */
+}
+
+void orc_df_decode(const uint8_t *df, orc_df_hdr_t *h) {
+  uint64_t w = be64_at(df);
+  h->idf = w & 0x00000000ffffffffULL;
+  h->sec = (w & 0x3fffffff00000000ULL) >> 32;
+  h->valid = (int)((w & 0x8000000000000000ULL) >> 63);
+  w = be64_at(df + 8);
+  h->epoch = (int)((w & 0x00000000fc000000ULL) >> 26);
+  w = be64_at(df + 16);
+  h->freq = (double)((w & 0x00000000ffff0000ULL) >> 16);
+  h->beam = (int)(w & 0x000000000000ffffULL);
+}
+
+int64_t orc_df_index(const orc_df_hdr_t *h, uint64_t ref_idf, uint64_t ref_sec) {
+  return (int64_t)h->idf + (int64_t)(h->sec - ref_sec) / 1.08E-4 - (int64_t)ref_idf;
+}
+
+void orc_assemble(const uint8_t *dfs, uint64_t ndf, uint32_t df_bytes, const uint8_t *chunk_of_df,
+                  uint64_t ref_idf, uint64_t ref_sec, uint8_t *block, uint64_t block_ndf,
+                  uint32_t nchunk, uint64_t *counts) {
+  for (uint64_t d = 0; d < ndf; d++) {
+    const uint8_t *df = dfs + d * df_bytes;
+    orc_df_hdr_t h;
+    orc_df_decode(df, &h);
+    const int64_t idf = orc_df_index(&h, ref_idf, ref_sec);
+    const uint32_t ifreq = chunk_of_df[d];
+    if (ifreq >= nchunk) { counts[nchunk + 2]++; continue; }
+    if (idf < 0) { counts[nchunk]++; continue; }
+    if ((uint64_t)idf >= block_ndf) { counts[nchunk + 1]++; continue; }
+    memcpy(block + ((uint64_t)idf * nchunk + ifreq) * 7168u, df + 64, 7168); /* capture.c:540-542 */
+    counts[ifreq]++;
+  }
+}

@@ -83,6 +83,24 @@ void orc_fill_synthetic(const orc_geom_t *g, uint8_t *buf, size_t nbytes,
 
 uint64_t orc_splitmix64(uint64_t x);
 
+/* ---- data frames (capture side) -------------------- */
+typedef struct orc_df_hdr { /* hdr_t, hdr.h:6-14 */
+  int valid;
+  uint64_t idf, sec;
+  int epoch, beam;
+  double freq;
+} orc_df_hdr_t;
+/* hdr_keys, hdr.c:10-28 (bswap_64 of the first three words) */
+void orc_df_decode(const uint8_t *df, orc_df_hdr_t *h);
+/* acquire_idf, capture.c:562-568 */
+int64_t orc_df_index(const orc_df_hdr_t *h, uint64_t ref_idf, uint64_t ref_sec);
+/* capture.c:527-547 placement of ndf frames (df_bytes each, 64-B header),
+ * in arrival order, into a payload-only block; counts[nchunk + 3] as
+ * b2p_assemble (include/b2p.h) */
+void orc_assemble(const uint8_t *dfs, uint64_t ndf, uint32_t df_bytes, const uint8_t *chunk_of_df,
+                  uint64_t ref_idf, uint64_t ref_sec, uint8_t *block, uint64_t block_ndf,
+                  uint32_t nchunk, uint64_t *counts);
+
 #ifdef __cplusplus
 }
 #endif

@@ -169,3 +169,54 @@ def fill_synthetic(g: Geom, nbytes: int, seed: int, subband: int, block: int,
         return np.clip(v, -128, 127).astype(np.int8).view(np.uint8)
     v = np.clip(v, -32768, 32767).astype(np.int16)
     return v.astype(">i2" if g.big_endian else "<i2").view(np.uint8)
+
+
+# ---------------------------------------------------------------- data frames
+# header words (hdr.c:10-28): w0 = idf | sec<<32 | valid<<63, w1 = epoch<<26,
+# w2 = beam | freq<<16, each stored big-endian (bswap_64 on read)
+
+DF_BYTES, DF_HDR, DF_PAYLOAD = 7232, 64, 7168
+
+
+def df_encode(idf, sec, valid=1, epoch=0, beam=0, freq=0) -> np.ndarray:
+    """[n, 64] uint8 headers for arrays of fields (the inverse of hdr_keys)."""
+    idf, sec = np.atleast_1d(np.asarray(idf, np.uint64)), np.atleast_1d(np.asarray(sec, np.uint64))
+    n = max(idf.size, sec.size)
+    b = lambda x: np.broadcast_to(np.asarray(x, np.uint64), (n,))  # noqa: E731
+    w0 = (b(idf) & np.uint64(0xFFFFFFFF)) | ((b(sec) & np.uint64(0x3FFFFFFF)) << np.uint64(32)) \
+        | ((b(valid) & np.uint64(1)) << np.uint64(63))
+    w1 = (b(epoch) & np.uint64(0x3F)) << np.uint64(26)
+    w2 = (b(beam) & np.uint64(0xFFFF)) | ((b(freq) & np.uint64(0xFFFF)) << np.uint64(16))
+    out = np.zeros((n, DF_HDR), dtype=np.uint8)
+    out[:, 0:24] = np.stack([w0, w1, w2], axis=1).astype(">u8").view(np.uint8).reshape(n, 24)
+    return out
+
+
+def df_decode(hdrs: np.ndarray) -> dict:
+    w = np.ascontiguousarray(hdrs[..., :24]).view(">u8").astype(np.uint64).reshape(-1, 3)
+    return {"idf": w[:, 0] & np.uint64(0xFFFFFFFF),
+            "sec": (w[:, 0] >> np.uint64(32)) & np.uint64(0x3FFFFFFF),
+            "valid": w[:, 0] >> np.uint64(63),
+            "epoch": (w[:, 1] >> np.uint64(26)) & np.uint64(0x3F),
+            "freq": (w[:, 2] >> np.uint64(16)) & np.uint64(0xFFFF),
+            "beam": w[:, 2] & np.uint64(0xFFFF)}
+
+
+def df_stream(block: np.ndarray, nchunk: int, ref_idf: int, ref_sec: int, order=None,
+              beam: int = 0, epoch: int = 0, freq0: int = 1300, ndf_period: int = 250000,
+              period_sec: int = 27):
+    """Disassemble a payload-only TFTFP block into (dfs [n, 7232], chunk_of_df [n]),
+    frames numbered from the reference (wrapping into the next 27-s period as
+    sync.c:119-125 does); `order` permutes / drops frames (arrival order)."""
+    nf = block.size // (nchunk * DF_PAYLOAD)
+    pay = block.reshape(nf * nchunk, DF_PAYLOAD)
+    k = np.arange(nf * nchunk)
+    t, c = k // nchunk, k % nchunk
+    gidf = ref_idf + t
+    idf, sec = gidf % ndf_period, ref_sec + (gidf // ndf_period) * period_sec
+    hdr = df_encode(idf, sec, 1, epoch, beam, freq0 + c)
+    dfs = np.concatenate([hdr, pay], axis=1)
+    chunk = c.astype(np.uint8)
+    if order is not None:
+        dfs, chunk = dfs[order], chunk[order]
+    return np.ascontiguousarray(dfs), np.ascontiguousarray(chunk)

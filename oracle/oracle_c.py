@@ -114,3 +114,19 @@ def ref_hdr_lib():
     L.hdr_keys.argtypes = [C.c_void_p, C.POINTER(HdrT)]
     L.hdr_keys.restype = C.c_int
     return L
+
+
+def assemble(dfs: np.ndarray, chunk_of_df: np.ndarray, ref_idf: int, ref_sec: int,
+             block: np.ndarray, block_ndf: int, nchunk: int, counts: np.ndarray | None = None):
+    """orc_assemble (capture.c:527-547 placement) into `block` in place."""
+    L = lib()
+    L.orc_assemble.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64,
+                               C.c_uint64, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
+    dfs = np.ascontiguousarray(dfs, dtype=np.uint8)
+    chunk_of_df = np.ascontiguousarray(chunk_of_df, dtype=np.uint8)
+    if counts is None:
+        counts = np.zeros(nchunk + 3, dtype=np.uint64)
+    ndf = dfs.size // 7232
+    L.orc_assemble(_ptr(dfs), ndf, 7232, _ptr(chunk_of_df), ref_idf, ref_sec, _ptr(block),
+                   block_ndf, nchunk, _ptr(counts))
+    return counts

@@ -338,22 +338,22 @@ static void drain_timing(b2p_ctx_t *c) {
 
 int b2p_close(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  if (c->copy_stream) hipStreamSynchronize(c->copy_stream);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   drain_timing(c);
-  for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
-    if (c->d_stage[i]) hipFree(c->d_stage[i]);
-    if (c->ev_copied[i]) hipEventDestroy(c->ev_copied[i]);
-    if (c->ev_consumed[i]) hipEventDestroy(c->ev_consumed[i]);
+    if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
+    if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+    if (c->ev_consumed[i]) (void)hipEventDestroy(c->ev_consumed[i]);
   }
-  if (c->d_rep) hipFree(c->d_rep);
-  if (c->d_out) hipFree(c->d_out);
-  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
-  if (c->region_a) hipEventDestroy(c->region_a);
-  if (c->region_b) hipEventDestroy(c->region_b);
-  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  if (c->d_rep) (void)hipFree(c->d_rep);
+  if (c->d_out) (void)hipFree(c->d_out);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->region_a) (void)hipEventDestroy(c->region_a);
+  if (c->region_b) (void)hipEventDestroy(c->region_b);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return B2P_OK;
 }
@@ -681,6 +681,31 @@ int b2p_fill_synthetic(b2p_ctx_t *c, void *dev, size_t nbytes, uint64_t seed, ui
   f.nchan = c->nchan;
   f.amp = c->g.nbit == 8 ? 35 : 3464;
   CK(c, launch_fill((uint4 *)dev, nbytes / 16, f, c->stream));
+  return B2P_OK;
+}
+
+int b2p_assemble(b2p_ctx_t *c, const void *dfs, uint64_t ndf, uint32_t df_bytes,
+                 const uint8_t *chunk_of_df, uint64_t ref_idf, uint64_t ref_sec, void *block,
+                 uint64_t block_ndf, uint32_t nchunk, unsigned long long *counts) {
+  if (!c || (ndf && (!dfs || !chunk_of_df)) || !block || !counts) return B2P_EINVAL;
+  if (df_bytes != 7232 || !nchunk || nchunk > 256 || !block_ndf)
+    return set_err(c, B2P_EINVAL, "b2p_assemble: 7232-B frames, 1..256 chunks");
+  if ((uintptr_t)dfs % 16 || (uintptr_t)block % 16)
+    return set_err(c, B2P_EALIGN, "b2p_assemble: 16-B aligned buffers");
+  CK(c, hipSetDevice(c->device));
+  AssembleArgs a;
+  a.dfs = (const unsigned char *)dfs;
+  a.ndf = ndf;
+  a.df_bytes = df_bytes;
+  a.hdr_bytes = 64;
+  a.chunk_of_df = chunk_of_df;
+  a.ref_idf = ref_idf;
+  a.ref_sec = ref_sec;
+  a.block = (unsigned char *)block;
+  a.block_ndf = block_ndf;
+  a.nchunk = nchunk;
+  a.counts = counts;
+  CK(c, launch_assemble(a, c->stream));
   return B2P_OK;
 }
 

@@ -73,7 +73,7 @@ int b2p_group_open(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int mode) {
   } else {
     g->done.resize(n, nullptr);
     for (int r = 0; r < n; ++r) {
-      hipSetDevice(g->dev[r]);
+      (void)hipSetDevice(g->dev[r]);
       if (hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming) != hipSuccess) {
         b2p_group_close(g);
         return gerr(nullptr, B2P_EHIP, "b2p_group_open", "hipEventCreate");
@@ -95,7 +95,7 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
   if (g->mode == 0) {
     ncclResult_t nr = ncclGroupStart();
     for (int r = 0; r < g->n && nr == ncclSuccess; ++r) {
-      hipSetDevice(g->dev[r]);
+      (void)hipSetDevice(g->dev[r]);
       nr = ncclGather(spectra[r], r == 0 ? root_out : nullptr, g->nout, ncclFloat32, 0, g->comm[r],
                       g->stream[r]);
     }
@@ -105,11 +105,11 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
     return B2P_OK;
   }
   for (int r = 0; r < g->n; ++r) {
-    hipSetDevice(g->dev[r]);
+    (void)hipSetDevice(g->dev[r]);
     if (hipEventRecord(g->done[r], g->stream[r]) != hipSuccess)
       return gerr(g, B2P_EHIP, "hipEventRecord", "");
   }
-  hipSetDevice(g->dev[0]);
+  (void)hipSetDevice(g->dev[0]);
   for (int r = 0; r < g->n; ++r) {
     if (hipStreamWaitEvent(g->stream[0], g->done[r], 0) != hipSuccess ||
         hipMemcpyPeerAsync(root_out + (size_t)r * g->nout, g->dev[0], spectra[r], g->dev[r], bytes,
@@ -136,8 +136,8 @@ int b2p_group_close(b2p_group_t *g) {
     if (c) ncclCommDestroy(c);
   for (size_t r = 0; r < g->done.size(); ++r)
     if (g->done[r]) {
-      hipSetDevice(g->dev[r]);
-      hipEventDestroy(g->done[r]);
+      (void)hipSetDevice(g->dev[r]);
+      (void)hipEventDestroy(g->done[r]);
     }
   delete g;
   return B2P_OK;

@@ -63,6 +63,21 @@ struct FillArgs {
   int32_t amp;
 };
 
+// TFTFP assembly of a raw data-frame stream (b2p_assemble)
+struct AssembleArgs {
+  const unsigned char *dfs;     // ndf frames of df_bytes (header + payload)
+  uint64_t ndf;
+  uint32_t df_bytes;            // 7232
+  uint32_t hdr_bytes;           // 64
+  const uint8_t *chunk_of_df;   // per frame: chunk (ifreq) index
+  uint64_t ref_idf, ref_sec;    // reference frame of the block
+  unsigned char *block;         // block_ndf x nchunk x 7168 B
+  uint64_t block_ndf;
+  uint32_t nchunk;
+  unsigned long long *counts;   // nchunk placed, then before / after / bad chunk
+};
+hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s);
+
 // which instantiation of the integrate kernel runs
 struct KernelChoice {
   int mode;       // Mode

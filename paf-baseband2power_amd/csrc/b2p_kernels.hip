@@ -352,6 +352,58 @@ __global__ void __launch_bounds__(256) b2p_fill_kernel(uint4 *dst, uint64_t nvec
   }
 }
 
+// ---- TFTFP assembly of a raw DF stream (capture.c:527-547) ------------------
+// One wave per data frame: every lane reads the (broadcast) 24-B header and
+// computes the frame index itself (capture.c:566, same double arithmetic),
+// so no barrier is needed; the 7168-B payload moves as 7 x 1 KiB wave loads
+// and stores to (idf * nchunk + chunk) * 7168.  Per-chunk counts go through
+// LDS and leave with one atomic per counter per workgroup.
+__global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
+  __shared__ unsigned long long cnt[256 + 3];
+  const uint32_t ncnt = a.nchunk + 3;
+  for (uint32_t j = threadIdx.x; j < ncnt; j += blockDim.x) cnt[j] = 0;
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t d = wave; d < a.ndf; d += nwaves) {
+    const unsigned char *df = a.dfs + d * (uint64_t)a.df_bytes;
+    const uint64_t w0 = __builtin_bswap64(*(const uint64_t *)df);  // hdr.c:15-18
+    const uint64_t idf = w0 & 0x00000000ffffffffULL;
+    const uint64_t sec = (w0 & 0x3fffffff00000000ULL) >> 32;
+    const int64_t rel = (int64_t)idf + (int64_t)(sec - a.ref_sec) / 1.08E-4 - (int64_t)a.ref_idf;
+    const uint32_t chunk = a.chunk_of_df[d];
+    uint32_t slot;
+    if (chunk >= a.nchunk) slot = a.nchunk + 2;
+    else if (rel < 0) slot = a.nchunk;
+    else if ((uint64_t)rel >= a.block_ndf) slot = a.nchunk + 1;
+    else slot = chunk;
+    if (lane == 0) atomicAdd(&cnt[slot], 1ull);
+    if (slot >= a.nchunk) continue;  // wave-uniform
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(df + a.hdr_bytes);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(a.block + ((uint64_t)rel * a.nchunk + chunk) * 7168ull);
+    u32x4 v[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) v[k] = __builtin_nontemporal_load(src + k * 64 + lane);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(v[k], dst + k * 64 + lane);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < ncnt; j += blockDim.x)
+    if (cnt[j]) atomicAdd(&a.counts[j], cnt[j]);
+}
+
+hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s) {
+  if (a.nchunk > 256) return hipErrorInvalidValue;
+  uint64_t blocks = (a.ndf + 3) / 4;  // 4 waves per workgroup
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return hipSuccess;
+  AssembleArgs arg = a;
+  void *args[] = {&arg};
+  return hipLaunchKernel(reinterpret_cast<const void *>(b2p_assemble_kernel), dim3((uint32_t)blocks),
+                         dim3(256), args, 0, s);
+}
+
 // ---- launchers --------------------------------------------------------------
 typedef void (*IntegrateFn)(IntegrateArgs);
 

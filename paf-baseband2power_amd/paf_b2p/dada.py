@@ -214,3 +214,59 @@ def read_dada_file(path: str):
         hdr = f.read(HDR_SIZE)
         data = np.frombuffer(f.read(), dtype=np.uint8)
     return hdr.split(b"\0", 1)[0], data
+
+
+# ---- BMF data-frame headers (include/b2p_df.h) ---------------------------------
+
+class DfHdr(C.Structure):
+    """b2p_df_hdr_t (= hdr_t, hdr.h:6-14)"""
+    _fields_ = [("valid", C.c_int), ("idf", C.c_uint64), ("sec", C.c_uint64),
+                ("epoch", C.c_int), ("beam", C.c_int), ("freq", C.c_double)]
+
+
+def _df_lib():
+    L = dlib()
+    if not getattr(L, "_df_ready", False):
+        L.b2p_df_decode.argtypes = [C.c_void_p, C.POINTER(DfHdr)]
+        L.b2p_df_decode.restype = None
+        L.b2p_df_encode.argtypes = [C.POINTER(DfHdr), C.c_void_p]
+        L.b2p_df_encode.restype = None
+        L.b2p_df_index.argtypes = [C.POINTER(DfHdr), C.POINTER(DfHdr)]
+        L.b2p_df_index.restype = C.c_int64
+        L.b2p_df_ref_advance.argtypes = [C.POINTER(DfHdr), C.c_uint64]
+        L.b2p_df_ref_advance.restype = None
+        L.b2p_df_chunk_from_ip.argtypes = [C.c_uint32]
+        L.b2p_df_chunk_from_ip.restype = C.c_int
+        L._df_ready = True
+    return L
+
+
+def df_decode(df: bytes) -> DfHdr:
+    h = DfHdr()
+    buf = C.create_string_buffer(bytes(df[:64]), 64)
+    _df_lib().b2p_df_decode(buf, C.byref(h))
+    return h
+
+
+def df_encode(idf: int, sec: int, valid: int = 1, epoch: int = 0, beam: int = 0,
+              freq: float = 0.0) -> bytes:
+    h = DfHdr(valid, idf, sec, epoch, beam, freq)
+    buf = C.create_string_buffer(64)
+    _df_lib().b2p_df_encode(C.byref(h), buf)
+    return buf.raw
+
+
+def df_index(hdr: DfHdr, ref: DfHdr) -> int:
+    return int(_df_lib().b2p_df_index(C.byref(hdr), C.byref(ref)))
+
+
+def df_ref_advance(ref: DfHdr, ndf: int) -> DfHdr:
+    r = DfHdr(ref.valid, ref.idf, ref.sec, ref.epoch, ref.beam, ref.freq)
+    _df_lib().b2p_df_ref_advance(C.byref(r), ndf)
+    return r
+
+
+def df_chunk_from_ip(a: int, b: int, c: int, d: int) -> int:
+    """chunk of the sender a.b.c.d (sin_addr.s_addr as stored, network order)"""
+    s_addr = a | (b << 8) | (c << 16) | (d << 24)  # bytes in memory: a, b, c, d
+    return int(_df_lib().b2p_df_chunk_from_ip(s_addr))

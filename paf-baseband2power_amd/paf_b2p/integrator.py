@@ -141,6 +141,15 @@ class Integrator:
         L.check(L.lib().b2p_fill_synthetic(self._ctx, C.c_void_p(d.ptr + offset), n, seed, subband,
                                            block, elem0), self._ctx)
 
+    def assemble(self, dfs: DeviceBuffer, ndf: int, chunk_of_df: DeviceBuffer, ref_idf: int,
+                 ref_sec: int, block: DeviceBuffer, block_ndf: int, nchunk: int,
+                 counts: DeviceBuffer) -> None:
+        """b2p_assemble: scatter raw 7232-B data frames into a TFTFP block."""
+        L.check(L.lib().b2p_assemble(self._ctx, C.c_void_p(dfs.ptr), ndf, 7232,
+                                     C.c_void_p(chunk_of_df.ptr), ref_idf, ref_sec,
+                                     C.c_void_p(block.ptr), block_ndf, nchunk,
+                                     C.c_void_p(counts.ptr)), self._ctx)
+
     # ---- measurement -------------------------------------------------------------
     def set_timing(self, mode: int | bool) -> None:
         """0 off, 1 per-launch events, 2 one event pair around a region."""

@@ -1,0 +1,105 @@
+"""BMF data-frame headers and TFTFP placement (CPU).
+
+The decode is pinned by the reference's own hdr.c (tests/golden/hdr_pin.npz:
+hdr_keys outputs on random headers, hdr.c:10-28); frame index, reference
+advance and chunk-from-IP restate capture.c:562-584 and sync.c:119-125.
+"""
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+from conftest import load_golden
+from paf_b2p import dada
+
+
+def test_decode_matches_reference_hdr_c():
+    d = load_golden("hdr_pin")
+    for i in range(d["df_headers"].shape[0]):
+        h = dada.df_decode(d["df_headers"][i].tobytes())
+        assert [h.valid, h.idf, h.sec, h.epoch, h.beam] == [int(x) for x in
+                                                             d["valid_idf_sec_epoch_beam"][i]]
+        assert h.freq == d["freq"][i]
+
+
+def test_encode_decode_roundtrip_and_reference():
+    rng = np.random.default_rng(7)
+    L = co.ref_hdr_lib()
+    for _ in range(300):
+        f = dict(idf=int(rng.integers(0, 2 ** 32)), sec=int(rng.integers(0, 2 ** 30)),
+                 valid=int(rng.integers(0, 2)), epoch=int(rng.integers(0, 64)),
+                 beam=int(rng.integers(0, 2 ** 16)), freq=float(rng.integers(0, 2 ** 16)))
+        raw = dada.df_encode(**f)
+        h = dada.df_decode(raw)
+        assert (h.idf, h.sec, h.valid, h.epoch, h.beam, h.freq) == tuple(f.values())
+        # the NumPy restatement encodes the same bytes
+        assert raw == npo.df_encode(f["idf"], f["sec"], f["valid"], f["epoch"], f["beam"],
+                                    int(f["freq"])).tobytes()
+        if L is not None:  # and the reference's own decoder reads them back
+            r = co.HdrT()
+            buf = np.frombuffer(raw, dtype=np.uint8).copy()
+            L.hdr_keys(buf.ctypes.data, r)
+            assert (r.idf, r.sec, r.valid, r.epoch, r.beam, r.freq) == tuple(f.values())
+
+
+def _index_restated(idf, sec, ridf, rsec):
+    # capture.c:566 in Python floats (IEEE double, as C)
+    secdiff = (sec - rsec) % 2 ** 64
+    if secdiff >= 2 ** 63:
+        secdiff -= 2 ** 64
+    v = float(idf) + float(secdiff) / 1.08E-4 - float(ridf)
+    return int(v)  # C conversion truncates toward zero
+
+
+@pytest.mark.parametrize("idf,sec,ridf,rsec", [
+    (100, 54, 90, 54), (5, 81, 249990, 54), (249995, 54, 10, 81), (0, 0, 0, 0),
+    (7, 27 * 1000, 3, 27 * 999), (12, 3, 0, 0), (0, 54, 249999, 27)])
+def test_frame_index_restates_capture(idf, sec, ridf, rsec):
+    h, r = dada.DfHdr(1, idf, sec, 0, 0, 0.0), dada.DfHdr(1, ridf, rsec, 0, 0, 0.0)
+    assert dada.df_index(h, r) == _index_restated(idf, sec, ridf, rsec)
+
+
+def test_ref_advance_wraps_period():
+    r = dada.DfHdr(1, 249000, 54, 0, 0, 0.0)
+    a = dada.df_ref_advance(r, 8192)  # sync.c:119-125
+    assert (a.idf, a.sec) == (249000 + 8192 - 250000, 81)
+    b = dada.df_ref_advance(dada.DfHdr(1, 10, 54, 0, 0, 0.0), 8192)
+    assert (b.idf, b.sec) == (8202, 54)
+    # the index of a frame stays the same measured from either reference
+    h = dada.DfHdr(1, 7000, 81, 0, 0, 0.0)
+    assert dada.df_index(h, r) == dada.df_index(h, a) + 8192
+
+
+def test_chunk_from_ip_table():
+    # capture.c:573-580: BMFs 10.16.X.1..12, X = 1..8; links 1,3,5,... carry chunks
+    got = {}
+    for x in range(1, 9):
+        for y in range(1, 13):
+            got[(x, y)] = dada.df_chunk_from_ip(10, 16, x, y)
+    assert got[(1, 1)] == 0 and got[(1, 2)] == 0 and got[(1, 12)] == 5
+    assert got[(2, 1)] == 6 and got[(8, 11)] == 47
+    assert sorted(set(got.values())) == list(range(48))
+
+
+def test_oracle_assembly_places_and_counts():
+    nchunk, block_ndf = 4, 6
+    rng = np.random.default_rng(3)
+    block = rng.integers(0, 256, block_ndf * nchunk * 7168, dtype=np.uint8)
+    ref_idf, ref_sec = 249998, 27  # the block crosses into the next period
+    order = rng.permutation(block_ndf * nchunk)[:-3]  # 3 frames lost
+    dfs, chunk = npo.df_stream(block, nchunk, ref_idf, ref_sec, order)
+    # a late frame (before the block) and a frame from the next block
+    extra, echunk = npo.df_stream(block[:nchunk * 7168 * 2], nchunk, ref_idf - 2, ref_sec)
+    later, lchunk = npo.df_stream(block[:nchunk * 7168], nchunk, ref_idf + block_ndf, ref_sec)
+    dfs = np.concatenate([dfs, extra[:1], later[:1]])
+    chunk = np.concatenate([chunk, echunk[:1], np.array([9], np.uint8)])  # bad chunk id too
+    out = np.full(block.size, 0xA5, dtype=np.uint8)
+    counts = co.assemble(dfs, chunk, ref_idf, ref_sec, out, block_ndf, nchunk)
+    got = out.reshape(-1, 7168)
+    want = block.reshape(-1, 7168)
+    placed = np.zeros(block_ndf * nchunk, bool)
+    placed[order] = True
+    assert np.array_equal(got[placed], want[placed])
+    assert np.all(got[~placed] == 0xA5)
+    exp = np.bincount(order % nchunk, minlength=nchunk).tolist() + [1, 0, 1]
+    assert counts.tolist() == exp

@@ -1,0 +1,71 @@
+"""GPU TFTFP assembly (b2p_assemble, capture.c:527-547) against the oracle's
+sequential placement, and raw data-frame stream -> assemble -> integrate
+against the oracle's spectrum of the original block."""
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+import paf_b2p
+
+pytestmark = pytest.mark.gpu
+SEED = 20181105
+
+
+def _run_gpu(it, dfs, chunk, ref_idf, ref_sec, block_init, block_ndf, nchunk):
+    d_dfs = it.upload(dfs.reshape(-1))
+    d_chk = it.upload(np.ascontiguousarray(chunk, np.uint8))
+    d_blk = it.upload(block_init)
+    d_cnt = it.upload(np.zeros(nchunk + 3, np.uint64))
+    it.assemble(d_dfs, dfs.shape[0], d_chk, ref_idf, ref_sec, d_blk, block_ndf, nchunk, d_cnt)
+    it.sync()
+    out = it.download(d_blk)
+    cnt = it.download(d_cnt).view(np.uint64)
+    return out, cnt, (d_dfs, d_chk, d_blk, d_cnt)
+
+
+@pytest.mark.parametrize("ref_idf", [1000, 249990])  # second case crosses a 27-s period
+def test_assemble_matches_oracle(gpu, ref_idf):
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * 64)
+    block_ndf, nchunk, ref_sec = 64, 48, 54
+    block = npo.fill_synthetic(g, g.block_bytes, SEED, 0, 3)
+    rng = np.random.default_rng(ref_idf)
+    order = rng.permutation(block_ndf * nchunk)[:-40]            # arrival order, 40 lost
+    dfs, chunk = npo.df_stream(block, nchunk, ref_idf, ref_sec, order)
+    early, ec = npo.df_stream(block[:nchunk * 7168 * 3], nchunk, ref_idf - 3, ref_sec)
+    late, lc = npo.df_stream(block[:nchunk * 7168 * 2], nchunk, ref_idf + block_ndf, ref_sec)
+    dfs = np.concatenate([early[5:20], dfs, late[:30]])
+    chunk = np.concatenate([ec[5:20], chunk, lc[:30]])
+    chunk[7] = 200                                               # a bad chunk id
+    init = np.full(block.size, 0x5A, np.uint8)
+    want = init.copy()
+    want_cnt = co.assemble(dfs, chunk, ref_idf, ref_sec, want, block_ndf, nchunk)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        got, cnt, bufs = _run_gpu(it, dfs, chunk, ref_idf, ref_sec, init, block_ndf, nchunk)
+        for b in bufs:
+            b.free()
+    assert np.array_equal(got, want)
+    assert cnt.tolist() == want_cnt.tolist()
+    assert int(cnt[:nchunk].sum()) == block_ndf * nchunk - 40
+
+
+def test_df_stream_to_spectrum(gpu):
+    # a full shuffled stream with its 64-B headers -> GPU assembly -> integrate
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * 256)
+    block_ndf, nchunk = 256, 48
+    block = npo.fill_synthetic(g, g.block_bytes, SEED, 1, 4)
+    order = np.random.default_rng(1).permutation(block_ndf * nchunk)
+    dfs, chunk = npo.df_stream(block, nchunk, 4242, 27 * 77, order)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        d_dfs = it.upload(dfs.reshape(-1))
+        d_chk = it.upload(chunk)
+        d_blk = it.alloc(g.block_bytes)
+        d_cnt = it.upload(np.zeros(nchunk + 3, np.uint64))
+        it.assemble(d_dfs, dfs.shape[0], d_chk, 4242, 27 * 77, d_blk, block_ndf, nchunk, d_cnt)
+        it.push(d_blk)  # stream-ordered after the assembly
+        out = it.finish()
+        for b in (d_dfs, d_chk, d_blk, d_cnt):
+            b.free()
+    assert np.array_equal(out.view(np.uint32), co.power(g, block).view(np.uint32))
