@@ -103,3 +103,50 @@ def test_oracle_assembly_places_and_counts():
     assert np.all(got[~placed] == 0xA5)
     exp = np.bincount(order % nchunk, minlength=nchunk).tolist() + [1, 0, 1]
     assert counts.tolist() == exp
+
+
+# ---- paf_dfgen: payload-only DADA file -> raw DF capture stream ------------------
+
+def _run_dfgen(tmp_path, block, nchunk, *args):
+    import os
+    import subprocess
+    src = tmp_path / "in.dada"
+    dada.write_dada_file(str(src), "HDR_SIZE 4096\n", block)
+    out, chk = tmp_path / "out.df", tmp_path / "chunks.u8"
+    subprocess.run([os.path.join(dada.BIN_DIR, "paf_dfgen"), "-i", str(src), "-o", str(out),
+                    "-n", str(nchunk), "-c", str(chk), *map(str, args)],
+                   check=True, capture_output=True)
+    dfs = np.fromfile(out, dtype=np.uint8).reshape(-1, npo.DF_BYTES)
+    return dfs, np.fromfile(chk, dtype=np.uint8)
+
+
+@pytest.mark.parametrize("ref_idf", [1000, 249995])
+def test_dfgen_matches_numpy_stream(tmp_path, ref_idf):
+    nchunk, nf = 4, 6
+    rng = np.random.default_rng(ref_idf)
+    block = rng.integers(0, 256, nf * nchunk * npo.DF_PAYLOAD, dtype=np.uint8)
+    dfs, chunk = _run_dfgen(tmp_path, block, nchunk, "-x", ref_idf, "-s", 54, "-f", 1300, "-b", 3,
+                            "-e", 5)
+    want, want_chunk = npo.df_stream(block, nchunk, ref_idf, 54, beam=3, epoch=5, freq0=1300)
+    assert np.array_equal(dfs, want) and np.array_equal(chunk, want_chunk)
+
+
+def test_dfgen_shuffled_lossy_stream_reassembles(tmp_path):
+    nchunk, nf = 3, 8
+    rng = np.random.default_rng(3)
+    block = rng.integers(0, 256, nf * nchunk * npo.DF_PAYLOAD, dtype=np.uint8)
+    dfs, chunk = _run_dfgen(tmp_path, block, nchunk, "-x", 249996, "-s", 27, "-r", 11, "-l", 200)
+    n = dfs.shape[0]
+    assert 0 < n < nf * nchunk  # some frames lost, order shuffled
+    out = np.zeros_like(block)
+    counts = co.assemble(dfs, chunk, 249996, 27, out, nf, nchunk)
+    assert int(counts[:nchunk].sum()) == n
+    # every frame that arrived lands where it came from; lost ones stay zero
+    got = out.reshape(nf * nchunk, -1)
+    src = block.reshape(nf * nchunk, -1)
+    hit = np.zeros(nf * nchunk, bool)
+    for i in range(n):
+        h = npo.df_decode(dfs[i, :64])
+        gidf = int(h["idf"][0]) + (int(h["sec"][0]) - 27) // 27 * 250000 - 249996
+        hit[gidf * nchunk + chunk[i]] = True
+    assert np.array_equal(got[hit], src[hit]) and not got[~hit].any()

@@ -38,6 +38,9 @@ for s in $STEPS; do
             --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
+    asm) run bench_assemble 600 python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
+    profasm) run prof_asm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_asm" -o run \
+            -- python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
