@@ -23,6 +23,7 @@
 //    integers: the result does not depend on arrival order).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "b2p_internal.h"
 
@@ -356,8 +357,23 @@ __global__ void __launch_bounds__(256) b2p_fill_kernel(uint4 *dst, uint64_t nvec
 // One wave per data frame: every lane reads the (broadcast) 24-B header and
 // computes the frame index itself (capture.c:566, same double arithmetic),
 // so no barrier is needed; the 7168-B payload moves as 7 x 1 KiB wave loads
-// and stores to (idf * nchunk + chunk) * 7168.  Per-chunk counts go through
-// LDS and leave with one atomic per counter per workgroup.
+// and stores to (idf * nchunk + chunk) * 7168.  K frames per iteration put
+// 7K loads in flight per lane before the first store.  Per-chunk counts go
+// through LDS and leave with one atomic per counter per workgroup.
+__device__ __forceinline__ uint32_t asm_slot(const AssembleArgs &a, uint64_t d, int64_t &rel) {
+  const unsigned char *df = a.dfs + d * (uint64_t)a.df_bytes;
+  const uint64_t w0 = __builtin_bswap64(*(const uint64_t *)df);  // hdr.c:15-18
+  const uint64_t idf = w0 & 0x00000000ffffffffULL;
+  const uint64_t sec = (w0 & 0x3fffffff00000000ULL) >> 32;
+  rel = (int64_t)idf + (int64_t)(sec - a.ref_sec) / 1.08E-4 - (int64_t)a.ref_idf;
+  const uint32_t chunk = a.chunk_of_df[d];
+  if (chunk >= a.nchunk) return a.nchunk + 2;
+  if (rel < 0) return a.nchunk;
+  if ((uint64_t)rel >= a.block_ndf) return a.nchunk + 1;
+  return chunk;
+}
+
+template <bool NTL, bool NTS, int K>
 __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
   __shared__ unsigned long long cnt[256 + 3];
   const uint32_t ncnt = a.nchunk + 3;
@@ -366,42 +382,62 @@ __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t d = wave; d < a.ndf; d += nwaves) {
-    const unsigned char *df = a.dfs + d * (uint64_t)a.df_bytes;
-    const uint64_t w0 = __builtin_bswap64(*(const uint64_t *)df);  // hdr.c:15-18
-    const uint64_t idf = w0 & 0x00000000ffffffffULL;
-    const uint64_t sec = (w0 & 0x3fffffff00000000ULL) >> 32;
-    const int64_t rel = (int64_t)idf + (int64_t)(sec - a.ref_sec) / 1.08E-4 - (int64_t)a.ref_idf;
-    const uint32_t chunk = a.chunk_of_df[d];
-    uint32_t slot;
-    if (chunk >= a.nchunk) slot = a.nchunk + 2;
-    else if (rel < 0) slot = a.nchunk;
-    else if ((uint64_t)rel >= a.block_ndf) slot = a.nchunk + 1;
-    else slot = chunk;
-    if (lane == 0) atomicAdd(&cnt[slot], 1ull);
-    if (slot >= a.nchunk) continue;  // wave-uniform
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(df + a.hdr_bytes);
-    u32x4 *dst = reinterpret_cast<u32x4 *>(a.block + ((uint64_t)rel * a.nchunk + chunk) * 7168ull);
-    u32x4 v[7];
+  for (uint64_t d0 = wave * K; d0 < a.ndf; d0 += nwaves * K) {
+    uint32_t slot[K];
+    int64_t rel[K];
+    u32x4 v[K][7];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) v[k] = __builtin_nontemporal_load(src + k * 64 + lane);
+    for (int j = 0; j < K; ++j) {
+      const uint64_t d = d0 + j;
+      slot[j] = d < a.ndf ? asm_slot(a, d, rel[j]) : 0xffffffffu;
+      if (slot[j] < a.nchunk) {  // wave-uniform
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(a.dfs + d * (uint64_t)a.df_bytes + a.hdr_bytes);
 #pragma unroll
-    for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(v[k], dst + k * 64 + lane);
+        for (int k = 0; k < 7; ++k)
+          v[j][k] = NTL ? __builtin_nontemporal_load(src + k * 64 + lane) : src[k * 64 + lane];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (slot[j] == 0xffffffffu) continue;
+      if (lane == 0) atomicAdd(&cnt[slot[j]], 1ull);
+      if (slot[j] >= a.nchunk) continue;
+      const uint32_t chunk = a.chunk_of_df[d0 + j];
+      u32x4 *dst = reinterpret_cast<u32x4 *>(a.block + ((uint64_t)rel[j] * a.nchunk + chunk) * 7168ull);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        if (NTS) __builtin_nontemporal_store(v[j][k], dst + k * 64 + lane);
+        else dst[k * 64 + lane] = v[j][k];
+      }
+    }
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < ncnt; j += blockDim.x)
     if (cnt[j]) atomicAdd(&a.counts[j], cnt[j]);
 }
 
+// B2P_ASM_VARIANT: 0 nt load+store K=1 (default), 1 nt K=2, 2 plain K=1,
+// 3 nt load / plain store K=1, 4 nt K=4; B2P_ASM_GRID: workgroups (4 waves)
 hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s) {
   if (a.nchunk > 256) return hipErrorInvalidValue;
-  uint64_t blocks = (a.ndf + 3) / 4;  // 4 waves per workgroup
-  if (blocks > 4096) blocks = 4096;
+  static const int variant = getenv("B2P_ASM_VARIANT") ? atoi(getenv("B2P_ASM_VARIANT")) : 0;
+  static const long grid_env = getenv("B2P_ASM_GRID") ? atol(getenv("B2P_ASM_GRID")) : 0;
+  const int k = variant == 1 ? 2 : (variant == 4 ? 4 : 1);
+  uint64_t blocks = (a.ndf + 4 * k - 1) / (4 * k);  // 4 waves per workgroup
+  const uint64_t cap = grid_env > 0 ? (uint64_t)grid_env : 8192;  // swept: profiles/r01_assemble_sweep.txt
+  if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
   AssembleArgs arg = a;
   void *args[] = {&arg};
-  return hipLaunchKernel(reinterpret_cast<const void *>(b2p_assemble_kernel), dim3((uint32_t)blocks),
-                         dim3(256), args, 0, s);
+  const void *f;
+  switch (variant) {
+    case 1: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 2>); break;
+    case 2: f = reinterpret_cast<const void *>(b2p_assemble_kernel<false, false, 1>); break;
+    case 3: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, false, 1>); break;
+    case 4: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 4>); break;
+    default: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 1>);
+  }
+  return hipLaunchKernel(f, dim3((uint32_t)blocks), dim3(256), args, 0, s);
 }
 
 // ---- launchers --------------------------------------------------------------

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--ndf", type=int, default=8192, help="frames per block (capture.h:20-28)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--order", choices=("both", "tm", "shuffled"), default="both")
     a = ap.parse_args()
     nchunk = 48
     geom = paf_b2p.bmf_geom(nsamp_int=a.ndf * 128)
@@ -72,6 +73,8 @@ def main():
                                         [:, rng.permutation(nchunk)].reshape(-1)),
         "fully shuffled": rng.permutation(n),
     }
+    if a.order != "both":
+        orders = {k: v for k, v in orders.items() if k.startswith("time") == (a.order == "tm")}
     for name, order in orders.items():
         t0 = time.perf_counter()
         dfs, chunk = build_stream(block, nchunk, 1000, 54, order)
@@ -119,6 +122,8 @@ def main():
             "stream_to_spectrum_us": round(both_s * 1e6, 1),
             "stream_to_spectrum_Msamples_s": round(a.ndf * 128 * it.nout / both_s / 1e6, 1),
             "host_stream_build_s": round(prep, 1),
+            "variant": os.environ.get("B2P_ASM_VARIANT", "0"),
+            "grid": os.environ.get("B2P_ASM_GRID", "default"),
         }), flush=True)
         d_dfs.free()
         d_chk.free()
