@@ -220,6 +220,10 @@ int b2p_assemble(b2p_ctx_t *ctx, const void *dfs, uint64_t ndf, uint32_t df_byte
 int b2p_dev_free(b2p_ctx_t *ctx, void *dev);
 /* kind: 1 host->device, 2 device->host, 3 device->device; synchronous */
 int b2p_memcpy(b2p_ctx_t *ctx, void *dst, const void *src, size_t bytes, int kind);
+/* fill device memory with a byte, ordered on the context's stream behind
+ * earlier work (clears a ring block before frames are assembled into it,
+ * so lost frames read as zeros rather than stale data) */
+int b2p_memset(b2p_ctx_t *ctx, void *dev, int value, size_t bytes);
 
 #ifdef __cplusplus
 }

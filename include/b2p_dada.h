@@ -62,6 +62,11 @@ typedef struct ipcbuf {
 #define IPCBUF_INIT {0, 0, -1, -1, NULL, NULL, 0, 0, -1, 0, 0, 0}
 
 int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers);
+/* device_id >= 0: blocks in that GPU's memory, owned by a holder process and
+ * shared through HIP IPC handles (PSRDADA ipcbuf_create_work; the sync
+ * segment's on_device_id).  -1: SysV shared memory. */
+int ipcbuf_create_work(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz,
+                       unsigned n_readers, int device_id);
 int ipcbuf_connect(ipcbuf_t *id, key_t key);
 int ipcbuf_disconnect(ipcbuf_t *id);
 int ipcbuf_destroy(ipcbuf_t *id);
@@ -86,6 +91,15 @@ uint64_t ipcbuf_get_nreaders(ipcbuf_t *id);
 char *ipcbuf_get_buffer(ipcbuf_t *id, uint64_t i);
 /* blocks written / cleared so far (monitoring, dada_dbmonitor role) */
 uint64_t ipcbuf_get_write_count(ipcbuf_t *id);
+/* -1 for a host ring; else the HIP device holding the blocks, whose
+ * addresses (ipcbuf_get_next_read/write, ipcio_open_block_*) are device
+ * pointers valid in this process.  Writers finish their kernels before
+ * ipcbuf_mark_filled; readers finish theirs before ipcbuf_mark_cleared. */
+int ipcbuf_get_device(ipcbuf_t *id);
+/* copy host or device memory into / out of a block of either kind
+ * (memcpy, or a synchronous hipMemcpy for a device ring) */
+int ipcbuf_copy_in(ipcbuf_t *id, char *block, const void *src, uint64_t n);
+int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n);
 uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread);
 
 /* ---- ipcio: block-level streaming over an ipcbuf ---- */
@@ -132,6 +146,11 @@ int dada_hdu_open_read(dada_hdu_t *hdu);
  * :129-130).  Header ring: hdr_nbufs blocks of hdr_bufsz bytes. */
 int dada_db_create(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
                    uint64_t hdr_nbufs, uint64_t hdr_bufsz);
+/* as dada_db_create, data blocks on HIP device device_id (-1: host); the
+ * header ring stays in host memory.  Removes both rings and stops the
+ * holder when destroyed. */
+int dada_db_create_work(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
+                        uint64_t hdr_nbufs, uint64_t hdr_bufsz, int device_id);
 int dada_db_destroy(key_t key);
 
 /* ---- ASCII header (ascii_header_set at capture.c:758-778) ---- */

@@ -724,6 +724,14 @@ int b2p_dev_free(b2p_ctx_t *c, void *dev) {
   return B2P_OK;
 }
 
+int b2p_memset(b2p_ctx_t *c, void *dev, int value, size_t bytes) {
+  if (!c || (!dev && bytes)) return B2P_EINVAL;
+  if (!bytes) return B2P_OK;
+  CK(c, hipSetDevice(c->device));
+  CK(c, hipMemsetAsync(dev, value, bytes, c->stream));
+  return B2P_OK;
+}
+
 int b2p_memcpy(b2p_ctx_t *c, void *dst, const void *src, size_t bytes, int kind) {
   if (!c || !dst || !src) return B2P_EINVAL;
   hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice

@@ -1,0 +1,241 @@
+/*
+ * dada_device.c -- GPU-resident ring blocks.
+ *
+ * PSRDADA keeps a device ring's blocks in GPU memory and names the device
+ * in the sync segment (`on_device_id`, ipcsync_t +512, SURVEY.md Appendix A;
+ * `ipc_alloc_cuda` in the reference's linked libpsrdada).  Here:
+ *
+ *  - a holder process (double-forked from the creator, so it outlives it)
+ *    allocates the blocks with hipMalloc, publishes one HIP IPC handle per
+ *    block in the sync segment, and keeps the memory alive until the ring
+ *    is destroyed (SIGTERM) or its sync segment disappears (and, when
+ *    DADA_HOLDER_IDLE_S is set, after that many seconds with no process
+ *    attached but itself -- a guard against rings orphaned by a killed run);
+ *  - every process that connects opens the handles (hipIpcOpenMemHandle),
+ *    so ipcbuf_get_next_read/write hand out device pointers;
+ *  - producers and consumers order their kernels against the ring with
+ *    their own stream synchronisation: a writer's kernels are complete
+ *    before ipcbuf_mark_filled, a reader's before ipcbuf_mark_cleared.
+ *
+ * HIP is reached through dlopen of libamdhip64.so.7, so libpafdada still
+ * loads (and host rings still work) on machines without ROCm; in a process
+ * that already mapped a HIP runtime (torch, libpafb2p) the same one is used.
+ */
+#include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/ipc.h>
+#include <sys/shm.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "dada_internal.h"
+
+typedef struct {
+  char reserved[DEV_HANDLE_BYTES];
+} ipc_handle_t; /* hipIpcMemHandle_t, hip_runtime_api.h:688-690 */
+
+static struct {
+  int loaded;
+  int (*set_device)(int);
+  int (*malloc_)(void **, size_t);
+  int (*free_)(void *);
+  int (*memset_)(void *, int, size_t);
+  int (*get_handle)(ipc_handle_t *, void *);
+  int (*open_handle)(void **, ipc_handle_t, unsigned);
+  int (*close_handle)(void *);
+  int (*memcpy_)(void *, const void *, size_t, int);
+  int (*sync)(void);
+  const char *(*err_str)(int);
+} hip;
+
+static int hip_load(void) {
+  if (hip.loaded) return hip.loaded > 0 ? 0 : -1;
+  void *h = dlopen("libamdhip64.so.7", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);
+  if (!h) h = dlopen("libamdhip64.so.7", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/libamdhip64.so.7", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) {
+    hip.loaded = -1;
+    return -1;
+  }
+#define SYM(field, name) *(void **)(&hip.field) = dlsym(h, name)
+  SYM(set_device, "hipSetDevice");
+  SYM(malloc_, "hipMalloc");
+  SYM(free_, "hipFree");
+  SYM(memset_, "hipMemset");
+  SYM(get_handle, "hipIpcGetMemHandle");
+  SYM(open_handle, "hipIpcOpenMemHandle");
+  SYM(close_handle, "hipIpcCloseMemHandle");
+  SYM(memcpy_, "hipMemcpy");
+  SYM(sync, "hipDeviceSynchronize");
+  SYM(err_str, "hipGetErrorString");
+#undef SYM
+  hip.loaded = (hip.set_device && hip.malloc_ && hip.free_ && hip.memset_ && hip.get_handle &&
+                hip.open_handle && hip.close_handle && hip.memcpy_ && hip.sync && hip.err_str)
+                   ? 1
+                   : -1;
+  return hip.loaded > 0 ? 0 : -1;
+}
+
+static void report(int fd, const char *what, int code) {
+  char msg[200];
+  int n = snprintf(msg, sizeof msg, "E%s: %s", what,
+                   code >= 0 && hip.err_str ? hip.err_str(code) : "unavailable");
+  if (n > 0) (void)!write(fd, msg, (size_t)n < sizeof msg ? (size_t)n : sizeof msg - 1);
+}
+
+/* the holder: owns the blocks until SIGTERM/SIGINT or the ring is removed */
+static void holder(int syncid, ipcsync_t *s, int device, int wfd) {
+  int rc;
+  const uint64_t n = s->nbufs;
+  void **blk = calloc(n, sizeof(void *));
+  if (!blk) {
+    report(wfd, "calloc", -1);
+    _exit(1);
+  }
+  if (hip_load() < 0) {
+    report(wfd, "dlopen libamdhip64.so.7", -1);
+    _exit(1);
+  }
+  if ((rc = hip.set_device(device)) != 0) {
+    report(wfd, "hipSetDevice", rc);
+    _exit(1);
+  }
+  for (uint64_t i = 0; i < n; i++) {
+    ipc_handle_t h;
+    if ((rc = hip.malloc_(&blk[i], s->bufsz)) != 0 || (rc = hip.memset_(blk[i], 0, s->bufsz)) != 0 ||
+        (rc = hip.get_handle(&h, blk[i])) != 0) {
+      report(wfd, "hipMalloc/hipIpcGetMemHandle", rc);
+      for (uint64_t j = 0; j <= i; j++)
+        if (blk[j]) hip.free_(blk[j]);
+      _exit(1);
+    }
+    memcpy(sync_handles(s) + i * DEV_HANDLE_BYTES, &h, DEV_HANDLE_BYTES);
+  }
+  hip.sync();
+  s->holder_pid = (int32_t)getpid();
+  s->on_device_id = device;
+  __atomic_store_n(&s->holder_state, 1, __ATOMIC_RELEASE);
+  (void)!write(wfd, "R", 1);
+  close(wfd);
+
+  sigset_t set;
+  sigemptyset(&set);
+  sigaddset(&set, SIGTERM);
+  sigaddset(&set, SIGINT);
+  sigaddset(&set, SIGHUP);
+  const char *idle_env = getenv("DADA_HOLDER_IDLE_S");
+  const long idle_max = idle_env ? atol(idle_env) : 0;
+  long idle = 0;
+  for (;;) {
+    struct timespec one = {1, 0};
+    if (sigtimedwait(&set, NULL, &one) > 0) break;
+    struct shmid_ds ds;
+    if (shmctl(syncid, IPC_STAT, &ds) < 0 || (ds.shm_perm.mode & SHM_DEST)) break;
+    idle = ds.shm_nattch <= 1 ? idle + 1 : 0;
+    if (idle_max > 0 && idle >= idle_max) break;
+  }
+  for (uint64_t i = 0; i < n; i++) hip.free_(blk[i]);
+  __atomic_store_n(&s->holder_state, 2, __ATOMIC_RELEASE);
+  shmdt(s);
+  _exit(0);
+}
+
+int dev_create_blocks(int syncid, ipcsync_t *s, int device) {
+  int fds[2];
+  if (pipe(fds) < 0) return -1;
+  /* block the stop signals before forking: the holder takes them with
+   * sigtimedwait and never runs a handler */
+  sigset_t set, old;
+  sigemptyset(&set);
+  sigaddset(&set, SIGTERM);
+  sigaddset(&set, SIGINT);
+  sigaddset(&set, SIGHUP);
+  sigprocmask(SIG_BLOCK, &set, &old);
+  pid_t mid = fork();
+  if (mid == 0) {
+    close(fds[0]);
+    setsid();
+    pid_t h = fork();
+    if (h != 0) _exit(h < 0 ? 1 : 0);
+    /* the holder: detached, stdio on /dev/null so no caller waits on it */
+    int dn = open("/dev/null", O_RDWR);
+    if (dn >= 0) {
+      dup2(dn, 0);
+      dup2(dn, 1);
+      dup2(dn, 2);
+      if (dn > 2) close(dn);
+    }
+    holder(syncid, s, device, fds[1]);
+  }
+  sigprocmask(SIG_SETMASK, &old, NULL);
+  close(fds[1]);
+  if (mid < 0) {
+    close(fds[0]);
+    return -1;
+  }
+  int st = 0;
+  while (waitpid(mid, &st, 0) < 0 && errno == EINTR) {
+  }
+  char msg[200] = {0};
+  ssize_t got;
+  do {
+    got = read(fds[0], msg, sizeof msg - 1);
+  } while (got < 0 && errno == EINTR);
+  close(fds[0]);
+  if (got >= 1 && msg[0] == 'R') return 0;
+  fprintf(stderr, "dada device ring: holder failed: %s\n", got > 1 ? msg + 1 : "no reply");
+  errno = ENODEV;
+  return -1;
+}
+
+int dev_stop_holder(ipcsync_t *s) {
+  if (s->holder_pid <= 0 || __atomic_load_n(&s->holder_state, __ATOMIC_ACQUIRE) != 1) return 0;
+  if (kill(s->holder_pid, SIGTERM) < 0) return errno == ESRCH ? 0 : -1;
+  for (int i = 0; i < 1000; i++) { /* <= 10 s for the holder to free its memory */
+    if (__atomic_load_n(&s->holder_state, __ATOMIC_ACQUIRE) == 2) return 0;
+    struct timespec t = {0, 10 * 1000 * 1000};
+    nanosleep(&t, NULL);
+  }
+  return -1;
+}
+
+int dev_open_blocks(ipcbuf_t *id) {
+  ipcsync_t *s = id->sync;
+  if (__atomic_load_n(&s->holder_state, __ATOMIC_ACQUIRE) != 1 || hip_load() < 0) {
+    errno = ENODEV;
+    return -1;
+  }
+  if (hip.set_device(s->on_device_id) != 0) {
+    errno = ENODEV;
+    return -1;
+  }
+  for (uint64_t i = 0; i < id->nbufs; i++) {
+    ipc_handle_t h;
+    void *p = NULL;
+    memcpy(&h, sync_handles(s) + i * DEV_HANDLE_BYTES, DEV_HANDLE_BYTES);
+    if (hip.open_handle(&p, h, 1 /* hipIpcMemLazyEnablePeerAccess */) != 0) {
+      errno = ENODEV;
+      return -1;
+    }
+    id->buffer[i] = p;
+  }
+  return 0;
+}
+
+void dev_close_blocks(ipcbuf_t *id) {
+  if (hip_load() < 0) return;
+  for (uint64_t i = 0; i < id->nbufs; i++)
+    if (id->buffer[i]) hip.close_handle(id->buffer[i]);
+}
+
+int dev_copy(void *dst, const void *src, uint64_t n) {
+  if (!n) return 0;
+  if (hip_load() < 0) return -1;
+  return hip.memcpy_(dst, src, n, 4 /* hipMemcpyDefault */) == 0 ? 0 : -1;
+}

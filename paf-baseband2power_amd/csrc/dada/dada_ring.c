@@ -22,44 +22,7 @@
 #include <unistd.h>
 
 #include "b2p_dada.h"
-
-#define SYNC_MAGIC 0x50414642u /* "PAFB" */
-#define SYNC_VERSION 1u
-
-/* semaphore set layout */
-#define SEM_CLEAR 0
-#define SEM_WLOCK 1
-#define SEM_FULL(r) (2 + (r))
-#define SEM_RLOCK(r) (2 + IPCBUF_READERS + (r))
-#define NSEMS (2 + 2 * IPCBUF_READERS)
-
-struct ipcsync {
-  uint32_t magic, version;
-  uint64_t nbufs, bufsz;
-  uint32_t n_readers;
-  int32_t semid;
-  uint64_t w_count;                  /* blocks filled so far            */
-  uint64_t r_count[IPCBUF_READERS];  /* blocks cleared by each reader   */
-  uint64_t eod_count;                /* transfer ends after this many   */
-  int32_t sod;
-  int32_t pad;
-  uint64_t s_buf, s_byte;
-  /* followed by: int32 shmid[nbufs]; uint32 clear_cnt[nbufs];
-   *              uint64 nbytes[nbufs] (8-aligned)                        */
-};
-
-static int32_t *sync_shmids(ipcsync_t *s) { return (int32_t *)(s + 1); }
-static uint32_t *sync_clear(ipcsync_t *s) {
-  return (uint32_t *)(sync_shmids(s) + s->nbufs);
-}
-static uint64_t *sync_nbytes(ipcsync_t *s) {
-  uintptr_t p = (uintptr_t)(sync_clear(s) + s->nbufs);
-  return (uint64_t *)((p + 7) & ~(uintptr_t)7);
-}
-static size_t sync_size(uint64_t nbufs) {
-  return sizeof(ipcsync_t) + nbufs * (sizeof(int32_t) + sizeof(uint32_t)) + 8 +
-         nbufs * sizeof(uint64_t);
-}
+#include "dada_internal.h"
 
 /* semop with EINTR retry; flags e.g. SEM_UNDO | IPC_NOWAIT */
 static int sem_do(int semid, int num, int op, int flags) {
@@ -129,8 +92,12 @@ int multilog_close(multilog_t *m) {
 /* ------------------------------------------------------------------ */
 /* ipcbuf                                                               */
 
-int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers) {
-  if (!id || !nbufs || !bufsz || n_readers > IPCBUF_READERS || nbufs > 32767) return -1;
+/* Build the sync segment, the semaphores and the blocks: SysV segments for
+ * a host ring, device memory held by a holder process for a device ring
+ * (dada_device.c).  The magic is written last, so a connector never sees a
+ * half-built ring. */
+static int ring_create(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers, int device) {
+  if (!nbufs || !bufsz || n_readers > IPCBUF_READERS || nbufs > 32767) return -1;
   int syncid = shmget(key, sync_size(nbufs), IPC_CREAT | IPC_EXCL | 0666);
   if (syncid < 0) return -1;
   ipcsync_t *s = shmat(syncid, NULL, 0);
@@ -143,6 +110,7 @@ int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsig
   for (uint64_t i = 0; i < nbufs; i++) sync_shmids(s)[i] = -1;
   s->bufsz = bufsz;
   s->n_readers = n_readers;
+  s->on_device_id = -1;
   s->semid = semget(IPC_PRIVATE, NSEMS, IPC_CREAT | 0666);
   int ok = s->semid >= 0;
   if (ok) {
@@ -159,22 +127,38 @@ int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsig
     arg.array = v;
     ok = semctl(s->semid, 0, SETALL, arg) == 0;
   }
-  for (uint64_t i = 0; ok && i < nbufs; i++) {
-    int sid = shmget(IPC_PRIVATE, bufsz, IPC_CREAT | 0666);
-    sync_shmids(s)[i] = sid;
-    if (sid < 0) ok = 0;
+  if (ok && device >= 0) {
+    ok = dev_create_blocks(syncid, s, device) == 0;
+  } else {
+    for (uint64_t i = 0; ok && i < nbufs; i++) {
+      int sid = shmget(IPC_PRIVATE, bufsz, IPC_CREAT | 0666);
+      sync_shmids(s)[i] = sid;
+      if (sid < 0) ok = 0;
+    }
   }
   if (!ok) {
+    const int e = errno;
     for (uint64_t i = 0; i < nbufs; i++)
       if (sync_shmids(s)[i] >= 0) shmctl(sync_shmids(s)[i], IPC_RMID, NULL);
     if (s->semid >= 0) semctl(s->semid, 0, IPC_RMID);
     shmdt(s);
     shmctl(syncid, IPC_RMID, NULL);
+    errno = e;
     return -1;
   }
-  s->magic = SYNC_MAGIC; /* last: a connector never sees a half-built ring */
   s->version = SYNC_VERSION;
+  __atomic_store_n(&s->magic, SYNC_MAGIC, __ATOMIC_RELEASE);
   shmdt(s);
+  return 0;
+}
+
+int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers) {
+  return ipcbuf_create_work(id, key, nbufs, bufsz, n_readers, -1);
+}
+
+int ipcbuf_create_work(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
+                       int device_id) {
+  if (!id || ring_create(key, nbufs, bufsz, n_readers, device_id) < 0) return -1;
   return ipcbuf_connect(id, key);
 }
 
@@ -190,7 +174,8 @@ int ipcbuf_connect(ipcbuf_t *id, key_t key) {
     id->sync = NULL;
     return -1;
   }
-  if (id->sync->magic != SYNC_MAGIC || id->sync->version != SYNC_VERSION) {
+  if (__atomic_load_n(&id->sync->magic, __ATOMIC_ACQUIRE) != SYNC_MAGIC ||
+      id->sync->version != SYNC_VERSION) {
     shmdt(id->sync);
     id->sync = NULL;
     errno = EINVAL;
@@ -201,13 +186,20 @@ int ipcbuf_connect(ipcbuf_t *id, key_t key) {
   id->semid = id->sync->semid;
   id->buffer = calloc(id->nbufs, sizeof(char *));
   if (!id->buffer) return -1;
-  for (uint64_t i = 0; i < id->nbufs; i++) {
-    void *p = shmat(sync_shmids(id->sync)[i], NULL, 0);
-    if (p == (void *)-1) {
+  if (id->sync->on_device_id >= 0) {
+    if (dev_open_blocks(id) < 0) {
       ipcbuf_disconnect(id);
       return -1;
     }
-    id->buffer[i] = p;
+  } else {
+    for (uint64_t i = 0; i < id->nbufs; i++) {
+      void *p = shmat(sync_shmids(id->sync)[i], NULL, 0);
+      if (p == (void *)-1) {
+        ipcbuf_disconnect(id);
+        return -1;
+      }
+      id->buffer[i] = p;
+    }
   }
   id->state = 1;
   return 0;
@@ -218,8 +210,12 @@ int ipcbuf_disconnect(ipcbuf_t *id) {
   if (id->state == 2) ipcbuf_unlock_write(id);
   if (id->state == 3) ipcbuf_unlock_read(id);
   if (id->buffer) {
-    for (uint64_t i = 0; i < id->nbufs; i++)
-      if (id->buffer[i]) shmdt(id->buffer[i]);
+    if (id->sync && id->sync->on_device_id >= 0) {
+      dev_close_blocks(id);
+    } else {
+      for (uint64_t i = 0; i < id->nbufs; i++)
+        if (id->buffer[i]) shmdt(id->buffer[i]);
+    }
     free(id->buffer);
     id->buffer = NULL;
   }
@@ -236,8 +232,14 @@ int ipcbuf_destroy(ipcbuf_t *id) {
   int32_t *ids = malloc(n * sizeof(int32_t));
   if (!ids) return -1;
   memcpy(ids, sync_shmids(id->sync), n * sizeof(int32_t));
+  ipcsync_t *s = shmat(syncid, NULL, 0); /* outlives the disconnect below */
   ipcbuf_disconnect(id);
-  for (uint64_t i = 0; i < n; i++) shmctl(ids[i], IPC_RMID, NULL);
+  if (s != (void *)-1) {
+    if (s->on_device_id >= 0) dev_stop_holder(s);
+    shmdt(s);
+  }
+  for (uint64_t i = 0; i < n; i++)
+    if (ids[i] >= 0) shmctl(ids[i], IPC_RMID, NULL);
   free(ids);
   semctl(semid, 0, IPC_RMID);
   shmctl(syncid, IPC_RMID, NULL);
@@ -365,6 +367,22 @@ uint64_t ipcbuf_get_nreaders(ipcbuf_t *id) { return id && id->sync ? id->sync->n
 char *ipcbuf_get_buffer(ipcbuf_t *id, uint64_t i) {
   return id && id->buffer && i < id->nbufs ? id->buffer[i] : NULL;
 }
+int ipcbuf_get_device(ipcbuf_t *id) { return id && id->sync ? id->sync->on_device_id : -1; }
+
+int ipcbuf_copy_in(ipcbuf_t *id, char *block, const void *src, uint64_t n) {
+  if (!id || !id->sync || (!block && n) || (!src && n)) return -1;
+  if (id->sync->on_device_id >= 0) return dev_copy(block, src, n);
+  memcpy(block, src, n);
+  return 0;
+}
+
+int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n) {
+  if (!id || !id->sync || (!block && n) || (!dst && n)) return -1;
+  if (id->sync->on_device_id >= 0) return dev_copy(dst, block, n);
+  memcpy(dst, block, n);
+  return 0;
+}
+
 uint64_t ipcbuf_get_write_count(ipcbuf_t *id) { return id && id->sync ? id->sync->w_count : 0; }
 uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread) {
   return id && id->sync && iread >= 0 && iread < IPCBUF_READERS ? id->sync->r_count[iread] : 0;
@@ -540,29 +558,47 @@ int dada_hdu_open_read(dada_hdu_t *h) {
 
 int dada_db_create(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers, uint64_t hdr_nbufs,
                    uint64_t hdr_bufsz) {
-  ipcbuf_t d = IPCBUF_INIT, hb = IPCBUF_INIT;
-  if (ipcbuf_create(&d, key, nbufs, bufsz, n_readers) < 0) return -1;
-  if (ipcbuf_create(&hb, key + 1, hdr_nbufs, hdr_bufsz, n_readers) < 0) {
-    ipcbuf_destroy(&d);
+  return dada_db_create_work(key, nbufs, bufsz, n_readers, hdr_nbufs, hdr_bufsz, -1);
+}
+
+/* the creator does not attach: a device ring's blocks are opened only by
+ * the processes that use them */
+int dada_db_create_work(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
+                        uint64_t hdr_nbufs, uint64_t hdr_bufsz, int device_id) {
+  if (ring_create(key, nbufs, bufsz, n_readers, device_id) < 0) return -1;
+  if (ring_create(key + 1, hdr_nbufs, hdr_bufsz, n_readers, -1) < 0) {
+    const int e = errno;
+    dada_db_destroy(key);
+    errno = e;
     return -1;
   }
-  ipcbuf_disconnect(&d);
-  ipcbuf_disconnect(&hb);
   return 0;
 }
 
-int dada_db_destroy(key_t key) {
+/* removes one ring without attaching its blocks (a device ring's holder is
+ * stopped instead) */
+static int ring_remove(key_t key) {
+  int syncid = shmget(key, 0, 0);
+  if (syncid < 0) return -1;
+  ipcsync_t *s = shmat(syncid, NULL, 0);
+  if (s == (void *)-1) return -1;
   int rc = 0;
-  ipcbuf_t d = IPCBUF_INIT, hb = IPCBUF_INIT;
-  if (ipcbuf_connect(&d, key) == 0)
-    ipcbuf_destroy(&d);
-  else
+  if (s->magic == SYNC_MAGIC && s->version == SYNC_VERSION) {
+    if (s->on_device_id >= 0) rc = dev_stop_holder(s);
+    for (uint64_t i = 0; i < s->nbufs; i++)
+      if (sync_shmids(s)[i] >= 0) shmctl(sync_shmids(s)[i], IPC_RMID, NULL);
+    semctl(s->semid, 0, IPC_RMID);
+  } else {
     rc = -1;
-  if (ipcbuf_connect(&hb, key + 1) == 0)
-    ipcbuf_destroy(&hb);
-  else
-    rc = -1;
+  }
+  shmdt(s);
+  shmctl(syncid, IPC_RMID, NULL);
   return rc;
+}
+
+int dada_db_destroy(key_t key) {
+  const int a = ring_remove(key), b = ring_remove(key + 1);
+  return a == 0 && b == 0 ? 0 : -1;
 }
 
 int64_t fileread(const char *filename, char *buffer, unsigned bufsz) {

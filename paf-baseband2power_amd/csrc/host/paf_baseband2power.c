@@ -55,6 +55,7 @@ typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
   float *spec_dev; /* this sub-band's spectrum (device) */
   uint64_t rbufsz;
   int locked;
+  int ondev; /* input blocks are in GPU memory (dada_db -g) */
 } sub_t;
 
 static void usage(void) {
@@ -168,6 +169,7 @@ typedef struct shared_t {
   int have[MAX_SUB]; /* this round: 1 whole block, 0 partial, -1 end of data */
   int failed;
   uint64_t nblocks, nskipped;
+  double t_first, t_last; /* first integration started, last output written */
 } shared_t;
 
 typedef struct worker_t {
@@ -201,11 +203,22 @@ static void *worker(void *arg) {
       continue;
     }
     const double t0 = now_s();
-    int rc = b2p_push(s->ctx, blk, bytes, 0); /* returns once the block is copied */
-    ipcio_close_block_read(s->in->data_block, bytes);
-    if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
-                                            sh->nsub == 1 ? 0 : 1);
-    if (rc == B2P_OK && sh->nsub == 1) rc = b2p_sync(s->ctx);
+    if (w->r == 0 && sh->t_first == 0) sh->t_first = t0;
+    int rc;
+    if (s->ondev) {
+      /* the block is already in HBM: one integrate launch reads it in place;
+       * it must be done with the block before the block goes back to the ring */
+      rc = b2p_integrate(s->ctx, blk, bytes, 1, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
+                         sh->nsub == 1 ? 0 : 1);
+      if (rc == B2P_OK) rc = b2p_sync(s->ctx);
+      ipcio_close_block_read(s->in->data_block, bytes);
+    } else {
+      rc = b2p_push(s->ctx, blk, bytes, 0); /* returns once the block is copied */
+      ipcio_close_block_read(s->in->data_block, bytes);
+      if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
+                                              sh->nsub == 1 ? 0 : 1);
+      if (rc == B2P_OK && sh->nsub == 1) rc = b2p_sync(s->ctx);
+    }
     if (rc != B2P_OK) {
       multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", w->r, b2p_strerror(rc), b2p_last_error(s->ctx));
       sh->failed = 1;
@@ -231,7 +244,8 @@ static void *worker(void *arg) {
           memcpy(o, sh->spec_host, sh->obytes);
           ipcio_close_block_write(sh->out->data_block, sh->obytes);
           sh->nblocks++;
-          const double dt = now_s() - t0;
+          sh->t_last = now_s();
+          const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s per sub-band, "
                    "%.1f Msamples/s in all", sh->nblocks, dt * 1e3, bytes / dt / 1e9,
                    (double)sh->nsub * (sh->nout / s->g.npol_out) * s->g.npol * s->g.nsamp_int / dt / 1e6);
@@ -349,8 +363,21 @@ int main(int argc, char *argv[]) {
       multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
       goto done;
     }
+    const int ring_dev = ipcbuf_get_device(&s->in->data_block->buf);
+    s->ondev = ring_dev >= 0;
+    if (s->ondev) {
+      b2p_info_t ci;
+      b2p_get_info(s->ctx, &ci);
+      if ((int)ci.device != ring_dev) {
+        multilog(log, LOG_ERR, "input ring %x lives on GPU %d, this sub-band runs on GPU %d",
+                 (unsigned)s->key, ring_dev, (int)ci.device);
+        goto done;
+      }
+      multilog(log, LOG_INFO, "input ring %x is GPU-resident (device %d): no H2D copy",
+               (unsigned)s->key, ring_dev);
+    }
     /* pin the input ring's blocks for DMA (dada_cuda_dbregister role) */
-    for (uint64_t i = 0; i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
+    for (uint64_t i = 0; !s->ondev && i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
       if (b2p_register_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i), s->rbufsz) != B2P_OK)
         multilog(log, LOG_INFO, "register block %" PRIu64 ": %s", i, b2p_last_error(s->ctx));
   }
@@ -450,7 +477,8 @@ done:
   for (int r = 0; r < conf.nsub; r++) {
     sub_t *s = &sub[r];
     if (s->ctx) {
-      for (uint64_t i = 0; s->in && s->in->data_block && i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
+      for (uint64_t i = 0; !s->ondev && s->in && s->in->data_block &&
+                           i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
         b2p_unregister_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i));
       if (r == 0 && sh.spec_host) b2p_unregister_host(s->ctx, sh.spec_host);
       if (s->spec_dev) b2p_dev_free(s->ctx, s->spec_dev);
@@ -462,8 +490,10 @@ done:
   }
   free(sh.spec_host);
   dada_hdu_destroy(out);
-  multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s",
-           sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED");
+  multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s, "
+           "%.6f s from the first integration to the last output",
+           sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED",
+           sh.t_last > sh.t_first ? sh.t_last - sh.t_first : 0.0);
   multilog_close(log);
   fclose(fp_log);
   return status;

@@ -66,15 +66,20 @@ int main(int argc, char **argv) {
   int rc = EXIT_SUCCESS;
   if (fwrite(hdu->header, 1, hdu->header_size, fp) != hdu->header_size) rc = EXIT_FAILURE;
   uint64_t total = 0, nblk = 0;
-  for (;;) {
+  ipcbuf_t *db = &hdu->data_block->buf;
+  char *stage = NULL; /* a GPU-resident ring's blocks come back through host */
+  if (ipcbuf_get_device(db) >= 0 && !(stage = malloc(ipcbuf_get_bufsz(db)))) rc = EXIT_FAILURE;
+  for (; rc == EXIT_SUCCESS;) {
     uint64_t bytes = 0, bid = 0;
     char *b = ipcio_open_block_read(hdu->data_block, &bytes, &bid);
     if (!b) break;
-    if (bytes && fwrite(b, 1, bytes, fp) != bytes) rc = EXIT_FAILURE;
+    if (stage && ipcbuf_copy_out(db, stage, b, bytes) < 0) rc = EXIT_FAILURE;
+    if (bytes && fwrite(stage ? stage : b, 1, bytes, fp) != bytes) rc = EXIT_FAILURE;
     ipcio_close_block_read(hdu->data_block, bytes);
     total += bytes;
     nblk++;
   }
+  free(stage);
   fclose(fp);
   multilog(log, LOG_INFO, "dbdisk: %s: %" PRIu64 " B in %" PRIu64 " blocks", ofile, total, nblk);
   dada_hdu_unlock_read(hdu);

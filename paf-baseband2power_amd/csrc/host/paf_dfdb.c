@@ -1,0 +1,271 @@
+/*
+ * paf_dfdb -- GPU-side producer for a GPU-resident input ring
+ * (SURVEY.md 8f ranks 2 and 3).
+ *
+ * The reference's capture threads copy each received data frame into the
+ * host ring block at (idf*NCHK_NIC + chunk)*7168 (capture.c:536-541), and
+ * the GPU stage would then copy the whole block to the device.  Here raw
+ * frames (a paf_dfgen stream file stands in for the sockets) go to HBM in
+ * batches and b2p_assemble scatters them straight into a ring block that
+ * lives in GPU memory (dada_db -g), which paf_baseband2power integrates in
+ * place: the payload crosses PCIe once, as frames.
+ *
+ *   paf_dfdb -a key -b header_file -c df_file -k chunk_file [-n nchunk]
+ *            [-x ref_idf] [-s ref_sec] [-d device] [-Z] [-e dir]
+ *     Frames arrive in batches of one block's worth; block b is assembled
+ *     from batches b-1, b and b+1, so a frame may arrive up to one block
+ *     early or late (the reference keeps late frames in its temp buffer,
+ *     capture.c:525-531).  The block is zeroed first unless -Z (the
+ *     reference leaves lost frames' slots stale).
+ *
+ *   paf_dfdb -a key -b header_file -R nblocks [-f layout] [-r seed] [-d device]
+ *     Replay: fill each ring block once with the synthetic generator, then
+ *     hand the ring's blocks out nblocks times without rewriting them -- a
+ *     consumer-side throughput test of the GPU-resident ring.  layout:
+ *     bmf (default), int8:NCHAN, int16:NCHAN[:be].
+ */
+#include <getopt.h>
+#include <inttypes.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "b2p.h"
+#include "b2p_dada.h"
+#include "b2p_df.h"
+
+#define HDR_SIZE DADA_DEFAULT_HEADER_SIZE
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+static int parse_layout(const char *lay, b2p_geom_t *g) {
+  b2p_geom_bmf(g);
+  if (!strcmp(lay, "bmf")) return 0;
+  if (strncmp(lay, "int8:", 5) && strncmp(lay, "int16:", 6)) return -1;
+  const int bits = lay[3] == '8' ? 8 : 16;
+  const char *p = strchr(lay, ':') + 1;
+  g->nbit = (uint32_t)bits;
+  g->nchunk = 1;
+  g->nsamp_df = 1;
+  g->nchan_chunk = (uint32_t)atoi(p);
+  g->big_endian = (bits == 16 && strstr(p, ":be")) ? 1 : 0;
+  return g->nchan_chunk ? 0 : -1;
+}
+
+typedef struct batch_t {
+  void *frames;  /* device: n x 7232 B */
+  void *chunks;  /* device: n chunk indices */
+  uint64_t n;
+} batch_t;
+
+/* next batch of up to cap frames from the stream files, via host staging */
+static int load_batch(b2p_ctx_t *ctx, FILE *fd, FILE *fc, batch_t *b, uint64_t cap, unsigned char *hf,
+                      unsigned char *hc) {
+  const size_t got = fread(hf, B2P_DF_BYTES, cap, fd);
+  b->n = got;
+  if (!got) return 0;
+  if (fread(hc, 1, got, fc) != got) {
+    fprintf(stderr, "paf_dfdb: chunk file shorter than the frame file\n");
+    return -1;
+  }
+  if (b2p_memcpy(ctx, b->frames, hf, got * B2P_DF_BYTES, 1) != B2P_OK ||
+      b2p_memcpy(ctx, b->chunks, hc, got, 1) != B2P_OK)
+    return -1;
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  key_t key = 0;
+  const char *hfile = NULL, *dfile = NULL, *cfile = NULL, *layout = "bmf", *logdir = NULL;
+  uint64_t ref_idf = 0, ref_sec = 0, seed = 20181105, replay = 0;
+  int nchunk = 48, device = 0, nozero = 0, arg, have_key = 0;
+  while ((arg = getopt(argc, argv, "a:b:c:k:n:x:s:d:ZR:f:r:e:h")) != -1) {
+    switch (arg) {
+      case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
+      case 'b': hfile = optarg; break;
+      case 'c': dfile = optarg; break;
+      case 'k': cfile = optarg; break;
+      case 'n': nchunk = atoi(optarg); break;
+      case 'x': ref_idf = strtoull(optarg, NULL, 10); break;
+      case 's': ref_sec = strtoull(optarg, NULL, 10); break;
+      case 'd': device = atoi(optarg); break;
+      case 'Z': nozero = 1; break;
+      case 'R': replay = strtoull(optarg, NULL, 10); break;
+      case 'f': layout = optarg; break;
+      case 'r': seed = strtoull(optarg, NULL, 10); break;
+      case 'e': logdir = optarg; break;
+      default:
+        fprintf(stdout,
+                "paf_dfdb -a key -b header -c frames.df -k chunks.u8 [-n nchunk] [-x ref_idf] "
+                "[-s ref_sec] [-d dev] [-Z]\n"
+                "paf_dfdb -a key -b header -R nblocks [-f bmf|int8:N|int16:N[:be]] [-r seed] [-d dev]\n");
+        return EXIT_FAILURE;
+    }
+  }
+  if (!have_key || !hfile || (!replay && (!dfile || !cfile)) || nchunk < 1 || nchunk > 256) {
+    fprintf(stderr, "paf_dfdb: -a, -b and either -c/-k or -R are required (-h for usage)\n");
+    return EXIT_FAILURE;
+  }
+  multilog_t *log = multilog_open("paf_dfdb", 0);
+  multilog_add(log, stderr);
+  FILE *logf = NULL;
+  if (logdir) {
+    char p[4096];
+    snprintf(p, sizeof p, "%s/paf_dfdb.log", logdir);
+    if ((logf = fopen(p, "w"))) multilog_add(log, logf);
+  }
+  int status = EXIT_FAILURE;
+  dada_hdu_t *hdu = dada_hdu_create(log);
+  dada_hdu_set_key(hdu, key);
+  b2p_ctx_t *ctx = NULL;
+  FILE *fd = NULL, *fc = NULL;
+  unsigned char *hf = NULL, *hc = NULL;
+  batch_t bt[3] = {{0}};
+  unsigned long long *d_cnt = NULL;
+  int locked = 0;
+  if (dada_hdu_connect(hdu) < 0 || dada_hdu_lock_write(hdu) < 0) {
+    multilog(log, LOG_ERR, "cannot attach/lock ring %x for writing", (unsigned)key);
+    goto done;
+  }
+  locked = 1;
+  ipcbuf_t *db = &hdu->data_block->buf;
+  const uint64_t bufsz = ipcbuf_get_bufsz(db), nbufs = ipcbuf_get_nbufs(db);
+  if (ipcbuf_get_device(db) < 0) {
+    multilog(log, LOG_ERR, "ring %x is not GPU-resident (create it with dada_db -g)", (unsigned)key);
+    goto done;
+  }
+  device = ipcbuf_get_device(db);
+
+  b2p_geom_t g;
+  if (replay) {
+    if (parse_layout(layout, &g) < 0) {
+      multilog(log, LOG_ERR, "unknown layout '%s'", layout);
+      goto done;
+    }
+  } else {
+    b2p_geom_bmf(&g);
+    g.nchunk = (uint32_t)nchunk;
+  }
+  const uint64_t fb = b2p_frame_bytes(&g);
+  if (!fb || bufsz % fb) {
+    multilog(log, LOG_ERR, "ring block %" PRIu64 " B is not a whole number of %" PRIu64 "-B frames",
+             bufsz, fb);
+    goto done;
+  }
+  g.nsamp_int = bufsz / fb * g.nsamp_df;
+  int rc = b2p_open(&ctx, &g, device);
+  if (rc != B2P_OK) {
+    multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
+    goto done;
+  }
+
+  /* header ring first (diskdb.cu:75-92 role) */
+  char *hb = ipcbuf_get_next_write(hdu->header_block);
+  if (!hb || fileread(hfile, hb, HDR_SIZE) < 0 || ipcbuf_mark_filled(hdu->header_block, HDR_SIZE) < 0) {
+    multilog(log, LOG_ERR, "cannot pass header %s", hfile);
+    goto done;
+  }
+  const double t0 = now_s();
+  uint64_t nblk = 0;
+  if (replay) {
+    for (uint64_t i = 0; i < replay; i++) {
+      uint64_t bid;
+      char *blk = ipcio_open_block_write(hdu->data_block, &bid);
+      if (!blk) goto done;
+      if (i < nbufs) { /* first pass: synthetic block i, then re-used as is */
+        if (b2p_fill_synthetic(ctx, blk, bufsz, seed, 0, i, 0) != B2P_OK || b2p_sync(ctx) != B2P_OK) {
+          multilog(log, LOG_ERR, "fill: %s", b2p_last_error(ctx));
+          goto done;
+        }
+      }
+      ipcio_close_block_write(hdu->data_block, bufsz);
+      nblk++;
+    }
+  } else {
+    const uint64_t block_ndf = bufsz / ((uint64_t)nchunk * B2P_DF_PAYLOAD_BYTES);
+    const uint64_t cap = block_ndf * (uint64_t)nchunk; /* frames per batch */
+    if (!(fd = fopen(dfile, "rb")) || !(fc = fopen(cfile, "rb"))) {
+      multilog(log, LOG_ERR, "cannot open %s / %s", dfile, cfile);
+      goto done;
+    }
+    hf = malloc(cap * B2P_DF_BYTES);
+    hc = malloc(cap);
+    if (!hf || !hc) goto done;
+    b2p_register_host(ctx, hf, cap * B2P_DF_BYTES); /* pinned: full PCIe rate */
+    for (int k = 0; k < 3; k++)
+      if (b2p_dev_alloc(ctx, &bt[k].frames, cap * B2P_DF_BYTES) != B2P_OK ||
+          b2p_dev_alloc(ctx, &bt[k].chunks, cap) != B2P_OK)
+        goto done;
+    if (b2p_dev_alloc(ctx, (void **)&d_cnt, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK)
+      goto done;
+    b2p_df_hdr_t ref = {1, ref_idf, ref_sec, 0, 0, 0.0};
+    /* window: slot (b+2)%3 = batch b-1, b%3 = batch b, (b+1)%3 = batch b+1 */
+    if (load_batch(ctx, fd, fc, &bt[0], cap, hf, hc) < 0 ||
+        load_batch(ctx, fd, fc, &bt[1], cap, hf, hc) < 0)
+      goto done;
+    uint64_t placed_all = 0, sent_all = 0;
+    for (uint64_t b = 0; bt[b % 3].n; b++) {
+      uint64_t bid;
+      char *blk = ipcio_open_block_write(hdu->data_block, &bid);
+      if (!blk) goto done;
+      if (!nozero && b2p_memset(ctx, blk, 0, bufsz) != B2P_OK) goto done;
+      if (b2p_memset(ctx, d_cnt, 0, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) goto done;
+      const int slots[3] = {(int)((b + 2) % 3), (int)(b % 3), (int)((b + 1) % 3)};
+      for (int j = 0; j < 3; j++) {
+        batch_t *x = &bt[slots[j]];
+        if ((j == 0 && b == 0) || !x->n) continue;
+        if (b2p_assemble(ctx, x->frames, x->n, B2P_DF_BYTES, x->chunks, ref.idf, ref.sec, blk,
+                         block_ndf, (uint32_t)nchunk, d_cnt) != B2P_OK) {
+          multilog(log, LOG_ERR, "assemble: %s", b2p_last_error(ctx));
+          goto done;
+        }
+      }
+      unsigned long long cnt[256 + 3];
+      if (b2p_sync(ctx) != B2P_OK ||
+          b2p_memcpy(ctx, cnt, d_cnt, (nchunk + 3) * sizeof(unsigned long long), 2) != B2P_OK)
+        goto done;
+      uint64_t placed = 0;
+      for (int c = 0; c < nchunk; c++) placed += cnt[c];
+      placed_all += placed;
+      sent_all += bt[b % 3].n;
+      ipcio_close_block_write(hdu->data_block, bufsz);
+      nblk++;
+      multilog(log, LOG_INFO, "block %" PRIu64 ": %" PRIu64 " of %" PRIu64 " frames placed (%.3f%% lost), "
+               "%llu with a bad chunk", b, placed, cap, 100.0 * (double)(cap - placed) / (double)cap,
+               cnt[nchunk + 2]);
+      b2p_df_ref_advance(&ref, block_ndf);
+      /* batch b-1 is done with: its slot takes batch b+2 */
+      if (load_batch(ctx, fd, fc, &bt[(b + 2) % 3], cap, hf, hc) < 0) goto done;
+    }
+    multilog(log, LOG_INFO, "%" PRIu64 " frames read, %" PRIu64 " placed", sent_all, placed_all);
+  }
+  const double el = now_s() - t0;
+  multilog(log, LOG_INFO, "dfdb: %" PRIu64 " blocks of %" PRIu64 " B in %.3f s (%.2f GB/s of blocks)",
+           nblk, bufsz, el, el > 0 ? (double)nblk * bufsz / el / 1e9 : 0.0);
+  status = EXIT_SUCCESS;
+
+done:
+  if (locked) dada_hdu_unlock_write(hdu); /* ends the transfer (EOD) */
+  dada_hdu_destroy(hdu);
+  if (ctx) {
+    for (int k = 0; k < 3; k++) {
+      if (bt[k].frames) b2p_dev_free(ctx, bt[k].frames);
+      if (bt[k].chunks) b2p_dev_free(ctx, bt[k].chunks);
+    }
+    if (d_cnt) b2p_dev_free(ctx, d_cnt);
+    if (hf) b2p_unregister_host(ctx, hf);
+    b2p_close(ctx);
+  }
+  free(hf);
+  free(hc);
+  if (fd) fclose(fd);
+  if (fc) fclose(fc);
+  multilog_close(log);
+  if (logf) fclose(logf);
+  return status;
+}

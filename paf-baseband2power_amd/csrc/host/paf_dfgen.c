@@ -6,9 +6,10 @@
  *
  *   paf_dfgen -i in.dada -o out.df -n NCHK [-x ref_idf] [-s ref_sec]
  *             [-b beam] [-e epoch] [-f freq0_MHz] [-r seed] [-l lost_per_mille]
- *             [-c chunks.u8]
+ *             [-c chunks.u8] [-w window]
  * Frame k*NCHK + c carries chunk c and DF number ref_idf + k, wrapping into
- * the next 27-s period (sync.c:119-125); -r shuffles the arrival order, -l
+ * the next 27-s period (sync.c:119-125); -r shuffles the arrival order
+ * (within consecutive windows of -w frames, default the whole file), -l
  * drops frames; -c writes the per-frame chunk index (what capture derives
  * from the sender's IP, capture.c:571-584).
  */
@@ -32,8 +33,9 @@ int main(int argc, char **argv) {
   const char *in = NULL, *out = NULL, *chunks = NULL;
   uint64_t ref_idf = 0, ref_sec = 0, seed = 0;
   int nchk = 48, beam = 0, epoch = 0, lost = 0, arg;
+  uint64_t window = 0;
   double freq0 = 1300.0;
-  while ((arg = getopt(argc, argv, "i:o:n:x:s:b:e:f:r:l:c:h")) != -1) {
+  while ((arg = getopt(argc, argv, "i:o:n:x:s:b:e:f:r:l:c:w:h")) != -1) {
     switch (arg) {
       case 'i': in = optarg; break;
       case 'o': out = optarg; break;
@@ -46,9 +48,10 @@ int main(int argc, char **argv) {
       case 'r': seed = strtoull(optarg, NULL, 10); break;
       case 'l': lost = atoi(optarg); break;
       case 'c': chunks = optarg; break;
+      case 'w': window = strtoull(optarg, NULL, 10); break;
       default:
         fprintf(stdout, "paf_dfgen -i in.dada -o out.df -n NCHK [-x idf] [-s sec] [-b beam] "
-                        "[-e epoch] [-f freq0] [-r seed] [-l lost_per_mille] [-c chunks.u8]\n");
+                        "[-e epoch] [-f freq0] [-r seed] [-l lost_per_mille] [-c chunks.u8] [-w window]\n");
         return EXIT_FAILURE;
     }
   }
@@ -74,12 +77,16 @@ int main(int argc, char **argv) {
   if (fread(data, 1, pay, fi) != pay) { fprintf(stderr, "paf_dfgen: short read\n"); return EXIT_FAILURE; }
   fclose(fi);
   for (uint64_t k = 0; k < n; k++) order[k] = k;
-  if (seed) { /* Fisher-Yates arrival order */
+  if (seed) { /* Fisher-Yates arrival order, window by window */
     rng_state = seed;
-    for (uint64_t k = n - 1; k > 0; k--) {
-      uint64_t j = rnd() % (k + 1), t = order[k];
-      order[k] = order[j];
-      order[j] = t;
+    const uint64_t w = window ? window : n;
+    for (uint64_t w0 = 0; w0 < n; w0 += w) {
+      const uint64_t m = n - w0 < w ? n - w0 : w;
+      for (uint64_t k = m - 1; k > 0; k--) {
+        uint64_t j = rnd() % (k + 1), t = order[w0 + k];
+        order[w0 + k] = order[w0 + j];
+        order[w0 + j] = t;
+      }
     }
   }
   FILE *fo = fopen(out, "wb");

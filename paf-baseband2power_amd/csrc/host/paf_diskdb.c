@@ -98,15 +98,31 @@ static int do_diskdb(conf_t *conf) {
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   uint64_t block_id, total = 0, nblk = 0;
+  /* a GPU-resident ring (dada_db -g) takes each block through host staging */
+  ipcbuf_t *db = &conf->hdu->data_block->buf;
+  char *stage = NULL;
+  if (ipcbuf_get_device(db) >= 0 && !(stage = malloc(conf->rbufsz))) {
+    multilog(conf->log, LOG_ERR, "cannot allocate %" PRIu64 " B of staging", conf->rbufsz);
+    return EXIT_FAILURE;
+  }
   while (!feof(conf->fp)) {
     char *curbuf = ipcio_open_block_write(conf->hdu->data_block, &block_id);
-    if (!curbuf) return EXIT_FAILURE;
-    size_t n = fread(curbuf, 1, conf->rbufsz, conf->fp);
+    if (!curbuf) {
+      free(stage);
+      return EXIT_FAILURE;
+    }
+    size_t n = fread(stage ? stage : curbuf, 1, conf->rbufsz, conf->fp);
+    if (stage && ipcbuf_copy_in(db, curbuf, stage, n) < 0) {
+      multilog(conf->log, LOG_ERR, "copy into device block failed");
+      free(stage);
+      return EXIT_FAILURE;
+    }
     ipcio_close_block_write(conf->hdu->data_block, n);
     total += n;
     nblk++;
     if (n < conf->rbufsz) break; /* the short block already ended the transfer */
   }
+  free(stage);
   clock_gettime(CLOCK_MONOTONIC, &t1);
   double el = (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
   multilog(conf->log, LOG_INFO, "diskdb: %" PRIu64 " B in %" PRIu64 " blocks, %.3f s (%.2f GB/s)",

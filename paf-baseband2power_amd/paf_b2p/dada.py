@@ -56,6 +56,11 @@ def dlib():
         L.ipcbuf_enable_eod.argtypes = [P]
         L.ipcbuf_get_write_count.restype = C.c_uint64
         L.ipcbuf_get_write_count.argtypes = [P]
+        L.ipcbuf_get_device.argtypes = [P]
+        L.ipcbuf_copy_in.argtypes = [P, P, P, C.c_uint64]
+        L.ipcbuf_copy_out.argtypes = [P, P, P, C.c_uint64]
+        L.dada_db_create_work.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint64,
+                                          C.c_uint64, C.c_int]
         _dl = L
     return _dl
 
@@ -113,7 +118,18 @@ def header_block(text: bytes | str, size: int = HDR_SIZE) -> bytes:
 # ---- rings --------------------------------------------------------------------------
 
 def create_ring(key: int, nbufs: int, bufsz: int, nreaders: int = 1, hdr_nbufs: int = 8,
-                hdr_bufsz: int = HDR_SIZE) -> None:
+                hdr_bufsz: int = HDR_SIZE, device: int = -1) -> None:
+    """device >= 0: data blocks in that GPU's memory (dada_db -g).  That ring
+    is made by the dada_db executable, never in this process: its holder is
+    forked, and forking a process that runs threads (torch) is not safe."""
+    if device >= 0:
+        import subprocess
+        r = subprocess.run([os.path.join(BIN_DIR, "dada_db"), "-k", f"{key:x}", "-b", str(bufsz),
+                            "-n", str(nbufs), "-r", str(nreaders), "-H", str(hdr_bufsz),
+                            "-g", str(device)], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            raise OSError(f"dada_db -g {device} {key:x}: {r.stderr.strip()}")
+        return
     if dlib().dada_db_create(key, nbufs, bufsz, nreaders, hdr_nbufs, hdr_bufsz) != 0:
         raise OSError(C.get_errno(), f"dada_db_create {key:x}")
 
@@ -141,6 +157,7 @@ class Hdu:
         self.data = s.data_block        # ipcio_t* (its first member is the ipcbuf_t)
         self.hdr = s.header_block       # ipcbuf_t*
         self.bufsz = L.ipcbuf_get_bufsz(self.data)
+        self.device = L.ipcbuf_get_device(self.data)  # -1: host ring
 
     # writer ----------------------------------------------------------------------
     def write_header(self, text: bytes | str) -> None:
@@ -161,7 +178,9 @@ class Hdu:
         n = len(data)
         if n > self.bufsz:
             raise ValueError("block too large")
-        C.memmove(p, bytes(data), n)
+        src = bytes(data)
+        if L.ipcbuf_copy_in(self.data, p, src, n) != 0:  # hipMemcpy for a device ring
+            raise OSError("copy into block")
         L.ipcio_close_block_write(self.data, n)
 
     # reader ----------------------------------------------------------------------
@@ -179,9 +198,11 @@ class Hdu:
         p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
         if not p:
             return None
-        out = C.string_at(p, n.value)
+        buf = C.create_string_buffer(n.value)
+        if n.value and L.ipcbuf_copy_out(self.data, buf, p, n.value) != 0:
+            raise OSError("copy out of block")
         L.ipcio_close_block_read(self.data, n.value)
-        return out
+        return buf.raw
 
     def eod(self) -> bool:
         return bool(dlib().ipcbuf_eod(self.data))

@@ -55,10 +55,14 @@ def _bin(name: str) -> str:
 
 def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
-        hfname: str | None = None, outfiles: list | None = None, gather: bool = False) -> list:
+        hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
+        device_ring: bool = False) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
-    sub-bands and gathers their spectra to its first GPU)."""
+    sub-bands and gathers their spectra to its first GPU).
+    device_ring=True puts each input ring's blocks on its chain's GPU
+    (dada_db -g): paf_diskdb copies into HBM and
+    paf_baseband2power integrates the block in place."""
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
                              timeout, hfname)
@@ -79,7 +83,8 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
                     f.write(f"key {k:x}\n")
             dada.destroy_ring(kin)
             dada.destroy_ring(kout)
-            dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"])
+            dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"],
+                             device=(gpu + r) if device_ring else -1)
             keys.append(kin)
             obytes = c["b2p_rbufsz"] * npol_out
             dada.create_ring(kout, c["b2p_nbuf"], obytes, c["b2p_nreader"])
@@ -208,10 +213,12 @@ def main(argv=None) -> int:
     ap.add_argument("-m", "--mean", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="one process for all sub-bands, spectra gathered to the first GPU")
+    ap.add_argument("--device-ring", action="store_true",
+                    help="input ring blocks in GPU memory (dada_db -g): no H2D in the integrator")
     a = ap.parse_args(argv)
     files = a.dfname if a.subbands > 1 or a.gather else a.dfname[0]
     outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean,
-               gather=a.gather)
+               gather=a.gather, device_ring=a.device_ring)
     print("\n".join(outs))
     return 0
 

@@ -281,3 +281,24 @@ def test_paf_baseband2power_cli_help_and_no_gpu(tmp_path, have_gpu):
     assert r.returncode == 1
     log = (tmp_path / "paf_baseband2power.log").read_text()
     assert "START PAF_PROCESS" in log and "no HIP device" in log
+
+
+def test_device_ring_without_gpu_fails_cleanly(tmp_path, have_gpu):
+    # dada_db -g: the holder cannot get a device here, so creation fails,
+    # says why, and leaves no segment behind
+    if have_gpu:
+        pytest.skip("a GPU is present")
+    key = fresh_key()
+    r = subprocess.run([os.path.join(BIN, "dada_db"), "-k", f"{key:x}", "-b", "4096", "-n", "2",
+                        "-g", "0"], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "holder failed" in r.stderr
+    with pytest.raises(OSError):
+        dada.Hdu(key, "R")
+    assert not dada.destroy_ring(key)
+
+
+def test_host_ring_reports_no_device(ring):
+    key = ring(2, 4096)
+    with dada.Hdu(key, "W") as w:
+        assert w.device == -1

@@ -1,0 +1,164 @@
+"""GPU-resident DADA rings: data blocks in HBM owned by
+a holder process (dada_db -g) and shared through HIP IPC handles.
+
+* bytes written by one process come out of another unchanged;
+* the three-process pipeline with the input ring on the GPU
+  (paf_diskdb copies into HBM, paf_baseband2power integrates in place)
+  matches the oracle;
+* paf_dfdb assembles a raw data-frame stream (paf_dfgen) on the GPU straight
+  into the ring block, and the spectra match the oracle of the original
+  blocks, with and without lost frames;
+* replay mode hands out re-used blocks, spectra match the oracle.
+"""
+import os
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+from paf_b2p import dada, pipeline
+
+pytestmark = pytest.mark.gpu
+SEED = 20181105
+BIN = dada.BIN_DIR
+HDR = os.path.join(os.path.dirname(BIN), "conf", "header_baseband2power.txt")
+_next = [0x7a00 + (os.getpid() % 32) * 32]
+
+
+def fresh_key():
+    k = _next[0]
+    _next[0] += 2
+    dada.destroy_ring(k)
+    return k
+
+
+def _wait(procs, timeout=300):
+    t_end = time.time() + timeout
+    while any(p.poll() is None for p in procs) and time.time() < t_end:
+        if any(p.poll() not in (None, 0) for p in procs):
+            break
+        time.sleep(0.05)
+    bad = [p for p in procs if p.poll() != 0]
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    errs = [p.stderr.read().decode(errors="replace") for p in procs]
+    msgs = [f"{os.path.basename(p.args[0])} rc={p.returncode}: {e[-600:]}" for p, e in zip(procs, errs)]
+    assert not bad, "\n".join(msgs)
+    return errs
+
+
+def test_device_ring_bytes_cross_processes(gpu, tmp_path):
+    key = fresh_key()
+    dada.create_ring(key, 3, 1 << 16, device=0)
+    try:
+        out = tmp_path / "o.dada"
+        rd = subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{key:x}", "-o", str(out)],
+                              stderr=subprocess.PIPE)
+        rng = np.random.default_rng(1)
+        blocks = [rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes() for _ in range(5)]
+        blocks.append(rng.integers(0, 256, 1000, dtype=np.uint8).tobytes())  # short = EOD
+        with dada.Hdu(key, "W") as w:
+            assert w.device == 0
+            w.write_header("HDR_SIZE 4096\nNBIT 8\n")
+            for b in blocks:
+                w.write_block(b)
+        _wait([rd])
+        hdr, data = dada.read_dada_file(str(out))
+        assert data.tobytes() == b"".join(blocks)
+    finally:
+        assert dada.destroy_ring(key)
+    with pytest.raises(OSError):  # destroyed: the holder is gone with it
+        dada.Hdu(key, "R")
+
+
+def test_pipeline_with_device_input_ring(gpu, tmp_path):
+    from test_gpu_pipeline import spectra, write_conf
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=64 * 128)
+    nblk = 3
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, SEED, 0, 11)
+    src = tmp_path / "bmf.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    conf = tmp_path / "p.conf"
+    kin, kout = fresh_key(), fresh_key()
+    write_conf(conf, 64, 48, 7168, 336, kin, kout, "header_baseband2power.txt")
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, str(src), layout="bmf", timeout=600,
+                        device_ring=True)
+    _, sp = spectra(outs[0], g.nout)
+    assert sp.shape == (nblk, g.nout)
+    for i in range(nblk):
+        blk = payload[i * g.block_bytes:(i + 1) * g.block_bytes]
+        assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk, nthreads=8).view(np.uint32))
+    log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
+    assert "GPU-resident" in log and "FINISH PAF_PROCESS: 3 integrations" in log
+
+
+def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz):
+    dada.create_ring(kin, nbufs, bufsz, device=0)
+    dada.create_ring(kout, 4, nout * 4)
+    try:
+        out = tmp_path / "power.dada"
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}",
+                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", layout],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen(producer, stderr=subprocess.PIPE)]
+        msgs = _wait(procs)
+        _, data = dada.read_dada_file(str(out))
+        return data.view(np.float32).reshape(-1, nout), msgs[2]
+    finally:
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+
+
+@pytest.mark.parametrize("lost", [0, 40])
+def test_dfdb_assembles_stream_into_device_ring(gpu, tmp_path, lost):
+    nchunk, block_ndf, nblk = 48, 64, 4
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=block_ndf * 128)
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, SEED, 2, 5)
+    src = tmp_path / "bmf.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
+    ref_idf, ref_sec = 249900, 27 * 40  # the stream crosses a 27-s period
+    per_block = block_ndf * nchunk
+    subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(nchunk),
+                    "-c", str(ck), "-x", str(ref_idf), "-s", str(ref_sec), "-r", "7",
+                    "-w", str(per_block * 3 // 2), "-l", str(lost)], check=True, capture_output=True)
+    kin, kout = fresh_key(), fresh_key()
+    sp, log = _run_chain(tmp_path, kin, kout,
+                         [os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-c", str(df),
+                          "-k", str(ck), "-n", str(nchunk), "-x", str(ref_idf), "-s", str(ref_sec)],
+                         "bmf", g.nout, 3, g.block_bytes)
+    dfs = np.fromfile(df, dtype=np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, dtype=np.uint8)
+    assert sp.shape[0] == nblk
+    idf, sec = ref_idf, ref_sec
+    for b in range(nblk):
+        want = np.zeros(g.block_bytes, np.uint8)  # lost frames read as zeros
+        co.assemble(dfs, chunk, idf, sec, want, block_ndf, nchunk)
+        if not lost:
+            assert np.array_equal(want, payload[b * g.block_bytes:(b + 1) * g.block_bytes])
+        assert np.array_equal(sp[b].view(np.uint32), co.power(g, want, nthreads=8).view(np.uint32))
+        gi = idf + block_ndf
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27
+    assert ("0.000% lost" in log) == (lost == 0)
+
+
+def test_replay_reuses_device_blocks(gpu, tmp_path):
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    nbufs, nrep = 3, 8
+    kin, kout = fresh_key(), fresh_key()
+    sp, _ = _run_chain(tmp_path, kin, kout,
+                       [os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-R", str(nrep),
+                        "-f", "int8:256", "-r", str(SEED)],
+                       "int8:256", g.nout, nbufs, g.block_bytes)
+    assert sp.shape[0] == nrep
+    want = [co.power(g, co.fill_synthetic(g, g.block_bytes, SEED, 0, i)) for i in range(nbufs)]
+    for i in range(nrep):
+        assert np.array_equal(sp[i].view(np.uint32), want[i % nbufs].view(np.uint32))

@@ -10,7 +10,7 @@ import pytest
 from conftest import REPO
 
 SRC = [os.path.join(REPO, "paf-baseband2power_amd", "csrc", "dada", f)
-       for f in ("dada_ring.c", "ascii_header.c")]
+       for f in ("dada_ring.c", "dada_device.c", "ascii_header.c")]
 DRIVER = os.path.join(REPO, "tests", "c", "ring_stress.c")
 
 
@@ -19,7 +19,7 @@ def test_dada_layer_under_sanitizer(tmp_path, san, key):
     exe = tmp_path / "ring_stress"
     cmd = ["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", f"-fsanitize={san}",
            "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"), DRIVER, *SRC,
-           "-o", str(exe), "-pthread"]
+           "-o", str(exe), "-pthread", "-ldl"]
     subprocess.run(cmd, check=True)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",

@@ -1,0 +1,93 @@
+"""Measure the GPU-resident ring path:
+
+  paf_dfdb -R (replay producer) -> device ring (dada_db -g) ->
+  paf_baseband2power (integrates the block in place) -> host ring -> paf_dbdisk
+
+on full-size BMF blocks (8192 frames x 48 chunks, 2.625 GiB).  The producer
+re-hands the ring's blocks without rewriting them, so the figure is what the
+consumer sustains through the ring: integrate launch + sync + semaphores +
+output block per integration.  Prints one JSON line.
+
+  python tools/bench_ring.py [--blocks 200] [--ndf 8192]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "paf-baseband2power_amd"))
+from paf_b2p import dada  # noqa: E402
+
+BIN = dada.BIN_DIR
+HDR = os.path.join(os.path.dirname(BIN), "conf", "header_baseband2power.txt")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=200)
+    ap.add_argument("--ndf", type=int, default=8192)
+    ap.add_argument("--nbufs", type=int, default=4)
+    a = ap.parse_args()
+    bufsz = a.ndf * 48 * 7168
+    nout = 336
+    kin, kout = 0x7e00, 0x7e10
+    for k in (kin, kout):
+        dada.destroy_ring(k)
+    d = tempfile.mkdtemp(prefix="bench_ring_")
+    dada.create_ring(kin, a.nbufs, bufsz, device=0)
+    dada.create_ring(kout, 8, nout * 4)
+    procs = []
+    try:
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o",
+                                   os.path.join(d, "power.dada")], stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
+                                   f"{kout:x}", "-c", d, "-d", "0", "-f", "bmf"],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR,
+                                   "-R", str(a.blocks), "-f", "bmf"], stderr=subprocess.PIPE)]
+        for p in procs:
+            p.wait(timeout=600)
+        wall = time.perf_counter() - t0
+        errs = [p.stderr.read().decode(errors="replace") for p in procs]
+        if any(p.returncode for p in procs):
+            print("\n".join(e[-800:] for e in errs), file=sys.stderr)
+            return 1
+        log = open(os.path.join(d, "paf_baseband2power.log")).read()
+        per = [float(m) for m in re.findall(r"integration \d+: ([0-9.]+) ms", log)]
+        m = re.search(r"FINISH PAF_PROCESS: (\d+) integrations.* ([0-9.]+) s from the first", log)
+        steady = per[a.nbufs + 1:] or per
+        med = statistics.median(steady)
+        samples = a.ndf * 128 * nout * 2  # channels x pols x time, as bench.py counts
+        n_int, el = (int(m.group(1)), float(m.group(2))) if m else (0, 0.0)
+        print(json.dumps({
+            "path": "device ring (dada_db -g) -> paf_baseband2power in place",
+            "block_bytes": bufsz, "blocks": a.blocks, "integrations_logged": len(per),
+            "consumer_ms_per_block_median": round(med, 3),
+            "consumer_GBps": round(bufsz / (med * 1e-3) / 1e9, 1),
+            "consumer_Msamples_s": round(samples / (med * 1e-3) / 1e6, 1),
+            "consumer_elapsed_s": el,
+            "ring_Msamples_s": round(n_int * samples / el / 1e6, 1) if el else None,
+            "ring_GBps": round(n_int * bufsz / el / 1e9, 1) if el else None,
+            "wall_s_incl_startup": round(wall, 2),
+        }), flush=True)
+        return 0
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

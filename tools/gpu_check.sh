@@ -5,6 +5,8 @@
 #   usage: tools/gpu_check.sh [steps...]   steps: smoke tests bench prof pmc
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
+# device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
+export DADA_HOLDER_IDLE_S=900
 OUT=gpurun_out
 mkdir -p "$OUT"
 STEPS=${*:-smoke tests bench prof}
@@ -45,6 +47,7 @@ for s in $STEPS; do
                 run asm_v${v}_g${g} 300 env B2P_ASM_VARIANT=$v B2P_ASM_GRID=$g python3 tools/bench_assemble.py \
                   --steps 10 --warmup 2 --order tm || exit $?
               done; done ;;
+    ring) run bench_ring 600 python3 tools/bench_ring.py --blocks 200 ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
@@ -57,6 +60,12 @@ for s in $STEPS; do
             -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
             -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
+    profbmf) run prof_bmf 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bmf" -o run \
+            -- python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
+    pmcbmf) run pmc_fetch_bmf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_bmf" -o run \
+            -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 &&
+         run pmc_write_bmf 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_bmf" -o run \
+            -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
