@@ -21,7 +21,8 @@
  *   paf_dfdb -a key -b header_file -R nblocks [-f layout] [-r seed] [-d device]
  *     Replay: fill each ring block once with the synthetic generator, then
  *     hand the ring's blocks out nblocks times without rewriting them -- a
- *     consumer-side throughput test of the GPU-resident ring.  layout:
+ *     consumer-side throughput test of a GPU-resident ring (or, for
+ *     comparison, of a host ring, whose consumer copies each block H2D).  layout:
  *     bmf (default), int8:NCHAN, int16:NCHAN[:be].
  */
 #include <getopt.h>
@@ -135,11 +136,12 @@ int main(int argc, char **argv) {
   locked = 1;
   ipcbuf_t *db = &hdu->data_block->buf;
   const uint64_t bufsz = ipcbuf_get_bufsz(db), nbufs = ipcbuf_get_nbufs(db);
-  if (ipcbuf_get_device(db) < 0) {
+  const int ondev = ipcbuf_get_device(db) >= 0;
+  if (!ondev && !replay) {
     multilog(log, LOG_ERR, "ring %x is not GPU-resident (create it with dada_db -g)", (unsigned)key);
     goto done;
   }
-  device = ipcbuf_get_device(db);
+  if (ondev) device = ipcbuf_get_device(db);
 
   b2p_geom_t g;
   if (replay) {
@@ -173,12 +175,15 @@ int main(int argc, char **argv) {
   const double t0 = now_s();
   uint64_t nblk = 0;
   if (replay) {
+    void *stage = NULL; /* a host ring's blocks are generated on the GPU, then copied down */
+    if (!ondev && b2p_dev_alloc(ctx, &stage, bufsz) != B2P_OK) goto done;
     for (uint64_t i = 0; i < replay; i++) {
       uint64_t bid;
       char *blk = ipcio_open_block_write(hdu->data_block, &bid);
       if (!blk) goto done;
       if (i < nbufs) { /* first pass: synthetic block i, then re-used as is */
-        if (b2p_fill_synthetic(ctx, blk, bufsz, seed, 0, i, 0) != B2P_OK || b2p_sync(ctx) != B2P_OK) {
+        if (b2p_fill_synthetic(ctx, ondev ? (void *)blk : stage, bufsz, seed, 0, i, 0) != B2P_OK ||
+            b2p_sync(ctx) != B2P_OK || (!ondev && b2p_memcpy(ctx, blk, stage, bufsz, 2) != B2P_OK)) {
           multilog(log, LOG_ERR, "fill: %s", b2p_last_error(ctx));
           goto done;
         }
@@ -186,6 +191,7 @@ int main(int argc, char **argv) {
       ipcio_close_block_write(hdu->data_block, bufsz);
       nblk++;
     }
+    if (stage) b2p_dev_free(ctx, stage);
   } else {
     const uint64_t block_ndf = bufsz / ((uint64_t)nchunk * B2P_DF_PAYLOAD_BYTES);
     const uint64_t cap = block_ndf * (uint64_t)nchunk; /* frames per batch */

@@ -97,8 +97,8 @@ def test_pipeline_with_device_input_ring(gpu, tmp_path):
     assert "GPU-resident" in log and "FINISH PAF_PROCESS: 3 integrations" in log
 
 
-def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz):
-    dada.create_ring(kin, nbufs, bufsz, device=0)
+def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz, device=0):
+    dada.create_ring(kin, nbufs, bufsz, device=device)
     dada.create_ring(kout, 4, nout * 4)
     try:
         out = tmp_path / "power.dada"
@@ -150,14 +150,15 @@ def test_dfdb_assembles_stream_into_device_ring(gpu, tmp_path, lost):
     assert ("0.000% lost" in log) == (lost == 0)
 
 
-def test_replay_reuses_device_blocks(gpu, tmp_path):
+@pytest.mark.parametrize("device", [0, -1])  # GPU-resident ring, and a host ring for contrast
+def test_replay_reuses_blocks(gpu, tmp_path, device):
     g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
     nbufs, nrep = 3, 8
     kin, kout = fresh_key(), fresh_key()
     sp, _ = _run_chain(tmp_path, kin, kout,
                        [os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-R", str(nrep),
                         "-f", "int8:256", "-r", str(SEED)],
-                       "int8:256", g.nout, nbufs, g.block_bytes)
+                       "int8:256", g.nout, nbufs, g.block_bytes, device=device)
     assert sp.shape[0] == nrep
     want = [co.power(g, co.fill_synthetic(g, g.block_bytes, SEED, 0, i)) for i in range(nbufs)]
     for i in range(nrep):

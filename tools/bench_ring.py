@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=200)
     ap.add_argument("--ndf", type=int, default=8192)
     ap.add_argument("--nbufs", type=int, default=4)
+    ap.add_argument("--host", action="store_true",
+                    help="host ring instead (the consumer copies every block H2D)")
     a = ap.parse_args()
     bufsz = a.ndf * 48 * 7168
     nout = 336
@@ -42,7 +44,7 @@ def main():
     for k in (kin, kout):
         dada.destroy_ring(k)
     d = tempfile.mkdtemp(prefix="bench_ring_")
-    dada.create_ring(kin, a.nbufs, bufsz, device=0)
+    dada.create_ring(kin, a.nbufs, bufsz, device=-1 if a.host else 0)
     dada.create_ring(kout, 8, nout * 4)
     procs = []
     try:
@@ -69,7 +71,8 @@ def main():
         samples = a.ndf * 128 * nout * 2  # channels x pols x time, as bench.py counts
         n_int, el = (int(m.group(1)), float(m.group(2))) if m else (0, 0.0)
         print(json.dumps({
-            "path": "device ring (dada_db -g) -> paf_baseband2power in place",
+            "path": ("host ring -> paf_baseband2power (pinned H2D, overlapped)" if a.host else
+                     "device ring (dada_db -g) -> paf_baseband2power in place"),
             "block_bytes": bufsz, "blocks": a.blocks, "integrations_logged": len(per),
             "consumer_ms_per_block_median": round(med, 3),
             "consumer_GBps": round(bufsz / (med * 1e-3) / 1e9, 1),

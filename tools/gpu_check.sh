@@ -47,7 +47,8 @@ for s in $STEPS; do
                 run asm_v${v}_g${g} 300 env B2P_ASM_VARIANT=$v B2P_ASM_GRID=$g python3 tools/bench_assemble.py \
                   --steps 10 --warmup 2 --order tm || exit $?
               done; done ;;
-    ring) run bench_ring 600 python3 tools/bench_ring.py --blocks 200 ;;
+    ring) run bench_ring 600 python3 tools/bench_ring.py --blocks 200 &&
+          run bench_ring_host 600 python3 tools/bench_ring.py --blocks 20 --host ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
