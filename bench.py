@@ -13,6 +13,11 @@ Multi-GPU (torchrun, one process per GPU): sub-band r on GPU r, no data-path
 collective; the K spectra of every rank are gathered to rank 0 over RCCL
 (torch.distributed "nccl") inside the timed region (configs[3]/[4]).
 value = all ranks' samples / max-over-ranks time  (weak scaling).
+--split time instead cuts ONE sub-band's integration along time across the
+ranks (second mode): each rank integrates its share, emits
+exact uint64 partials, and one RCCL reduce (SUM) of the K x nout partials
+brings them to rank 0, which rounds once to fp32 (strong scaling; value =
+one sub-band's samples / max-over-ranks time).
 
 Prints ONE JSON line on rank 0.  Options beyond the driver contract:
   --config c2|c5|bmf|c3   workload (c3 = pinned host buffer, H2D overlapped;
@@ -55,6 +60,8 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise torch.distributed even at world size 1 (rehearses the "
                          "RCCL gather path on one GPU)")
+    ap.add_argument("--split", default="subband", choices=["subband", "time"],
+                    help="time: one integration split across the ranks (strong scaling)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="use b2p_push + b2p_finish_async instead of b2p_integrate")
     return ap.parse_args()
@@ -110,13 +117,27 @@ def main():
     rccl = dist_on and a.dist_backend == "nccl"
     if dist_on:
         D.init(a.dist_backend, local)
-    subband = D.subband_of(rank)
+    split = a.split == "time"
+    subband = 0 if split else D.subband_of(rank)
+    spb = samples_per_block(geom)  # one sub-band's integration
+    elem0 = 0
+    if split:  # this rank's share of the integration's frames
+        first, nf = D.time_share(rank, world, geom.nsamp_int // geom.nsamp_df)
+        full_nsamp = geom.nsamp_int
+        geom = paf_b2p.make_geom(**{f: getattr(geom, f) for f, _ in geom._fields_ if f != "reserved"})
+        geom.nsamp_int = nf * geom.nsamp_df
+        elem0 = first * paf_b2p.geometry.frame_bytes(geom) // (geom.nbit // 8)
     # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
     it = paf_b2p.Integrator(geom, device=local)
     nout, bb = it.nout, it.block_bytes
-    spb = samples_per_block(geom)
 
-    if rccl:
+    if split:
+        # exact partial sums, K x nout uint64 (as int64 for torch), reduced
+        # to rank 0 after the loop; rank 0 then rounds them to fp32
+        sums_t = torch.zeros((max(a.steps, 1), nout), dtype=torch.int64, device="cuda")
+        spec_t = torch.zeros((max(a.steps, 1), nout), dtype=torch.float32, device="cuda")
+        out_ptr = sums_t.data_ptr()
+    elif rccl:
         # finalize writes the K spectra straight into torch device memory;
         # the gather runs after one it.sync() at the end of the timed loop
         out_t = torch.zeros((a.steps, nout), dtype=torch.float32, device="cuda")
@@ -131,7 +152,7 @@ def main():
         import numpy as np
         hb = np.empty(bb, dtype=np.uint8)
         d = it.alloc(bb)
-        it.fill_synthetic(d, SEED, subband, 0)
+        it.fill_synthetic(d, SEED, subband, 0, elem0=elem0)
         hb[:] = it.download(d)
         d.free()
         it.register_host(hb)
@@ -139,11 +160,15 @@ def main():
     else:
         for b in range(NBLOCKS):
             d = it.alloc(bb)
-            it.fill_synthetic(d, SEED, subband, b)
+            it.fill_synthetic(d, SEED, subband, b, elem0=elem0)
             blocks.append(d)
     it.sync()
 
     def step(k, out_row):
+        if split:  # this rank's share -> exact partial sums (row out_row)
+            it.push(blocks[k % len(blocks)])
+            it.finish_partial(out_ptr + (out_row or 0) * nout * 8, True)
+            return
         dst = out_ptr + (out_row or 0) * nout * 4
         if a.no_fuse or host_mode:  # the push / finish_async pair
             it.push(blocks[k % len(blocks)])
@@ -169,7 +194,21 @@ def main():
         step(a.warmup + k, k)
     it.set_timing(0)  # records the closing event right behind the last launch
     it.sync()
-    if rccl:
+    if split:
+        if dist_on:
+            torch.cuda.synchronize()
+            if rccl:
+                total = D.reduce_sums(sums_t)  # RCCL reduce (SUM) of K x nout partials
+            else:  # gloo rehearsal: partials through host memory
+                host_total = D.reduce_sums(sums_t.cpu())
+                total = host_total.cuda() if host_total is not None else None
+        else:
+            total = sums_t
+        if rank == 0:
+            it.finalize_sums(total.data_ptr(), a.steps, spec_t.data_ptr(), full_nsamp)
+            it.sync()
+        torch.cuda.synchronize()
+    elif rccl:
         gathered = D.gather_spectra(out_t)  # RCCL all-gather of K x nout fp32
         torch.cuda.synchronize()
     elif dist_on:
@@ -181,7 +220,7 @@ def main():
     st = it.stats()
 
     el_max = D.max_over_ranks(el, "cuda" if rccl else "cpu") if dist_on else el
-    if dist_on and rank == 0:
+    if dist_on and rank == 0 and not split:
         assert len(gathered) == world and all(g.shape == (a.steps, nout) for g in gathered)
 
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
@@ -190,7 +229,7 @@ def main():
     traffic, traffic_src = pmc_traffic(a.config)
 
     if rank == 0:
-        value = D.aggregate_rate(n_gpus, a.steps, spb, el_max)
+        value = D.aggregate_rate(1 if split else n_gpus, a.steps, spb, el_max)
         res = {
             "metric": "baseband Msamples/s integrated + % HBM-read roofline, 1024x1024 accum",
             "value": round(value, 1),
@@ -200,23 +239,27 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(el_max / max(a.steps, 1) * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if split else "weak",
             "vs_baseline": None,
             "dtype": f"int{geom.nbit}" + ("-be" if geom.big_endian else ""),
             "data": "synthetic (counter-based SplitMix64 Gaussian, seed 20181105, sub-band = rank)",
             "config": {
-                "workload": cfg["what"] + ("" if world == 1 else f"; {world} sub-bands, 1 per GPU"),
+                "workload": cfg["what"] + (
+                    f"; ONE integration split by time over {world} GPU(s), exact partials reduced"
+                    if split else ("" if world == 1 else f"; {world} sub-bands, 1 per GPU")),
                 "baseline_config": {"c2": "configs[1]", "c5": "configs[4]", "c3": "configs[2]",
                                     "bmf": "reference-native"}[a.config],
                 "nchan": int(geom.nchunk * geom.nchan_chunk),
                 "npol": int(geom.npol),
                 "nsamp_int": int(geom.nsamp_int),
-                "bytes_per_integration": int(bb),
+                "bytes_per_integration": int(bb * (world if split else 1)),
                 "input": "pinned host buffer, H2D overlapped (PCIe-inclusive)" if host_mode
                          else f"HBM-resident, {NBLOCKS} rotating blocks",
-                "parallelism": f"sub-band sharding x{n_gpus}" + (
+                "parallelism": (f"time split x{n_gpus}" + (
+                    (", RCCL reduce (SUM) of uint64 partials" if rccl else ", gloo reduce (rehearsal)")
+                    if dist_on else "")) if split else (f"sub-band sharding x{n_gpus}" + (
                     (", RCCL all-gather of spectra" if rccl else ", gloo gather (rehearsal)")
-                    if dist_on else ""),
+                    if dist_on else "")),
                 "launch": {"threads": it.info.threads, "columns": it.info.columns,
                            "row_groups": it.info.row_groups, "replicas": it.info.replicas,
                            "unroll": it.info.unroll, "nt_loads": bool(it.info.nontemporal)},

@@ -153,6 +153,17 @@ int b2p_finish(b2p_ctx_t *ctx, float *out);
 /* Same, enqueued: out is device memory (out_is_device = 1) or pinned host
  * memory; valid after b2p_sync(). */
 int b2p_finish_async(b2p_ctx_t *ctx, float *out, int out_is_device);
+/* As b2p_finish_async, but emits the integration's exact uint64 sums
+ * (nout values) instead of fp32: the partial of one member of a time-split
+ * integration (b2p_group_reduce), or for callers that reduce sums
+ * themselves.  Replaces the finalize of the reference's unwritten
+ * kernel.cu:1-7 for that mode. */
+int b2p_finish_partial_async(b2p_ctx_t *ctx, uint64_t *sums, int sums_is_device);
+/* fp32 from reduced exact sums: nspec x nout uint64 on this context's device
+ * -> out (device), one RNE rounding each; with mean set, divided by
+ * nsamp_total (0: this context's nsamp_int).  Stream-ordered. */
+int b2p_finalize_sums(b2p_ctx_t *ctx, const uint64_t *sums, uint64_t nspec, uint64_t nsamp_total,
+                      float *out);
 int b2p_sync(b2p_ctx_t *ctx);
 /* One whole integration in one call: push exactly block_bytes and emit it,
  * enqueued (out valid after b2p_sync()).  For a device span this is ONE
@@ -178,6 +189,13 @@ uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
 typedef struct b2p_group b2p_group_t;
 int b2p_group_open(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode);
 int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);
+/* Time-split mode (second mode): member r integrated its share
+ * of ONE sub-band's samples and emitted exact sums with
+ * b2p_finish_partial_async; sums[r] holds `count` uint64 on member r's
+ * device.  root_sum (member 0's device) receives their total: RCCL
+ * ncclReduce(ncclUint64, ncclSum) in mode 0, peer copies + a sum kernel in
+ * mode 1.  Exact, so bit-identical to a single-GPU integration. */
+int b2p_group_reduce(b2p_group_t *grp, uint64_t *const *sums, uint64_t count, uint64_t *root_sum);
 int b2p_group_sync(b2p_group_t *grp);
 const char *b2p_group_last_error(const b2p_group_t *grp); /* grp may be NULL */
 int b2p_group_close(b2p_group_t *grp);

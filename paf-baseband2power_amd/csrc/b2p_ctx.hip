@@ -60,7 +60,8 @@ struct b2p_ctx {
     int set;
     float *dev_out;              // where the kernel writes the spectrum
     float *host_out;             // non-null: D2H copy after it
-  } pend = {0, 0, nullptr, nullptr};
+    int raw;                     // 1: exact uint64 sums instead of fp32
+  } pend = {0, 0, nullptr, nullptr, 0};
   uint32_t interleave = 0;
   int fuse = 0;  // b2p_integrate: finalize in the last workgroup (1) or a
                  // separate launch (0, measured faster: DESIGN.md)
@@ -307,7 +308,8 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (hipMalloc(&c->d_rep, rep_bytes) != hipSuccess) return fail(set_err(c, B2P_ENOMEM, "hipMalloc replicas"));
   c->d_ticket = (uint32_t *)(c->d_rep + 2 * set_words);
 
-  if (hipMalloc(&c->d_out, (size_t)c->nout * sizeof(float)) != hipSuccess)
+  // sized for uint64 sums too (b2p_finish_partial_async to host)
+  if (hipMalloc(&c->d_out, (size_t)c->nout * sizeof(unsigned long long)) != hipSuccess)
     return fail(set_err(c, B2P_ENOMEM, "hipMalloc out"));
   if (hipMemsetAsync(c->d_rep, 0, rep_bytes, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
@@ -409,6 +411,10 @@ static hipEvent_t pool_event(b2p_ctx_t *c) {
 }
 
 // Enqueue one integrate launch over a device span (frame-aligned).  With
+static size_t pend_bytes(const b2p_ctx_t *c) {
+  return (size_t)c->nout * (c->pend.raw ? sizeof(unsigned long long) : sizeof(float));
+}
+
 // fused_out set, the launch also emits the integration (last workgroup).
 static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out) {
   IntegrateArgs a;
@@ -435,10 +441,12 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   // the previous integration's finalize rides on this launch (extra block)
   a.fin_rep = nullptr;
   a.fin_out = nullptr;
+  a.fin_raw = 0;
   const bool carry = c->pend.valid;
   if (carry) {
     a.fin_rep = c->d_rep + (size_t)c->pend.set * c->nrep * c->nout;
     a.fin_out = c->pend.dev_out;
+    a.fin_raw = (uint32_t)c->pend.raw;
     grid += 1;
   }
   EvPair p{nullptr, nullptr, nbytes, 0};
@@ -455,8 +463,8 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   if (c->timing == 1) c->pending.push_back(p);
   if (carry) {
     if (c->pend.host_out)
-      CK(c, hipMemcpyAsync(c->pend.host_out, c->pend.dev_out, (size_t)c->nout * sizeof(float),
-                           hipMemcpyDeviceToHost, c->stream));
+      CK(c, hipMemcpyAsync(c->pend.host_out, c->pend.dev_out, pend_bytes(c), hipMemcpyDeviceToHost,
+                           c->stream));
     c->pend.valid = 0;
   }
   return B2P_OK;
@@ -472,6 +480,7 @@ static int flush_pending(b2p_ctx_t *c) {
   f.out = c->pend.dev_out;
   f.mean = c->g.mean;
   f.nsamp = (double)c->g.nsamp_int;
+  f.raw = (uint32_t)c->pend.raw;
   EvPair p{nullptr, nullptr, 0, 1};
   if (c->timing == 2) {
     c->region_finalizes++;
@@ -484,8 +493,8 @@ static int flush_pending(b2p_ctx_t *c) {
   CK(c, launch_finalize(f, c->stream, p.a, p.b));
   if (c->timing == 1) c->pending.push_back(p);
   if (c->pend.host_out)
-    CK(c, hipMemcpyAsync(c->pend.host_out, c->pend.dev_out, (size_t)c->nout * sizeof(float),
-                         hipMemcpyDeviceToHost, c->stream));
+    CK(c, hipMemcpyAsync(c->pend.host_out, c->pend.dev_out, pend_bytes(c), hipMemcpyDeviceToHost,
+                         c->stream));
   c->pend.valid = 0;
   return B2P_OK;
 }
@@ -562,7 +571,7 @@ int b2p_internal_flush(b2p_ctx_t *c) {
 
 extern "C" {
 
-int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
+static int finish_common(b2p_ctx_t *c, void *out, int out_is_device, int raw) {
   if (!c || !out) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));
   int rc = flush_pending(c);  // two finishes in a row: the first runs alone
@@ -570,14 +579,39 @@ int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
   // defer: the next integrate launch (or b2p_sync) emits this integration
   c->pend.valid = 1;
   c->pend.set = c->cur;
-  c->pend.dev_out = out_is_device ? out : c->d_out;
-  c->pend.host_out = out_is_device ? nullptr : out;
+  c->pend.raw = raw;
+  c->pend.dev_out = out_is_device ? (float *)out : c->d_out;
+  c->pend.host_out = out_is_device ? nullptr : (float *)out;
   c->cur ^= 1;
   const uint64_t got = c->samples;
   c->samples = 0;
   if (got != c->g.nsamp_int)
     return set_err(c, B2P_EPARTIAL, "integration had %llu of %llu samples", (unsigned long long)got,
                    (unsigned long long)c->g.nsamp_int);
+  return B2P_OK;
+}
+
+int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
+  return finish_common(c, out, out_is_device, 0);
+}
+
+int b2p_finish_partial_async(b2p_ctx_t *c, uint64_t *sums, int sums_is_device) {
+  return finish_common(c, sums, sums_is_device, 1);
+}
+
+int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64_t nsamp_total,
+                      float *out) {
+  if (!c || !sums || !out) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  int rc = flush_pending(c);  // sums this context still owes come first
+  if (rc != B2P_OK) return rc;
+  ConvertArgs a;
+  a.sums = (const unsigned long long *)sums;
+  a.out = out;
+  a.n = nspec * c->nout;
+  a.mean = c->g.mean;
+  a.nsamp = (double)(nsamp_total ? nsamp_total : c->g.nsamp_int);
+  CK(c, launch_convert(a, c->stream));
   return B2P_OK;
 }
 

@@ -1,10 +1,13 @@
-// Multi-GPU gather of per-channel spectra (include/b2p.h "b2p_group").
+// Multi-GPU collectives of the integrator (include/b2p.h "b2p_group").
 //
 // sub-bands shard with no exchange during the integrate; the
-// only collective is the final gather of each sub-band's spectrum to the
-// root device -- RCCL over xGMI (ncclCommInitAll + ncclGather,
-// /opt/rocm/include/rccl/rccl.h:236,745), issued on each context's own
-// stream so it is ordered behind that context's finalize.  Mode 1 replaces
+// collective is the final gather of each sub-band's spectrum to the root
+// device -- RCCL over xGMI (ncclCommInitAll + ncclGather,
+// /opt/rocm/include/rccl/rccl.h:236,745).  The second mode splits ONE
+// sub-band's integration across members by time; their exact uint64 partial
+// sums meet in an ncclReduce(ncclUint64, ncclSum) at the root, so the result
+// is bit-identical to one GPU's.  Both are issued on each context's own
+// stream, ordered behind that context's finalize.  Mode 1 replaces
 // RCCL with peer copies for rigs where several contexts share one device
 // (RCCL refuses duplicate devices in a communicator).
 #include <hip/hip_runtime.h>
@@ -26,6 +29,8 @@ struct b2p_group {
   std::vector<hipStream_t> stream;
   std::vector<ncclComm_t> comm;
   std::vector<hipEvent_t> done;  // mode 1: member r's spectrum is final
+  unsigned long long *scratch = nullptr;  // mode 1 reduce: rows gathered on the root
+  uint64_t scratch_count = 0;
   uint32_t nout = 0;
   char err[256] = {0};
 };
@@ -119,6 +124,56 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
   return B2P_OK;
 }
 
+int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint64_t *root_sum) {
+  if (!g || !sums || !root_sum || !count) return B2P_EINVAL;
+  for (int r = 0; r < g->n; ++r) {
+    int rc = b2p_internal_flush(g->ctx[r]);
+    if (rc != B2P_OK) return gerr(g, rc, "flush", b2p_last_error(g->ctx[r]));
+  }
+  if (g->mode == 0) {  // exact: integer sums, any order
+    ncclResult_t nr = ncclGroupStart();
+    for (int r = 0; r < g->n && nr == ncclSuccess; ++r) {
+      (void)hipSetDevice(g->dev[r]);
+      nr = ncclReduce(sums[r], r == 0 ? root_sum : nullptr, count, ncclUint64, ncclSum, 0, g->comm[r],
+                      g->stream[r]);
+    }
+    ncclResult_t ne = ncclGroupEnd();
+    if (nr != ncclSuccess || ne != ncclSuccess)
+      return gerr(g, B2P_EHIP, "ncclReduce", ncclGetErrorString(nr != ncclSuccess ? nr : ne));
+    return B2P_OK;
+  }
+  // mode 1: rows copied to the root, summed there
+  (void)hipSetDevice(g->dev[0]);
+  if (g->scratch_count < count * (uint64_t)g->n) {
+    if (g->scratch) (void)hipFree(g->scratch);
+    g->scratch = nullptr;
+    g->scratch_count = 0;
+    if (hipMalloc(&g->scratch, count * (uint64_t)g->n * sizeof(unsigned long long)) != hipSuccess)
+      return gerr(g, B2P_ENOMEM, "b2p_group_reduce", "hipMalloc");
+    g->scratch_count = count * (uint64_t)g->n;
+  }
+  for (int r = 0; r < g->n; ++r) {
+    (void)hipSetDevice(g->dev[r]);
+    if (hipEventRecord(g->done[r], g->stream[r]) != hipSuccess)
+      return gerr(g, B2P_EHIP, "hipEventRecord", "");
+  }
+  (void)hipSetDevice(g->dev[0]);
+  const size_t bytes = count * sizeof(unsigned long long);
+  for (int r = 0; r < g->n; ++r) {
+    if (hipStreamWaitEvent(g->stream[0], g->done[r], 0) != hipSuccess ||
+        hipMemcpyPeerAsync(g->scratch + (size_t)r * count, g->dev[0], sums[r], g->dev[r], bytes,
+                           g->stream[0]) != hipSuccess)
+      return gerr(g, B2P_EHIP, "hipMemcpyPeerAsync", "");
+  }
+  b2p::SumRowsArgs a;
+  a.src = g->scratch;
+  a.dst = (unsigned long long *)root_sum;
+  a.count = count;
+  a.nrows = (uint32_t)g->n;
+  if (b2p::launch_sum_rows(a, g->stream[0]) != hipSuccess) return gerr(g, B2P_EHIP, "sum_rows", "");
+  return B2P_OK;
+}
+
 int b2p_group_sync(b2p_group_t *g) {
   if (!g) return B2P_EINVAL;
   for (int r = 0; r < g->n; ++r) {
@@ -134,6 +189,10 @@ int b2p_group_close(b2p_group_t *g) {
   if (!g) return B2P_EINVAL;
   for (auto c : g->comm)
     if (c) ncclCommDestroy(c);
+  if (g->scratch) {
+    (void)hipSetDevice(g->dev[0]);
+    (void)hipFree(g->scratch);
+  }
   for (size_t r = 0; r < g->done.size(); ++r)
     if (g->done[r]) {
       (void)hipSetDevice(g->dev[r]);

@@ -38,6 +38,7 @@ struct IntegrateArgs {
   // workgroup of this launch (grid = NC*G + 1) when fin_out is set
   unsigned long long *fin_rep;  // its replica set (re-zeroed)
   float *fin_out;
+  uint32_t fin_raw;             // 1: fin_out receives the exact uint64 sums
   uint32_t nwork;               // streaming workgroups (NC*G)
 };
 
@@ -48,6 +49,24 @@ struct FinalizeArgs {
   float *out;
   uint32_t mean;
   double nsamp;
+  uint32_t raw;                 // 1: out receives the exact uint64 sums
+};
+
+// fp32 from exact sums that were reduced elsewhere (b2p_finalize_sums)
+struct ConvertArgs {
+  const unsigned long long *sums;
+  float *out;
+  uint64_t n;
+  uint32_t mean;
+  double nsamp;
+};
+
+// dst[i] = sum over r < nrows of src[r*count + i] (b2p_group_reduce, mode 1)
+struct SumRowsArgs {
+  const unsigned long long *src;
+  unsigned long long *dst;
+  uint64_t count;
+  uint32_t nrows;
 };
 
 struct FillArgs {
@@ -77,6 +96,8 @@ struct AssembleArgs {
   unsigned long long *counts;   // nchunk placed, then before / after / bad chunk
 };
 hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s);
+hipError_t launch_convert(const ConvertArgs &a, hipStream_t s);
+hipError_t launch_sum_rows(const SumRowsArgs &a, hipStream_t s);
 
 // which instantiation of the integrate kernel runs
 struct KernelChoice {

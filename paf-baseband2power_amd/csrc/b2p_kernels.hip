@@ -163,7 +163,10 @@ b2p_integrate_kernel(IntegrateArgs a) {
       a.fin_rep[k] = 0;
     }
     __syncthreads();
-    for (uint32_t j = t; j < a.nout; j += blockDim.x) a.fin_out[j] = to_output(lds[j], a.mean, a.nsamp);
+    if (a.fin_raw)
+      for (uint32_t j = t; j < a.nout; j += blockDim.x) reinterpret_cast<unsigned long long *>(a.fin_out)[j] = lds[j];
+    else
+      for (uint32_t j = t; j < a.nout; j += blockDim.x) a.fin_out[j] = to_output(lds[j], a.mean, a.nsamp);
     return;
   }
   const uint32_t col = blockIdx.x % a.NC;
@@ -296,7 +299,25 @@ __global__ void __launch_bounds__(256) b2p_finalize_kernel(FinalizeArgs a) {
   __syncthreads();
   if (w == 0 && j < a.nout) {
     const unsigned long long tot = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-    a.out[j] = to_output(tot, a.mean, a.nsamp);
+    if (a.raw)
+      reinterpret_cast<unsigned long long *>(a.out)[j] = tot;
+    else
+      a.out[j] = to_output(tot, a.mean, a.nsamp);
+  }
+}
+
+__global__ void __launch_bounds__(256) b2p_convert_kernel(ConvertArgs a) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    a.out[i] = to_output(a.sums[i], a.mean, a.nsamp);
+}
+
+__global__ void __launch_bounds__(256) b2p_sum_rows_kernel(SumRowsArgs a) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long s = 0;
+    for (uint32_t r = 0; r < a.nrows; ++r) s += a.src[(uint64_t)r * a.count + i];
+    a.dst[i] = s;
   }
 }
 
@@ -493,6 +514,22 @@ hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s, hipEvent_t ev0,
   void *args[] = {&arg};
   return hipExtLaunchKernel(reinterpret_cast<const void *>(b2p_finalize_kernel), dim3(grid),
                             dim3(256), args, 0, s, ev0, ev1, 0);
+}
+
+hipError_t launch_convert(const ConvertArgs &a, hipStream_t s) {
+  uint64_t blocks = (a.n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(b2p_convert_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_rows(const SumRowsArgs &a, hipStream_t s) {
+  uint64_t blocks = (a.count + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(b2p_sum_rows_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_fill(uint4 *dst, uint64_t nvec, const FillArgs &f, hipStream_t s) {

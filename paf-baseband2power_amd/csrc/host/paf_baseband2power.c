@@ -42,6 +42,7 @@ typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
   int npol_out;
   int mean;
   int nsub;
+  int nsplit; /* > 1: one ring's integration split by time over nsplit GPUs */
 } conf_t;
 
 typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
@@ -53,6 +54,7 @@ typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
   b2p_geom_t g;
   double tsamp_us;
   float *spec_dev; /* this sub-band's spectrum (device) */
+  uint64_t *part_dev; /* time split: this member's exact partial sums (device) */
   uint64_t rbufsz;
   int locked;
   int ondev; /* input blocks are in GPU memory (dada_db -g) */
@@ -73,6 +75,8 @@ static void usage(void) {
           " -p  Output pols: 1 = |X|^2+|Y|^2 (default), 2 = X and Y\n"
           " -m  Write the time average instead of the sum\n"
           " -n  Number of sub-bands (rings key_in + 0x10*r, GPUs d + r), gathered to GPU d\n"
+          " -t  Split each integration of the one input ring by time over N GPUs (d + r);\n"
+          "     exact partial sums are reduced on GPU d (host ring: N PCIe links in parallel)\n"
           " -h  show help\n");
 }
 
@@ -170,6 +174,10 @@ typedef struct shared_t {
   int failed;
   uint64_t nblocks, nskipped;
   double t_first, t_last; /* first integration started, last output written */
+  /* time split (-t): the block every member takes its share of */
+  char *blk;
+  uint64_t blk_bytes, share_bytes, nsamp_full;
+  uint64_t *root_sum; /* on member 0's device */
 } shared_t;
 
 typedef struct worker_t {
@@ -258,16 +266,93 @@ static void *worker(void *arg) {
   return NULL;
 }
 
+/* -t N: member r integrates bytes [r*share, (r+1)*share) of every block of
+ * the one input ring; member 0 reduces the exact partial sums (RCCL
+ * ncclReduce, b2p_group_reduce) and rounds once (second mode) */
+static void *worker_split(void *arg) {
+  worker_t *w = (worker_t *)arg;
+  shared_t *sh = w->sh;
+  sub_t *s = &sh->sub[w->r];
+  sub_t *s0 = &sh->sub[0];
+  for (;;) {
+    if (w->r == 0) {
+      uint64_t bid = 0;
+      sh->blk_bytes = 0;
+      sh->blk = ipcio_open_block_read(s0->in->data_block, &sh->blk_bytes, &bid);
+      sh->have[0] = !sh->blk ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
+    }
+    pthread_barrier_wait(&sh->bar);
+    if (sh->have[0] <= 0 || sh->failed) {
+      if (w->r == 0 && sh->blk) {
+        ipcio_close_block_read(s0->in->data_block, sh->blk_bytes);
+        if (sh->have[0] == 0 && !sh->failed) {
+          sh->nskipped++;
+          multilog(sh->log, LOG_INFO, "partial integration skipped (block held %" PRIu64 " of %" PRIu64
+                   " B)", sh->blk_bytes, s0->rbufsz);
+        }
+      }
+      const int stop = sh->have[0] < 0 || sh->failed;
+      pthread_barrier_wait(&sh->bar);
+      if (stop) break;
+      continue;
+    }
+    const double t0 = now_s();
+    if (w->r == 0 && sh->t_first == 0) sh->t_first = t0;
+    int rc = b2p_push(s->ctx, sh->blk + (uint64_t)w->r * sh->share_bytes, sh->share_bytes, 0);
+    if (rc == B2P_OK) rc = b2p_finish_partial_async(s->ctx, s->part_dev, 1);
+    if (rc != B2P_OK) {
+      multilog(sh->log, LOG_ERR, "member %d: %s (%s)", w->r, b2p_strerror(rc), b2p_last_error(s->ctx));
+      sh->failed = 1;
+    }
+    pthread_barrier_wait(&sh->bar); /* every share has left the host block */
+    if (w->r == 0) {
+      ipcio_close_block_read(s0->in->data_block, sh->blk_bytes);
+      if (!sh->failed) {
+        uint64_t *parts[MAX_SUB];
+        for (int r = 0; r < sh->nsub; r++) parts[r] = sh->sub[r].part_dev;
+        rc = b2p_group_reduce(sh->grp, parts, sh->nout, sh->root_sum);
+        if (rc == B2P_OK)
+          rc = b2p_finalize_sums(s0->ctx, sh->root_sum, 1, sh->nsamp_full, s0->spec_dev);
+        if (rc == B2P_OK) rc = b2p_memcpy(s0->ctx, sh->spec_host, s0->spec_dev, sh->obytes, 2);
+        if (rc != B2P_OK) {
+          multilog(sh->log, LOG_ERR, "reduce: %s / %s", b2p_group_last_error(sh->grp),
+                   b2p_last_error(s0->ctx));
+          sh->failed = 1;
+        }
+      }
+      if (!sh->failed) {
+        uint64_t bid;
+        char *o = ipcio_open_block_write(sh->out->data_block, &bid);
+        if (!o) {
+          sh->failed = 1;
+        } else {
+          memcpy(o, sh->spec_host, sh->obytes);
+          ipcio_close_block_write(sh->out->data_block, sh->obytes);
+          sh->nblocks++;
+          sh->t_last = now_s();
+          const double dt = sh->t_last - t0;
+          multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s over %d GPUs",
+                   sh->nblocks, dt * 1e3, sh->blk_bytes / dt / 1e9, sh->nsub);
+        }
+      }
+    }
+    pthread_barrier_wait(&sh->bar);
+    if (sh->failed) break;
+  }
+  return NULL;
+}
+
 int main(int argc, char *argv[]) {
   int arg;
   conf_t conf;
   memset(&conf, 0, sizeof conf);
   conf.npol_out = 1;
   conf.nsub = 1;
+  conf.nsplit = 1;
   strcpy(conf.dir, ".");
   int have_in = 0, have_out = 0;
 
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:mh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:mh")) != -1) {
     switch (arg) {
       case 'h':
         usage();
@@ -291,11 +376,13 @@ int main(int argc, char *argv[]) {
       case 'f': snprintf(conf.layout, sizeof conf.layout, "%s", optarg); break;
       case 'p': conf.npol_out = atoi(optarg); break;
       case 'n': conf.nsub = atoi(optarg); break;
+      case 't': conf.nsplit = atoi(optarg); break;
       case 'm': conf.mean = 1; break;
       default: usage(); return EXIT_FAILURE;
     }
   }
-  if (!have_in || !have_out || conf.nsub < 1 || conf.nsub > MAX_SUB) {
+  if (!have_in || !have_out || conf.nsub < 1 || conf.nsub > MAX_SUB || conf.nsplit < 1 ||
+      conf.nsplit > MAX_SUB || (conf.nsub > 1 && conf.nsplit > 1)) {
     usage();
     return EXIT_FAILURE;
   }
@@ -335,12 +422,26 @@ int main(int argc, char *argv[]) {
   sh.out = out;
   int dup_dev = 0;
 
-  for (int r = 0; r < conf.nsub; r++) {
+  const int split = conf.nsplit > 1;
+  const int nmem = split ? conf.nsplit : conf.nsub;
+  sh.nsub = nmem;
+  for (int r = 0; r < nmem; r++) {
     sub_t *s = &sub[r];
     s->r = r;
     s->key = conf.key_in + 0x10 * r;
     s->device = ndev == 1 ? 0 : (conf.device_id + r) % ndev;
     if (r && s->device == sub[0].device) dup_dev = 1;
+    if (split && r > 0) { /* members share ring 0; each takes a time share */
+      s->g = sub[0].g;
+      s->rbufsz = sub[0].rbufsz;
+      s->tsamp_us = sub[0].tsamp_us;
+      int rc = b2p_open(&s->ctx, &s->g, s->device);
+      if (rc != B2P_OK) {
+        multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
+        goto done;
+      }
+      continue;
+    }
     s->in = dada_hdu_create(log);
     dada_hdu_set_key(s->in, s->key);
     if (dada_hdu_connect(s->in) < 0 || dada_hdu_lock_read(s->in) < 0) {
@@ -354,6 +455,17 @@ int main(int argc, char *argv[]) {
     }
     s->rbufsz = ipcbuf_get_bufsz(&s->in->data_block->buf);
     if (pick_geometry(&conf, s->in->header, s->rbufsz, &s->g, &s->tsamp_us, log) < 0) goto done;
+    if (split) { /* every member's context integrates one time share */
+      const uint64_t frames = s->g.nsamp_int / s->g.nsamp_df;
+      if (frames % (uint64_t)conf.nsplit) {
+        multilog(log, LOG_ERR, "%" PRIu64 " frames per block do not split into %d equal shares", frames,
+                 conf.nsplit);
+        goto done;
+      }
+      sh.nsamp_full = s->g.nsamp_int;
+      s->g.nsamp_int /= (uint64_t)conf.nsplit;
+      sh.share_bytes = s->rbufsz / (uint64_t)conf.nsplit;
+    }
     if (r && memcmp(&s->g, &sub[0].g, sizeof s->g)) {
       multilog(log, LOG_ERR, "sub-band %d layout differs from sub-band 0", r);
       goto done;
@@ -365,6 +477,11 @@ int main(int argc, char *argv[]) {
     }
     const int ring_dev = ipcbuf_get_device(&s->in->data_block->buf);
     s->ondev = ring_dev >= 0;
+    if (s->ondev && split) {
+      multilog(log, LOG_ERR, "-t splits host rings (one PCIe link per GPU); ring %x is on a GPU",
+               (unsigned)s->key);
+      goto done;
+    }
     if (s->ondev) {
       b2p_info_t ci;
       b2p_get_info(s->ctx, &ci);
@@ -385,6 +502,10 @@ int main(int argc, char *argv[]) {
   b2p_get_info(sub[0].ctx, &info);
   sh.nout = info.nout;
   sh.obytes = (uint64_t)conf.nsub * info.nout * sizeof(float);
+  if (split)
+    multilog(log, LOG_INFO, "time split: each integration of ring %x over %d GPUs, %" PRIu64
+             " B per share, exact partials reduced on GPU %d", (unsigned)conf.key_in, conf.nsplit,
+             sh.share_bytes, sub[0].device);
   multilog(log, LOG_INFO,
            "%d sub-band(s): nbit %u %s, %u chunks x %u chans x %u samp/DF, %u outputs each, "
            "%" PRIu64 " samples per integration, first GPU %d",
@@ -411,20 +532,22 @@ int main(int argc, char *argv[]) {
     memset(ohdr, 0, ohsz);
     memcpy(ohdr, sub[0].in->header, sub[0].in->header_size < ohsz ? sub[0].in->header_size : ohsz);
     ohdr[ohsz - 1] = 0;
-    const double tsamp_out = sub[0].tsamp_us * (double)sub[0].g.nsamp_int;
+    const uint64_t nsamp_out = split ? sh.nsamp_full : sub[0].g.nsamp_int;
+    const double tsamp_out = sub[0].tsamp_us * (double)nsamp_out;
     double tmpl = 0;
     if (ascii_header_get(ohdr, "TSAMP", "%lf", &tmpl) == 1 && tmpl != tsamp_out)
       multilog(log, LOG_INFO, "TSAMP %.6g us in the input header replaced by %.6f us "
-               "(= %.6f us x %" PRIu64 ")", tmpl, tsamp_out, sub[0].tsamp_us, sub[0].g.nsamp_int);
+               "(= %.6f us x %" PRIu64 ")", tmpl, tsamp_out, sub[0].tsamp_us, nsamp_out);
     ascii_header_set(ohdr, "NBIT", "%d", 32);
     ascii_header_set(ohdr, "NDIM", "%d", 1);
     ascii_header_set(ohdr, "NPOL", "%u", sub[0].g.npol_out);
     ascii_header_set(ohdr, "NCHAN", "%u", conf.nsub * info.nchan);
     ascii_header_set(ohdr, "TSAMP", "%.6f", tsamp_out);
     ascii_header_set(ohdr, "BYTES_PER_SECOND", "%.6f", sh.obytes / (tsamp_out * 1e-6));
-    ascii_header_set(ohdr, "NSAMP_INT", "%" PRIu64, sub[0].g.nsamp_int);
+    ascii_header_set(ohdr, "NSAMP_INT", "%" PRIu64, nsamp_out);
     ascii_header_set(ohdr, "POWER_MODE", "%s", sub[0].g.mean ? "MEAN" : "SUM");
     if (conf.nsub > 1) ascii_header_set(ohdr, "NSUBBAND", "%d", conf.nsub);
+    if (split) ascii_header_set(ohdr, "NSPLIT", "%d", conf.nsplit);
     ascii_header_del(ohdr, "NCHUNK");
     ascii_header_del(ohdr, "NCHAN_CHUNK");
     ascii_header_del(ohdr, "NSAMP_DF");
@@ -438,7 +561,25 @@ int main(int argc, char *argv[]) {
     if (!sh.spec_host) goto done;
     b2p_register_host(sub[0].ctx, sh.spec_host, hb);
   }
-  if (conf.nsub > 1) {
+  if (split) {
+    for (int r = 0; r < nmem; r++)
+      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].part_dev, info.nout * sizeof(uint64_t)) != B2P_OK)
+        goto done;
+    if (b2p_dev_alloc(sub[0].ctx, (void **)&sub[0].spec_dev, info.nout * sizeof(float)) != B2P_OK ||
+        b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_sum, info.nout * sizeof(uint64_t)) != B2P_OK)
+      goto done;
+    b2p_ctx_t *ctxs[MAX_SUB];
+    for (int r = 0; r < nmem; r++) ctxs[r] = sub[r].ctx;
+    const char *gm = getenv("B2P_GATHER");
+    int mode = dup_dev || (gm && !strcmp(gm, "copy")) ? 1 : 0;
+    int rc = b2p_group_open(&sh.grp, ctxs, nmem, mode);
+    if (rc != B2P_OK) {
+      multilog(log, LOG_ERR, "b2p_group_open: %s", b2p_group_last_error(NULL));
+      goto done;
+    }
+    multilog(log, LOG_INFO, "reduce of %d time shares to GPU %d via %s", nmem, sub[0].device,
+             mode ? "peer copies (shared device)" : "RCCL ncclReduce");
+  } else if (conf.nsub > 1) {
     for (int r = 0; r < conf.nsub; r++)
       if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, info.nout * sizeof(float)) != B2P_OK)
         goto done;
@@ -458,15 +599,15 @@ int main(int argc, char *argv[]) {
   }
 
   {
-    pthread_barrier_init(&sh.bar, NULL, (unsigned)conf.nsub);
+    pthread_barrier_init(&sh.bar, NULL, (unsigned)nmem);
     pthread_t th[MAX_SUB];
     worker_t wk[MAX_SUB];
-    for (int r = 0; r < conf.nsub; r++) {
+    for (int r = 0; r < nmem; r++) {
       wk[r].sh = &sh;
       wk[r].r = r;
-      pthread_create(&th[r], NULL, worker, &wk[r]);
+      pthread_create(&th[r], NULL, split ? worker_split : worker, &wk[r]);
     }
-    for (int r = 0; r < conf.nsub; r++) pthread_join(th[r], NULL);
+    for (int r = 0; r < nmem; r++) pthread_join(th[r], NULL);
     pthread_barrier_destroy(&sh.bar);
   }
   status = sh.failed ? EXIT_FAILURE : EXIT_SUCCESS;
@@ -474,9 +615,11 @@ int main(int argc, char *argv[]) {
 done:
   if (out_locked) dada_hdu_unlock_write(out); /* ends the output transfer (EOD) */
   if (sh.grp) b2p_group_close(sh.grp);
-  for (int r = 0; r < conf.nsub; r++) {
+  for (int r = 0; r < sh.nsub; r++) {
     sub_t *s = &sub[r];
     if (s->ctx) {
+      if (s->part_dev) b2p_dev_free(s->ctx, s->part_dev);
+      if (r == 0 && sh.root_sum) b2p_dev_free(s->ctx, sh.root_sum);
       for (uint64_t i = 0; !s->ondev && s->in && s->in->data_block &&
                            i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
         b2p_unregister_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i));

@@ -1,10 +1,18 @@
-"""Multi-GPU plumbing: one process per GPU, one sub-band per process.
+"""Multi-GPU plumbing: one process per GPU.
 
-SURVEY.md 8e: independent DADA sub-bands shard with no exchange during the
-integrate; the only collective is the final gather of the per-channel
-power spectra to rank 0 (RCCL over xGMI with the "nccl" backend on ROCm;
-gloo in the CPU tests).  Spectra are a few KiB, so the gather is
-latency-bound; it is issued once per batch of integrations, not per block.
+SURVEY.md 8e, two modes:
+
+* sub-band sharding (default): independent DADA sub-bands, one per rank,
+  with no exchange during the integrate; the only collective is the final
+  gather of the per-channel power spectra to rank 0.
+* time split: ONE sub-band's integration is cut along time into one share
+  per rank; each rank emits exact uint64 partial sums and rank 0 receives
+  their total through a reduce (SUM), then rounds once to fp32, so the
+  result is bit-identical to one GPU's.
+
+RCCL over xGMI with the "nccl" backend on ROCm; gloo in the CPU tests.
+Spectra and partials are a few KiB, so the collectives are latency-bound;
+each is issued once per batch of integrations, not per block.
 """
 from __future__ import annotations
 
@@ -42,6 +50,26 @@ def gather_spectra(local: torch.Tensor) -> list[torch.Tensor] | None:
     bufs = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(bufs, local.contiguous())
     return bufs if dist.get_rank() == 0 else None
+
+
+def time_share(rank: int, world: int, nframes: int) -> tuple[int, int]:
+    """(first frame, frames) of rank's share of an nframes integration: the
+    time axis is cut into world equal contiguous shares."""
+    if world < 1 or nframes % world:
+        raise ValueError(f"{nframes} frames do not split into {world} equal shares")
+    n = nframes // world
+    return rank * n, n
+
+
+def reduce_sums(local: torch.Tensor) -> torch.Tensor | None:
+    """Sum of every rank's [K, nout] exact partial sums on rank 0 (None
+    elsewhere).  The sums are uint64 bit patterns held as int64: totals stay
+    below 2**53, so the signed add is the exact one."""
+    if local.dtype != torch.int64:
+        raise TypeError("partial sums travel as int64")
+    t = local.contiguous().clone()
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+    return t if dist.get_rank() == 0 else None
 
 
 def max_over_ranks(x: float, device: str = "cpu") -> float:

@@ -77,6 +77,26 @@ class Integrator:
         L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,) if allow_partial else ())
         return out
 
+    def finish_partial(self, out_ptr: int | None = None, out_is_device: bool = False,
+                       allow_partial: bool = False):
+        """b2p_finish_partial_async: the integration's exact uint64 sums (a
+        member's share of a time-split integration).  With out_ptr None the
+        sums are returned (blocking)."""
+        if out_ptr is None:
+            out = np.zeros(self.nout, dtype=np.uint64)
+            rc = L.lib().b2p_finish_partial_async(self._ctx, out.ctypes.data_as(C.c_void_p), 0)
+            L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,) if allow_partial else ())
+            self.sync()
+            return out
+        rc = L.lib().b2p_finish_partial_async(self._ctx, C.c_void_p(out_ptr), int(out_is_device))
+        return L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,) if allow_partial else ())
+
+    def finalize_sums(self, sums_ptr: int, nspec: int, out_ptr: int, nsamp_total: int = 0) -> None:
+        """b2p_finalize_sums: fp32 (one RNE rounding) from nspec x nout exact
+        sums in device memory, stream-ordered."""
+        L.check(L.lib().b2p_finalize_sums(self._ctx, C.c_void_p(sums_ptr), nspec, nsamp_total,
+                                          C.c_void_p(out_ptr)), self._ctx)
+
     def finish_async(self, out_ptr: int, out_is_device: bool) -> int:
         rc = L.lib().b2p_finish_async(self._ctx, C.c_void_p(out_ptr), int(out_is_device))
         return L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,))
@@ -204,6 +224,15 @@ class Group:
     def gather(self, spectra_ptrs: list[int], root_out_ptr: int) -> None:
         arr = (C.c_void_p * len(spectra_ptrs))(*spectra_ptrs)
         rc = L.lib().b2p_group_gather(self._g, arr, C.c_void_p(root_out_ptr))
+        if rc != L.B2P_OK:
+            raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
+        L.check(L.lib().b2p_group_sync(self._g))
+
+    def reduce(self, sums_ptrs: list[int], count: int, root_sum_ptr: int) -> None:
+        """b2p_group_reduce: exact uint64 sum of every member's partial sums
+        (time-split mode) into root_sum on the first member's device."""
+        arr = (C.c_void_p * len(sums_ptrs))(*sums_ptrs)
+        rc = L.lib().b2p_group_reduce(self._g, arr, count, C.c_void_p(root_sum_ptr))
         if rc != L.B2P_OK:
             raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
         L.check(L.lib().b2p_group_sync(self._g))

@@ -56,13 +56,15 @@ def _bin(name: str) -> str:
 def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
-        device_ring: bool = False) -> list:
+        device_ring: bool = False, split: int = 1) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
     sub-bands and gathers their spectra to its first GPU).
     device_ring=True puts each input ring's blocks on its chain's GPU
     (dada_db -g): paf_diskdb copies into HBM and
-    paf_baseband2power integrates the block in place."""
+    paf_baseband2power integrates the block in place.  split=N cuts every
+    integration of a (single) chain by time over N GPUs (paf_baseband2power
+    -t N, SURVEY.md 8e second mode)."""
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
                              timeout, hfname)
@@ -100,6 +102,8 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
                 b2p_cmd += ["-f", layout]
             if mean:
                 b2p_cmd.append("-m")
+            if split > 1:
+                b2p_cmd += ["-t", str(split)]
             procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
                                           stderr=subprocess.PIPE))
             procs.append(subprocess.Popen(b2p_cmd, stderr=subprocess.PIPE))
@@ -213,12 +217,14 @@ def main(argv=None) -> int:
     ap.add_argument("-m", "--mean", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="one process for all sub-bands, spectra gathered to the first GPU")
+    ap.add_argument("-t", "--split", type=int, default=1,
+                    help="split each integration by time over N GPUs (exact partials reduced)")
     ap.add_argument("--device-ring", action="store_true",
                     help="input ring blocks in GPU memory (dada_db -g): no H2D in the integrator")
     a = ap.parse_args(argv)
     files = a.dfname if a.subbands > 1 or a.gather else a.dfname[0]
     outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean,
-               gather=a.gather, device_ring=a.device_ring)
+               gather=a.gather, device_ring=a.device_ring, split=a.split)
     print("\n".join(outs))
     return 0
 

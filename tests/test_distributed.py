@@ -79,3 +79,65 @@ def test_aggregate_rate_formula():
     from paf_b2p import distributed as D
     # 8 ranks x 10 steps x 2^29 samples in 1 s
     assert D.aggregate_rate(8, 10, 1 << 29, 1.0) == 8 * 10 * (1 << 29) / 1e6
+
+
+def _split_worker(rank, world, port, q):
+    # SURVEY.md 8e second mode: one integration cut along time, exact
+    # partial sums reduced to rank 0, rounded once there
+    for p in (PKG, ORACLE):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    import b2p_oracle as npo
+    from paf_b2p import distributed as D
+
+    r, w, _ = D.env_ranks()
+    D.init("gloo", r)
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=128 * 8)
+    first, nf = D.time_share(r, w, g.nsamp_int // g.nsamp_df)
+    parts = []
+    for k in range(2):
+        full = npo.fill_synthetic(g, g.block_bytes, 20181105, 0, k)
+        mine = full[first * g.frame_bytes:(first + nf) * g.frame_bytes]
+        parts.append(npo.integrate(g, mine).view(np.int64))
+    # large values near the exactness limit travel unchanged too
+    parts.append(np.full(g.nout, (1 << 52) // w + r, dtype=np.int64))
+    tot = D.reduce_sums(torch.from_numpy(np.stack(parts)))
+    q.put((r, None if tot is None else tot.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_time_split_reduce_is_exact():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    sys.path.insert(0, ORACLE)
+    import b2p_oracle as npo
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=128 * 8)
+    assert res[1] is None
+    tot = res[0].view(np.uint64)
+    for k in range(2):
+        full = npo.fill_synthetic(g, g.block_bytes, 20181105, 0, k)
+        assert np.array_equal(tot[k], npo.integrate(g, full))
+        assert np.array_equal(npo.finalize(g, tot[k]), npo.power(g, full))
+    assert np.all(tot[2] == (1 << 52) // world * world + sum(range(world)))
+
+
+def test_time_share_rules():
+    sys.path.insert(0, PKG)
+    from paf_b2p import distributed as D
+    assert [D.time_share(r, 4, 8192) for r in range(4)] == [(0, 2048), (2048, 2048),
+                                                             (4096, 2048), (6144, 2048)]
+    with pytest.raises(ValueError):
+        D.time_share(0, 3, 8192)

@@ -74,3 +74,88 @@ def test_multi_subband_c_host_gathered(gpu, tmp_path):
             assert np.array_equal(sp[i, r].view(np.uint32), co.power(g, blk).view(np.uint32))
     log = open(str(tmp_path / "out" / "paf_baseband2power.log")).read()
     assert "gather of 3 sub-bands" in log
+
+
+# ---- time-split mode (second mode) -----------------------------
+
+@pytest.mark.parametrize("npol_out,mean", [(1, 0), (2, 1)])
+def test_partial_sums_and_finalize(gpu, npol_out, mean):
+    # exact sums out of one context, fp32 from them = the normal finish
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * 32, npol_out=npol_out, mean=mean)
+    block = co.fill_synthetic(g, g.block_bytes, SEED, 0, 3)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        d = it.upload(block)
+        it.push(d)
+        sums = it.finish_partial()                      # host, blocking
+        assert np.array_equal(sums, co.integrate(g, block))
+        ds, out = it.alloc(g.nout * 8 * 2), it.alloc(g.nout * 4 * 2)
+        for k in range(2):                              # async, device rows
+            it.push(d)
+            it.finish_partial(ds.ptr + k * g.nout * 8, True)
+        it.finalize_sums(ds.ptr, 2, out.ptr)
+        it.sync()
+        got = it.download(out).view(np.float32).reshape(2, g.nout)
+        for b in (d, ds, out):
+            b.free()
+    want = co.power(g, block)
+    assert all(np.array_equal(got[k].view(np.uint32), want.view(np.uint32)) for k in range(2))
+
+
+@pytest.mark.parametrize("n,mode", [(1, 0), (4, 1)])
+def test_group_time_split_equals_one_gpu(gpu, n, mode):
+    # one BMF integration cut into n time shares, one member each; the
+    # reduced exact sums round to the single-GPU spectrum bit for bit
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * 64, mean=1)
+    block = co.fill_synthetic(g, g.block_bytes, SEED, 5, 2)
+    share = npo.Geom(**{**g.asdict(), "nsamp_int": g.nsamp_int // n})
+    its = [paf_b2p.Integrator(paf_b2p.make_geom(**share.asdict())) for _ in range(n)]
+    bufs, sums = [], []
+    for r, it in enumerate(its):
+        d = it.upload(block[r * share.block_bytes:(r + 1) * share.block_bytes])
+        s = it.alloc(g.nout * 8)
+        it.push(d)
+        it.finish_partial(s.ptr, True)                  # deferred: reduce flushes it
+        bufs.append(d)
+        sums.append(s)
+    root_sum, root_out = its[0].alloc(g.nout * 8), its[0].alloc(g.nout * 4)
+    with paf_b2p.Group(its, mode=mode) as grp:
+        grp.reduce([s.ptr for s in sums], g.nout, root_sum.ptr)
+    its[0].finalize_sums(root_sum.ptr, 1, root_out.ptr, g.nsamp_int)
+    its[0].sync()
+    tot = its[0].download(root_sum).view(np.uint64)
+    got = its[0].download(root_out).view(np.float32)
+    assert np.array_equal(tot, co.integrate(g, block))
+    assert np.array_equal(got.view(np.uint32), co.power(g, block).view(np.uint32))
+    for b in bufs + sums + [root_sum, root_out]:
+        b.free()
+    for it in its:
+        it.close()
+
+
+@pytest.mark.parametrize("split,mean", [(3, 0), (2, 1)])
+def test_c_host_time_split(gpu, tmp_path, split, mean):
+    # paf_baseband2power -t N: one host ring, each integration cut by time over
+    # N contexts (all on the one test GPU: peer-copy reduce), same spectra
+    from test_gpu_pipeline import spectra, write_conf
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * 48, mean=mean)
+    nblk = 2
+    payload = co.fill_synthetic(g, g.block_bytes * nblk + g.block_bytes // 3, SEED, 0, 21)
+    src = tmp_path / "bmf.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 48, 48, 7168, 336, 0x7c30 + 0x40 * split, 0x7d30 + 0x40 * split,
+               "header_baseband2power.txt")
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, str(src), layout="bmf", mean=bool(mean),
+                        split=split, timeout=600)
+    hdr, sp = spectra(outs[0], g.nout)
+    assert sp.shape == (nblk, g.nout)
+    for i in range(nblk):
+        blk = payload[i * g.block_bytes:(i + 1) * g.block_bytes]
+        assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk, nthreads=8).view(np.uint32))
+    assert dada.header_get(hdr, "NSPLIT", "%d") == split
+    assert dada.header_get(hdr, "NSAMP_INT", "%d") == g.nsamp_int
+    log = open(str(tmp_path / "out" / "paf_baseband2power.log")).read()
+    assert f"reduce of {split} time shares" in log and "partial integration skipped" in log

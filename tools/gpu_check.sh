@@ -39,6 +39,12 @@ for s in $STEPS; do
     benchdist1) run bench_dist1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist ;;
+    benchsplit) run bench_split1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+            --master-addr 127.0.0.1 --master-port 29513 bench.py --steps 20 --warmup 2 \
+            --cpu-seconds 0 --force-dist --split time &&
+          run bench_split2gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --steps 10 --warmup 2 \
+            --dist-backend gloo --split time ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
     asm) run bench_assemble 600 python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
     profasm) run prof_asm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_asm" -o run \
