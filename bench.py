@@ -81,9 +81,27 @@ def pmc_traffic(config: str):
         return None, None
 
 
+def _host_cpu() -> dict:
+    """model / logical CPUs / NUMA nodes of the box (SURVEY.md 8d asks for them)"""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        numa = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node")])
+    except OSError:
+        numa = None
+    return {"model": model, "logical_cpus": os.cpu_count(), "numa_nodes": numa}
+
+
 def cpu_baseline(geom, seconds: float, threads: int):
     """The oracle's C restatement (oracle/b2p_oracle.c), OpenMP over host
-    threads, on a bounded sample of the same workload held in host RAM."""
+    threads, on a bounded sample of the same workload held in host RAM;
+    a quarter of the budget times it on one thread as well."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import b2p_oracle as npo  # noqa: E402
     import oracle_c as co  # noqa: E402
@@ -92,19 +110,26 @@ def cpu_baseline(geom, seconds: float, threads: int):
     buf = co.fill_synthetic(g, sample_bytes, SEED, 0, 0)
     if threads <= 0:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    co.integrate(g, buf[: g.frame_bytes * 64], nthreads=threads)  # warm
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        co.integrate(g, buf, nthreads=threads)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or passes >= 100000:
-            break
-    samples = passes * sample_bytes // g.word_bytes * g.npol
-    return {"value": round(samples / el / 1e6, 2), "unit": "Msamples/s", "cores": threads,
+
+    def timed(nthreads, budget):
+        co.integrate(g, buf[: g.frame_bytes * 64], nthreads=nthreads)  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            co.integrate(g, buf, nthreads=nthreads)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget or passes >= 100000:
+                return passes, el
+
+    passes, el = timed(threads, seconds * 0.75)
+    p1, e1 = timed(1, seconds * 0.25)
+    per_pass = sample_bytes // g.word_bytes * g.npol
+    return {"value": round(passes * per_pass / el / 1e6, 2), "unit": "Msamples/s", "cores": threads,
             "kind": "port",
             "sample": f"{passes} passes over {sample_bytes >> 20} MiB of the same synthetic "
-                      f"{g.nchan}-chan int{g.nbit} block ({el:.1f} s, host RAM, no file I/O)"}
+                      f"{g.nchan}-chan int{g.nbit} block ({el:.1f} s, host RAM, no file I/O)",
+            "value_1thread": round(p1 * per_pass / e1 / 1e6, 2),
+            "host": _host_cpu()}
 
 
 def main():
