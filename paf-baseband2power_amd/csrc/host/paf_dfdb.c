@@ -128,6 +128,7 @@ int main(int argc, char **argv) {
   unsigned char *hf = NULL, *hc = NULL;
   batch_t bt[3] = {{0}};
   unsigned long long *d_cnt = NULL;
+  void *stage = NULL; /* replay into a host ring: blocks generated on the GPU, copied down */
   int locked = 0;
   if (dada_hdu_connect(hdu) < 0 || dada_hdu_lock_write(hdu) < 0) {
     multilog(log, LOG_ERR, "cannot attach/lock ring %x for writing", (unsigned)key);
@@ -175,7 +176,6 @@ int main(int argc, char **argv) {
   const double t0 = now_s();
   uint64_t nblk = 0;
   if (replay) {
-    void *stage = NULL; /* a host ring's blocks are generated on the GPU, then copied down */
     if (!ondev && b2p_dev_alloc(ctx, &stage, bufsz) != B2P_OK) goto done;
     for (uint64_t i = 0; i < replay; i++) {
       uint64_t bid;
@@ -191,7 +191,6 @@ int main(int argc, char **argv) {
       ipcio_close_block_write(hdu->data_block, bufsz);
       nblk++;
     }
-    if (stage) b2p_dev_free(ctx, stage);
   } else {
     const uint64_t block_ndf = bufsz / ((uint64_t)nchunk * B2P_DF_PAYLOAD_BYTES);
     const uint64_t cap = block_ndf * (uint64_t)nchunk; /* frames per batch */
@@ -264,6 +263,7 @@ done:
       if (bt[k].chunks) b2p_dev_free(ctx, bt[k].chunks);
     }
     if (d_cnt) b2p_dev_free(ctx, d_cnt);
+    if (stage) b2p_dev_free(ctx, stage);
     if (hf) b2p_unregister_host(ctx, hf);
     b2p_close(ctx);
   }

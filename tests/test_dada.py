@@ -302,3 +302,16 @@ def test_host_ring_reports_no_device(ring):
     key = ring(2, 4096)
     with dada.Hdu(key, "W") as w:
         assert w.device == -1
+
+
+def test_dfdb_refuses_host_ring_for_assembly(tmp_path, ring):
+    # frame assembly writes device memory: paf_dfdb needs a dada_db -g ring
+    key = ring(2, 48 * 7168)
+    (tmp_path / "s.df").write_bytes(b"")
+    (tmp_path / "s.chunks").write_bytes(b"")
+    hdr = tmp_path / "h.txt"
+    hdr.write_text("HDR_SIZE 4096\n")
+    r = subprocess.run([os.path.join(BIN, "paf_dfdb"), "-a", f"{key:x}", "-b", str(hdr), "-c",
+                        str(tmp_path / "s.df"), "-k", str(tmp_path / "s.chunks")],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "not GPU-resident" in r.stderr
