@@ -185,6 +185,23 @@ def test_full_bmf_block_vs_c_oracle(gpu):
     assert same_bits(out, co.power(g, host, nthreads=16))
 
 
+def test_full_1024ch_int16_8gib_vs_c_oracle(gpu):
+    # configs 3/5 at int16 = 8 GiB per integration (more than
+    # 2^32 bytes and 2^29 16-B vectors in one launch), X and Y kept apart
+    g = npo.Geom(nbit=16, nchan_chunk=1024, npol_out=2)
+    assert g.block_bytes == 8 << 30
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        d = it.alloc(g.block_bytes)
+        it.fill_synthetic(d, SEED, 6, 0)
+        it.push(d)
+        out = it.finish()
+        host = it.download(d)
+        d.free()
+    assert out.shape == (2048,)
+    assert same_bits(out, co.power(g, host, nthreads=16))
+    del host
+
+
 def test_full_1024ch_properties(gpu):
     # configs 3/5 layout at full size: push order / chunking invariance and
     # run-to-run determinism (exact integer sums), plus two back-to-back
