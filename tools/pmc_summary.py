@@ -22,13 +22,15 @@ import statistics
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "b2p_integrate_kernel"
 # bytes one integrate launch must read (bench.py configs, one integration)
-ALGORITHMIC = {"c2": 1 << 30, "c5": 1 << 32, "bmf": 2818572288}
+ALGORITHMIC = {"c2": 1 << 30, "c5": 1 << 32, "bmf": 2818572288,
+               # b2p_assemble of a full BMF block: 393216 x (7232 read + 7168 written)
+               "assemble": 393216 * (7232 + 7168)}
 
 
-def counter(path, name):
+def counter(path, name, kernel=KERNEL):
     vals = []
     for row in csv.DictReader(open(path)):
-        if KERNEL in row["Kernel_Name"] and row["Counter_Name"] == name:
+        if kernel in row["Kernel_Name"] and row["Counter_Name"] == name:
             vals.append(float(row["Counter_Value"]))
     return vals
 
@@ -41,16 +43,17 @@ def main():
     ap.add_argument("--stats")
     ap.add_argument("--round", default="r01")
     ap.add_argument("--algorithmic-bytes", type=int, default=0)
+    ap.add_argument("--kernel", default=KERNEL)
     a = ap.parse_args()
-    f = counter(a.fetch, "FETCH_SIZE")
-    w = counter(a.write, "WRITE_SIZE")
+    f = counter(a.fetch, "FETCH_SIZE", a.kernel)
+    w = counter(a.write, "WRITE_SIZE", a.kernel)
     fetch_kib, write_kib = statistics.median(f), statistics.median(w)
     hbm = int(fetch_kib * 1024 * 2 + write_kib * 1024)
     alg = a.algorithmic_bytes or ALGORITHMIC.get(a.config, 0)
     fetch_dst = f"profiles/{a.round}_{a.config}_pmc_fetch.csv"
     write_dst = f"profiles/{a.round}_{a.config}_pmc_write.csv"
     out = {
-        "kernel": KERNEL,
+        "kernel": a.kernel,
         "config": a.config,
         "launches_measured": len(f),
         "fetch_size_kib_median": fetch_kib,
