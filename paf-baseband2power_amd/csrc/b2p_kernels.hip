@@ -394,7 +394,7 @@ __device__ __forceinline__ uint32_t asm_slot(const AssembleArgs &a, uint64_t d, 
   return chunk;
 }
 
-template <bool NTL, bool NTS, int K>
+template <bool NTL, bool NTS, int K, bool EAGER>
 __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
   __shared__ unsigned long long cnt[256 + 3];
   const uint32_t ncnt = a.nchunk + 3;
@@ -410,9 +410,16 @@ __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint64_t d = d0 + j;
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(a.dfs + d * (uint64_t)a.df_bytes + a.hdr_bytes);
+      if (EAGER && d < a.ndf) {
+        // the payload loads do not wait for the header: every frame in the
+        // buffer is read, the header only decides where (or whether) it lands
+#pragma unroll
+        for (int k = 0; k < 7; ++k)
+          v[j][k] = NTL ? __builtin_nontemporal_load(src + k * 64 + lane) : src[k * 64 + lane];
+      }
       slot[j] = d < a.ndf ? asm_slot(a, d, rel[j]) : 0xffffffffu;
-      if (slot[j] < a.nchunk) {  // wave-uniform
-        const u32x4 *src = reinterpret_cast<const u32x4 *>(a.dfs + d * (uint64_t)a.df_bytes + a.hdr_bytes);
+      if (!EAGER && slot[j] < a.nchunk) {  // wave-uniform
 #pragma unroll
         for (int k = 0; k < 7; ++k)
           v[j][k] = NTL ? __builtin_nontemporal_load(src + k * 64 + lane) : src[k * 64 + lane];
@@ -437,13 +444,15 @@ __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
     if (cnt[j]) atomicAdd(&a.counts[j], cnt[j]);
 }
 
-// B2P_ASM_VARIANT: 0 nt load+store K=1 (default), 1 nt K=2, 2 plain K=1,
-// 3 nt load / plain store K=1, 4 nt K=4; B2P_ASM_GRID: workgroups (4 waves)
+// B2P_ASM_VARIANT: 0 nt load+store, payload loads issued before the header
+// is decoded (default); 1 the same with 2 frames per iteration; 2 plain
+// loads/stores; 3 nt loads / plain stores; 4 header first, then payload (the
+// round-1 kernel); 5 header first, 2 frames.  B2P_ASM_GRID: workgroups of 4 waves
 hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s) {
   if (a.nchunk > 256) return hipErrorInvalidValue;
   static const int variant = getenv("B2P_ASM_VARIANT") ? atoi(getenv("B2P_ASM_VARIANT")) : 0;
   static const long grid_env = getenv("B2P_ASM_GRID") ? atol(getenv("B2P_ASM_GRID")) : 0;
-  const int k = variant == 1 ? 2 : (variant == 4 ? 4 : 1);
+  const int k = (variant == 1 || variant == 5) ? 2 : 1;
   uint64_t blocks = (a.ndf + 4 * k - 1) / (4 * k);  // 4 waves per workgroup
   const uint64_t cap = grid_env > 0 ? (uint64_t)grid_env : 8192;  // swept: profiles/r01_assemble_sweep.txt
   if (blocks > cap) blocks = cap;
@@ -452,11 +461,12 @@ hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s) {
   void *args[] = {&arg};
   const void *f;
   switch (variant) {
-    case 1: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 2>); break;
-    case 2: f = reinterpret_cast<const void *>(b2p_assemble_kernel<false, false, 1>); break;
-    case 3: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, false, 1>); break;
-    case 4: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 4>); break;
-    default: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 1>);
+    case 1: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 2, true>); break;
+    case 2: f = reinterpret_cast<const void *>(b2p_assemble_kernel<false, false, 1, true>); break;
+    case 3: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, false, 1, true>); break;
+    case 4: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 1, false>); break;
+    case 5: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 2, false>); break;
+    default: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 1, true>);
   }
   return hipLaunchKernel(f, dim3((uint32_t)blocks), dim3(256), args, 0, s);
 }

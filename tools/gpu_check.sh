@@ -49,7 +49,7 @@ for s in $STEPS; do
     asm) run bench_assemble 600 python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
     profasm) run prof_asm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
-    asmsweep) for v in 0 1 2 3 4; do for g in 1024 2048 4096 8192; do
+    asmsweep) for v in 0 1 4 5; do for g in 4096 8192 16384; do
                 run asm_v${v}_g${g} 300 env B2P_ASM_VARIANT=$v B2P_ASM_GRID=$g python3 tools/bench_assemble.py \
                   --steps 10 --warmup 2 --order tm || exit $?
               done; done ;;
