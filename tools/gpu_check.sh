@@ -59,6 +59,7 @@ for s in $STEPS; do
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm &&
          run pmc_write_asm 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm ;;
+    matrix) run perf_matrix 600 python3 tools/perf_matrix.py --steps 20 ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&

@@ -1,0 +1,75 @@
+"""Integrate-kernel throughput over the layouts the path supports, at full
+integration size (1024 x 1024 samples), HBM-resident, region-timed:
+int8 / int16 LE / int16 BE (BMF), 1 or 2 output pols, narrow and wide
+channel counts.  One JSON line per case; a slow corner shows up as a low
+GB/s against the ~7 TB/s of the headline layouts.
+
+  python tools/perf_matrix.py [--steps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "paf-baseband2power_amd"))
+import torch  # noqa: E402,F401  (one HIP runtime per process)
+
+import paf_b2p  # noqa: E402
+from paf_b2p.geometry import generic_geom, bmf_geom, make_geom  # noqa: E402
+
+CASES = [
+    ("int8 256ch (configs[1])", lambda **k: generic_geom(256, **k)),
+    ("int8 1024ch (configs[2..4])", lambda **k: generic_geom(1024, **k)),
+    ("int8 64ch", lambda **k: generic_geom(64, **k)),
+    ("int8 336ch", lambda **k: generic_geom(336, **k)),
+    ("int16 LE 256ch", lambda **k: generic_geom(256, nbit=16, **k)),
+    ("int16 LE 48ch", lambda **k: generic_geom(48, nbit=16, **k)),
+    ("int16 BE BMF 48x7", lambda **k: bmf_geom(**k)),
+    ("int16 BE TFTFP 8x8", lambda **k: make_geom(nbit=16, big_endian=1, nchunk=8, nsamp_df=128,
+                                                 nchan_chunk=8, **k)),
+]
+
+
+def run(name, geom, steps):
+    it = paf_b2p.Integrator(geom)
+    bb = it.block_bytes
+    blocks = []
+    for b in range(2):
+        d = it.alloc(bb)
+        it.fill_synthetic(d, 20181105, 0, b)
+        blocks.append(d)
+    out = it.alloc(it.nout * 4 * steps)
+    for k in range(3):
+        it.integrate(blocks[k % 2], out.ptr, True)
+    it.sync()
+    it.reset_stats()
+    it.set_timing(2)
+    for k in range(steps):
+        it.integrate(blocks[k % 2], out.ptr + k * it.nout * 4, True)
+    it.set_timing(0)
+    it.sync()
+    st = it.stats()
+    us = st["kernel_ms"] / steps * 1e3
+    res = {"case": name, "npol_out": geom.npol_out, "bytes": bb, "us_per_integration": round(us, 1),
+           "GBps": round(bb / us / 1e3, 1), "threads": it.info.threads, "unroll": it.info.unroll,
+           "row_groups": it.info.row_groups, "columns": it.info.columns}
+    for d in blocks + [out]:
+        d.free()
+    it.close()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    for name, mk in CASES:
+        for npo in (1, 2):
+            print(json.dumps(run(name, mk(npol_out=npo), a.steps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
