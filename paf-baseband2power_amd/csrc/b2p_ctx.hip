@@ -202,11 +202,23 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
     int v = atoi(e);
     if (v >= 64 && v <= 1024) maxT = (uint32_t)v;
   }
-  if (c->CP <= maxT) {
-    const uint32_t L = c->CP / gcd_u(c->CP, 64) * 64;  // lcm(CP, 64)
+  const uint32_t L = c->CP / gcd_u(c->CP, 64) * 64;  // lcm(CP, 64)
+  uint32_t colB = 0;  // whole-wave divisor of L for a row split into columns
+  if (c->CP <= maxT && L > maxT && g->nchunk == 1)
+    for (uint32_t b = maxT / 64 * 64; b >= 256 && !colB; b -= 64)
+      if (L % b == 0) colB = b;
+  if (c->CP <= maxT && !colB) {
     c->B = L <= maxT ? (maxT / L) * L : (maxT / c->CP) * c->CP;
     c->S = c->B;
     c->NC = 1;
+  } else if (colB) {
+    // the channel period fits a workgroup but not in whole waves (e.g. 336
+    // int8 channels = 84 vectors): a row of lcm(period, 64) vectors split
+    // into whole-wave columns keeps every lane on fixed channels without a
+    // partial wave (504 threads measured 6.3 TB/s, tools/perf_matrix.py)
+    c->B = colB;
+    c->S = L;
+    c->NC = L / colB;
   } else {
     // the frame is split into NC = CP / B columns: the largest whole-wave B
     // (multiple of 64) that divides the frame -- partial waves straddle
@@ -229,7 +241,9 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   c->Bpad = (c->B + 63) / 64 * 64;
   // one workgroup per CU: with ~32 KiB of loads in flight per CU more
   // resident waves only cost bandwidth (tools/tune.py sweep)
-  uint32_t per_cu = 1;
+  // ... counted as ~8 waves: a narrower workgroup (a frame that only
+  // divides into 256-thread columns) gets two per CU
+  uint32_t per_cu = std::max<uint32_t>(1, 512 / c->Bpad);
   if (const char *e = getenv("B2P_WG_PER_CU")) {
     int v = atoi(e);
     if (v >= 1 && v <= 32) per_cu = (uint32_t)v;
