@@ -153,7 +153,7 @@ def main():
         geom.nsamp_int = nf * geom.nsamp_df
         elem0 = first * paf_b2p.geometry.frame_bytes(geom) // (geom.nbit // 8)
     # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
-    it = paf_b2p.Integrator(geom, device=local)
+    it = paf_b2p.Integrator(geom, device=D.device_of(local))
     nout, bb = it.nout, it.block_bytes
 
     if split:

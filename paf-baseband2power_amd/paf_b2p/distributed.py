@@ -33,11 +33,20 @@ def subband_of(rank: int) -> int:
     return rank
 
 
+def device_of(local_rank: int) -> int:
+    """GPU of a local rank: rank r on GPU r when every GPU is visible; when a
+    launcher gives each process fewer devices (one visible GPU), wrap
+    (paf_baseband2power.cu:89-90 uses index 0 with one GPU)."""
+    n = torch.cuda.device_count()  # does not initialise HIP
+    return local_rank % n if n > 0 else 0
+
+
 def init(backend: str, local_rank: int) -> None:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dev = device_of(local_rank)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     else:
         dist.init_process_group(backend)
 

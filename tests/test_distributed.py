@@ -141,3 +141,14 @@ def test_time_share_rules():
                                                              (4096, 2048), (6144, 2048)]
     with pytest.raises(ValueError):
         D.time_share(0, 3, 8192)
+
+
+def test_device_of_wraps_to_visible_devices(monkeypatch):
+    sys.path.insert(0, PKG)
+    from paf_b2p import distributed as D
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert [D.device_of(r) for r in (0, 3, 7)] == [0, 3, 7]
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert D.device_of(5) == 0          # one visible GPU per process
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
+    assert D.device_of(2) == 0
