@@ -60,6 +60,13 @@ for s in $STEPS; do
          run pmc_write_asm 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm ;;
     matrix) run perf_matrix 600 python3 tools/perf_matrix.py --steps 20 ;;
+    knobs) i=0
+           for kv in "B2P_UNROLL=8" "B2P_UNROLL=16" "B2P_MAX_THREADS=448" "B2P_MAX_THREADS=256" \
+                     "B2P_INTERLEAVE=1" "B2P_INTERLEAVE=0" "B2P_WG_PER_CU=2" "B2P_NT=0"; do
+             i=$((i+1))
+             run knob_$i 300 env $kv python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 2 &&
+             run knob16_$i 300 env $kv python3 tools/perf_matrix.py --steps 20 --only "int16 LE 256ch" --npol-out 1 || exit $?
+           done ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&

@@ -65,10 +65,18 @@ def run(name, geom, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--only", default="", help="substring of the case names to run")
+    ap.add_argument("--npol-out", type=int, default=0, help="1 or 2 (default both)")
     a = ap.parse_args()
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("B2P_")}
     for name, mk in CASES:
-        for npo in (1, 2):
-            print(json.dumps(run(name, mk(npol_out=npo), a.steps)), flush=True)
+        if a.only and a.only not in name:
+            continue
+        for npo in ((a.npol_out,) if a.npol_out else (1, 2)):
+            r = run(name, mk(npol_out=npo), a.steps)
+            if knobs:
+                r["env"] = knobs
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
