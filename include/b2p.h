@@ -164,6 +164,13 @@ int b2p_finish_partial_async(b2p_ctx_t *ctx, uint64_t *sums, int sums_is_device)
  * nsamp_total (0: this context's nsamp_int).  Stream-ordered. */
 int b2p_finalize_sums(b2p_ctx_t *ctx, const uint64_t *sums, uint64_t nspec, uint64_t nsamp_total,
                       float *out);
+/* Host fences on the context's stream, for consumers that keep several ring
+ * blocks in flight: b2p_fence returns a ticket covering everything enqueued
+ * so far (a deferred finalize stays deferred); b2p_fence_wait blocks until
+ * that work has finished.  The last 8 tickets wait precisely; an older one
+ * waits for the whole stream. */
+int b2p_fence(b2p_ctx_t *ctx, uint64_t *ticket);
+int b2p_fence_wait(b2p_ctx_t *ctx, uint64_t ticket);
 int b2p_sync(b2p_ctx_t *ctx);
 /* One whole integration in one call: push exactly block_bytes and emit it,
  * enqueued (out valid after b2p_sync()).  For a device span this is ONE

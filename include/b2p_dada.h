@@ -56,10 +56,12 @@ typedef struct ipcbuf {
   uint64_t nbufs, bufsz;
   int iread;              /* reader slot, -1 if not a reader */
   uint64_t xfer_count;    /* blocks taken by this process */
-  int cur_open;           /* a block is open */
-  uint64_t cur_index;
+  int cur_open;           /* blocks open (writer: 0/1; reader: up to read_depth) */
+  uint64_t cur_index;     /* the block opened last */
+  int read_depth;         /* reader: blocks it may hold at once (0 = 1, PSRDADA) */
+  int eod_pending;        /* reader: the empty EOD block waits behind open ones */
 } ipcbuf_t;
-#define IPCBUF_INIT {0, 0, -1, -1, NULL, NULL, 0, 0, -1, 0, 0, 0}
+#define IPCBUF_INIT {0, 0, -1, -1, NULL, NULL, 0, 0, -1, 0, 0, 0, 0, 0}
 
 int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers);
 /* device_id >= 0: blocks in that GPU's memory, owned by a holder process and
@@ -77,7 +79,12 @@ int ipcbuf_unlock_read(ipcbuf_t *id);
 char *ipcbuf_get_next_write(ipcbuf_t *id);
 int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes);
 char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes);
-int ipcbuf_mark_cleared(ipcbuf_t *id);
+int ipcbuf_mark_cleared(ipcbuf_t *id); /* releases the OLDEST block this reader holds */
+/* Extension (not in PSRDADA): let a reader hold up to `depth` blocks at once,
+ * so a GPU consumer can launch on block k+1 before block k's kernel has
+ * finished with it.  ipcbuf_get_next_read / ipcio_open_block_read take the
+ * next block; ipcbuf_mark_cleared / ipcio_close_block_read release the oldest. */
+int ipcbuf_set_read_depth(ipcbuf_t *id, int depth);
 int ipcbuf_enable_sod(ipcbuf_t *id, uint64_t start_buf, uint64_t start_byte);
 int ipcbuf_disable_sod(ipcbuf_t *id);
 int ipcbuf_enable_eod(ipcbuf_t *id); /* end the transfer with an empty block */

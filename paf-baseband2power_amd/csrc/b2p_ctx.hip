@@ -80,6 +80,9 @@ struct b2p_ctx {
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> ev_pool;
   b2p_stats_t stats{};
+  // b2p_fence tickets: event ring
+  hipEvent_t fence_ev[8] = {};
+  uint64_t fence_next = 0;
   char err[256] = {0};
 };
 
@@ -367,6 +370,8 @@ int b2p_close(b2p_ctx_t *c) {
   if (c->d_rep) (void)hipFree(c->d_rep);
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  for (auto e : c->fence_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->region_a) (void)hipEventDestroy(c->region_a);
   if (c->region_b) (void)hipEventDestroy(c->region_b);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -626,6 +631,27 @@ int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64
   a.mean = c->g.mean;
   a.nsamp = (double)(nsamp_total ? nsamp_total : c->g.nsamp_int);
   CK(c, launch_convert(a, c->stream));
+  return B2P_OK;
+}
+
+int b2p_fence(b2p_ctx_t *c, uint64_t *ticket) {
+  if (!c || !ticket) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  const int slot = (int)(c->fence_next % 8);
+  if (!c->fence_ev[slot]) CK(c, hipEventCreateWithFlags(&c->fence_ev[slot], hipEventDisableTiming));
+  CK(c, hipEventRecord(c->fence_ev[slot], c->stream));
+  *ticket = c->fence_next++;
+  return B2P_OK;
+}
+
+int b2p_fence_wait(b2p_ctx_t *c, uint64_t ticket) {
+  if (!c || ticket >= c->fence_next) return B2P_EINVAL;
+  CK(c, hipSetDevice(c->device));
+  if (c->fence_next - ticket > 8) {  // its event was recorded again since
+    CK(c, hipStreamSynchronize(c->stream));
+    return B2P_OK;
+  }
+  CK(c, hipEventSynchronize(c->fence_ev[ticket % 8]));
   return B2P_OK;
 }
 

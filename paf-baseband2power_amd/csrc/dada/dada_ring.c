@@ -312,29 +312,46 @@ int ipcbuf_enable_eod(ipcbuf_t *id) {
 
 static int reader_at_eod(ipcbuf_t *id) {
   uint64_t eod = __atomic_load_n(&id->sync->eod_count, __ATOMIC_ACQUIRE);
-  return eod && id->sync->r_count[id->iread] >= eod;
+  return eod && id->sync->r_count[id->iread] + (uint64_t)id->cur_open >= eod;
+}
+
+int ipcbuf_set_read_depth(ipcbuf_t *id, int depth) {
+  if (!id || depth < 1 || (uint64_t)depth > id->nbufs) return -1;
+  id->read_depth = depth;
+  return 0;
 }
 
 char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {
-  if (!id || id->state != 3 || id->cur_open) return NULL;
+  if (!id || id->state != 3) return NULL;
+  if (id->cur_open >= (id->read_depth > 1 ? id->read_depth : 1)) return NULL;
   if (reader_at_eod(id)) return NULL;
   if (sem_do(id->semid, SEM_FULL(id->iread), -1, 0) < 0) return NULL;
-  id->cur_index = id->sync->r_count[id->iread] % id->nbufs;
-  id->cur_open = 1;
+  id->cur_index = (id->sync->r_count[id->iread] + (uint64_t)id->cur_open) % id->nbufs;
+  id->cur_open++;
   if (bytes) *bytes = sync_nbytes(id->sync)[id->cur_index];
   return id->buffer[id->cur_index];
 }
 
-int ipcbuf_mark_cleared(ipcbuf_t *id) {
-  if (!id || id->state != 3 || !id->cur_open) return -1;
+static int clear_oldest(ipcbuf_t *id) {
   ipcsync_t *s = id->sync;
-  const uint64_t idx = id->cur_index;
+  const uint64_t idx = s->r_count[id->iread] % id->nbufs;
   s->r_count[id->iread]++;
-  id->cur_open = 0;
+  id->cur_open--;
   id->xfer_count++;
   if (__atomic_add_fetch(&sync_clear(s)[idx], 1, __ATOMIC_ACQ_REL) == s->n_readers) {
     __atomic_store_n(&sync_clear(s)[idx], 0, __ATOMIC_RELEASE);
     if (sem_do(id->semid, SEM_CLEAR, 1, 0) < 0) return -1;
+  }
+  return 0;
+}
+
+int ipcbuf_mark_cleared(ipcbuf_t *id) {
+  if (!id || id->state != 3 || id->cur_open < 1) return -1;
+  if (clear_oldest(id) < 0) return -1;
+  /* an empty EOD block taken behind open ones goes once it is the oldest */
+  if (id->eod_pending && id->cur_open == 1) {
+    id->eod_pending = 0;
+    return clear_oldest(id);
   }
   return 0;
 }
@@ -426,7 +443,10 @@ char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id
   char *p = ipcbuf_get_next_read(&ipc->buf, &bytes);
   if (!p) return NULL;
   if (bytes == 0 && ipcbuf_eod(&ipc->buf)) { /* empty EOD marker block */
-    ipcbuf_mark_cleared(&ipc->buf);
+    if (ipc->buf.cur_open == 1)
+      ipcbuf_mark_cleared(&ipc->buf);
+    else
+      ipc->buf.eod_pending = 1; /* released after the blocks still open */
     return NULL;
   }
   if (curbufsz) *curbufsz = bytes;

@@ -266,6 +266,83 @@ static void *worker(void *arg) {
   return NULL;
 }
 
+/* One sub-band on a GPU-resident ring: two blocks in flight.  Block k's
+ * launch is enqueued before block k-1 is released, so the GPU never waits
+ * on the host between integrations.  Block k-1 goes back to the ring once
+ * its launch has finished (b2p_fence).  Its spectrum is finalized by launch
+ * k and copied to the host behind it, so outputs trail by one block. */
+static int write_output(shared_t *sh, const float *spec) {
+  uint64_t bid;
+  char *o = ipcio_open_block_write(sh->out->data_block, &bid);
+  if (!o) return -1;
+  memcpy(o, spec, sh->obytes);
+  ipcio_close_block_write(sh->out->data_block, sh->obytes);
+  sh->nblocks++;
+  sh->t_last = now_s();
+  return 0;
+}
+
+static void run_device_pipelined(shared_t *sh) {
+  sub_t *s = &sh->sub[0];
+  ipcio_t *in = s->in->data_block;
+  const size_t sb = (sh->obytes + 4095) / 4096 * 4096;
+  float *spec = aligned_alloc(4096, 3 * sb); /* spectra k-2, k-1, k */
+  if (!spec || ipcbuf_set_read_depth(&in->buf, 2) < 0) {
+    free(spec);
+    sh->failed = 1;
+    return;
+  }
+  b2p_register_host(s->ctx, spec, 3 * sb);
+#define SPEC(k) ((float *)((char *)spec + ((k) % 3) * sb))
+  uint64_t k = 0, written = 0, ticket[2] = {0, 0};
+  int open_prev = 0; /* block k-1 still held */
+  for (;;) {
+    uint64_t bytes = 0, bid = 0;
+    char *blk = ipcio_open_block_read(in, &bytes, &bid);
+    const int full = blk && bytes == s->rbufsz;
+    if (!full) { /* end of data or a partial block: drain the pipeline */
+      if (b2p_sync(s->ctx) != B2P_OK) sh->failed = 1;
+      if (open_prev) ipcio_close_block_read(in, 0);
+      open_prev = 0;
+      for (; !sh->failed && written < k; written++)
+        if (write_output(sh, SPEC(written)) < 0) sh->failed = 1;
+      if (blk) {
+        ipcio_close_block_read(in, bytes);
+        sh->nskipped++;
+        multilog(sh->log, LOG_INFO, "partial integration skipped (a block held %" PRIu64 " of %" PRIu64
+                 " B)", bytes, s->rbufsz);
+      }
+      if (!blk || sh->failed) break;
+      continue;
+    }
+    const double t0 = now_s();
+    if (sh->t_first == 0) sh->t_first = t0;
+    int rc = b2p_integrate(s->ctx, blk, bytes, 1, SPEC(k), 0);
+    if (rc == B2P_OK) rc = b2p_fence(s->ctx, &ticket[k & 1]);
+    if (rc == B2P_OK && open_prev) {
+      rc = b2p_fence_wait(s->ctx, ticket[(k - 1) & 1]); /* launch k-1 is done */
+      ipcio_close_block_read(in, 0);                     /* releases block k-1 */
+      open_prev = 0;
+      for (; rc == B2P_OK && written + 2 <= k; written++) /* spectrum k-2 is home */
+        if (write_output(sh, SPEC(written)) < 0) rc = B2P_EHIP;
+    }
+    if (rc != B2P_OK) {
+      multilog(sh->log, LOG_ERR, "integrate: %s (%s)", b2p_strerror(rc), b2p_last_error(s->ctx));
+      sh->failed = 1;
+      ipcio_close_block_read(in, 0);
+      break;
+    }
+    open_prev = 1;
+    k++;
+    if (k % 64 == 1)
+      multilog(sh->log, LOG_INFO, "integration %" PRIu64 " enqueued (%.3f ms since the previous)",
+               k, (now_s() - t0) * 1e3);
+  }
+#undef SPEC
+  b2p_unregister_host(s->ctx, spec);
+  free(spec);
+}
+
 /* -t N: member r integrates bytes [r*share, (r+1)*share) of every block of
  * the one input ring; member 0 reduces the exact partial sums (RCCL
  * ncclReduce, b2p_group_reduce) and rounds once (second mode) */
@@ -599,6 +676,11 @@ int main(int argc, char *argv[]) {
   }
 
   {
+    if (!split && nmem == 1 && sub[0].ondev && !getenv("B2P_NO_PIPELINE")) {
+      multilog(log, LOG_INFO, "GPU-resident input: two blocks in flight");
+      run_device_pipelined(&sh);
+      goto joined;
+    }
     pthread_barrier_init(&sh.bar, NULL, (unsigned)nmem);
     pthread_t th[MAX_SUB];
     worker_t wk[MAX_SUB];
@@ -610,6 +692,7 @@ int main(int argc, char *argv[]) {
     for (int r = 0; r < nmem; r++) pthread_join(th[r], NULL);
     pthread_barrier_destroy(&sh.bar);
   }
+joined:
   status = sh.failed ? EXIT_FAILURE : EXIT_SUCCESS;
 
 done:

@@ -97,6 +97,8 @@ PROTOTYPES = {
     "b2p_memcpy": (C.c_int, [_P, _P, _P, C.c_size_t, C.c_int]),
     "b2p_memset": (C.c_int, [_P, _P, C.c_int, C.c_size_t]),
     "b2p_finish_partial_async": (C.c_int, [_P, _P, C.c_int]),
+    "b2p_fence": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "b2p_fence_wait": (C.c_int, [_P, C.c_uint64]),
     "b2p_finalize_sums": (C.c_int, [_P, _P, C.c_uint64, C.c_uint64, _P]),
     "b2p_group_reduce": (C.c_int, [_P, _P, C.c_uint64, _P]),
     "b2p_group_open": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int]),

@@ -57,6 +57,7 @@ def dlib():
         L.ipcbuf_get_write_count.restype = C.c_uint64
         L.ipcbuf_get_write_count.argtypes = [P]
         L.ipcbuf_get_device.argtypes = [P]
+        L.ipcbuf_set_read_depth.argtypes = [P, C.c_int]
         L.ipcbuf_copy_in.argtypes = [P, P, P, C.c_uint64]
         L.ipcbuf_copy_out.argtypes = [P, P, P, C.c_uint64]
         L.dada_db_create_work.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint64,
@@ -203,6 +204,28 @@ class Hdu:
             raise OSError("copy out of block")
         L.ipcio_close_block_read(self.data, n.value)
         return buf.raw
+
+    def set_read_depth(self, depth: int) -> None:
+        """hold up to `depth` blocks at once (extension, include/b2p_dada.h)"""
+        if dlib().ipcbuf_set_read_depth(self.data, depth) != 0:
+            raise ValueError(f"read depth {depth}")
+
+    def open_block(self):
+        """(bytes of the next block, its length) without releasing it, or None
+        at end of data; release with close_block (oldest first)"""
+        L = dlib()
+        n, bid = C.c_uint64(), C.c_uint64()
+        p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
+        if not p:
+            return None
+        buf = C.create_string_buffer(n.value)
+        if n.value and L.ipcbuf_copy_out(self.data, buf, p, n.value) != 0:
+            raise OSError("copy out of block")
+        return buf.raw
+
+    def close_block(self) -> None:
+        if dlib().ipcio_close_block_read(self.data, 0) != 0:
+            raise OSError("close_block_read")
 
     def eod(self) -> bool:
         return bool(dlib().ipcbuf_eod(self.data))

@@ -97,6 +97,15 @@ class Integrator:
         L.check(L.lib().b2p_finalize_sums(self._ctx, C.c_void_p(sums_ptr), nspec, nsamp_total,
                                           C.c_void_p(out_ptr)), self._ctx)
 
+    def fence(self) -> int:
+        """b2p_fence: ticket for everything enqueued so far"""
+        t = C.c_uint64()
+        L.check(L.lib().b2p_fence(self._ctx, C.byref(t)), self._ctx)
+        return t.value
+
+    def fence_wait(self, ticket: int) -> None:
+        L.check(L.lib().b2p_fence_wait(self._ctx, ticket), self._ctx)
+
     def finish_async(self, out_ptr: int, out_is_device: bool) -> int:
         rc = L.lib().b2p_finish_async(self._ctx, C.c_void_p(out_ptr), int(out_is_device))
         return L.check(rc, self._ctx, allow=(L.B2P_EPARTIAL,))

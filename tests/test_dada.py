@@ -315,3 +315,38 @@ def test_dfdb_refuses_host_ring_for_assembly(tmp_path, ring):
                         str(tmp_path / "s.df"), "-k", str(tmp_path / "s.chunks")],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "not GPU-resident" in r.stderr
+
+
+@pytest.mark.parametrize("short_last", [True, False])
+def test_reader_read_depth_two(ring, short_last):
+    # extension: a reader holds two blocks; releases go oldest first, the ring
+    # keeps every block until it is released, and EOD (short block, or the
+    # empty block of unlock_write) still ends the transfer
+    key = ring(3, 4096)
+    blocks = [bytes([i]) * 4096 for i in range(6)] + ([b"\x07" * 100] if short_last else [])
+    got, held_max = [], [0]
+
+    def reader():
+        with dada.Hdu(key, "R") as r:
+            r.read_header()
+            r.set_read_depth(2)
+            held = []
+            while (b := r.open_block()) is not None:
+                held.append(b)
+                held_max[0] = max(held_max[0], len(held))
+                if len(held) == 2:
+                    got.append(held.pop(0))
+                    r.close_block()
+            while held:
+                got.append(held.pop(0))
+                r.close_block()
+
+    t = threading.Thread(target=reader)
+    t.start()
+    with dada.Hdu(key, "W") as w:
+        w.write_header("HDR_SIZE 4096\n")
+        for b in blocks:
+            w.write_block(b)
+    t.join(60)
+    assert not t.is_alive()
+    assert got == blocks and held_max[0] == 2
