@@ -33,6 +33,7 @@
 #define MSTR_LEN 512 /* paf_baseband2power.cuh:4 */
 #define TSAMP_BMF_US (27.0 / 32.0) /* README.md:2 */
 #define MAX_SUB 64
+#define kWarm 8 /* outputs before the steady-state clock starts (FINISH line) */
 
 typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
   int device_id;
@@ -174,6 +175,7 @@ typedef struct shared_t {
   int failed;
   uint64_t nblocks, nskipped;
   double t_first, t_last; /* first integration started, last output written */
+  double t_warm;          /* output kWarm written: start of the steady-state span */
   /* time split (-t): the block every member takes its share of */
   char *blk;
   uint64_t blk_bytes, share_bytes, nsamp_full;
@@ -184,6 +186,18 @@ typedef struct worker_t {
   shared_t *sh;
   int r;
 } worker_t;
+
+static int write_output(shared_t *sh, const float *spec) {
+  uint64_t bid;
+  char *o = ipcio_open_block_write(sh->out->data_block, &bid);
+  if (!o) return -1;
+  memcpy(o, spec, sh->obytes);
+  ipcio_close_block_write(sh->out->data_block, sh->obytes);
+  sh->nblocks++;
+  sh->t_last = now_s();
+  if (sh->nblocks == kWarm) sh->t_warm = sh->t_last;
+  return 0;
+}
 
 static void *worker(void *arg) {
   worker_t *w = (worker_t *)arg;
@@ -245,14 +259,9 @@ static void *worker(void *arg) {
         }
       }
       if (!sh->failed) {
-        char *o = ipcio_open_block_write(sh->out->data_block, &bid);
-        if (!o) {
+        if (write_output(sh, sh->spec_host) < 0) {
           sh->failed = 1;
         } else {
-          memcpy(o, sh->spec_host, sh->obytes);
-          ipcio_close_block_write(sh->out->data_block, sh->obytes);
-          sh->nblocks++;
-          sh->t_last = now_s();
           const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s per sub-band, "
                    "%.1f Msamples/s in all", sh->nblocks, dt * 1e3, bytes / dt / 1e9,
@@ -271,16 +280,6 @@ static void *worker(void *arg) {
  * on the host between integrations.  Block k-1 goes back to the ring once
  * its launch has finished (b2p_fence).  Its spectrum is finalized by launch
  * k and copied to the host behind it, so outputs trail by one block. */
-static int write_output(shared_t *sh, const float *spec) {
-  uint64_t bid;
-  char *o = ipcio_open_block_write(sh->out->data_block, &bid);
-  if (!o) return -1;
-  memcpy(o, spec, sh->obytes);
-  ipcio_close_block_write(sh->out->data_block, sh->obytes);
-  sh->nblocks++;
-  sh->t_last = now_s();
-  return 0;
-}
 
 static void run_device_pipelined(shared_t *sh) {
   sub_t *s = &sh->sub[0];
@@ -334,9 +333,9 @@ static void run_device_pipelined(shared_t *sh) {
     }
     open_prev = 1;
     k++;
-    if (k % 64 == 1)
-      multilog(sh->log, LOG_INFO, "integration %" PRIu64 " enqueued (%.3f ms since the previous)",
-               k, (now_s() - t0) * 1e3);
+    if (getenv("B2P_TRACE_PIPELINE") || k % 64 == 1)
+      multilog(sh->log, LOG_INFO, "integration %" PRIu64 " enqueued, %.3f ms in the loop body, "
+               "%.3f ms since the first", k, (now_s() - t0) * 1e3, (now_s() - sh->t_first) * 1e3);
   }
 #undef SPEC
   b2p_unregister_host(s->ctx, spec);
@@ -398,15 +397,9 @@ static void *worker_split(void *arg) {
         }
       }
       if (!sh->failed) {
-        uint64_t bid;
-        char *o = ipcio_open_block_write(sh->out->data_block, &bid);
-        if (!o) {
+        if (write_output(sh, sh->spec_host) < 0) {
           sh->failed = 1;
         } else {
-          memcpy(o, sh->spec_host, sh->obytes);
-          ipcio_close_block_write(sh->out->data_block, sh->obytes);
-          sh->nblocks++;
-          sh->t_last = now_s();
           const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s over %d GPUs",
                    sh->nblocks, dt * 1e3, sh->blk_bytes / dt / 1e9, sh->nsub);
@@ -717,9 +710,11 @@ done:
   free(sh.spec_host);
   dada_hdu_destroy(out);
   multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s, "
-           "%.6f s from the first integration to the last output",
+           "%.6f s from the first integration to the last output, %.6f s for the last %" PRIu64,
            sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED",
-           sh.t_last > sh.t_first ? sh.t_last - sh.t_first : 0.0);
+           sh.t_last > sh.t_first ? sh.t_last - sh.t_first : 0.0,
+           sh.nblocks > kWarm ? sh.t_last - sh.t_warm : 0.0,
+           sh.nblocks > kWarm ? sh.nblocks - kWarm : (uint64_t)0);
   multilog_close(log);
   fclose(fp_log);
   return status;

@@ -5,8 +5,9 @@
 
 on full-size BMF blocks (8192 frames x 48 chunks, 2.625 GiB).  The producer
 re-hands the ring's blocks without rewriting them, so the figure is what the
-consumer sustains through the ring: integrate launch + sync + semaphores +
-output block per integration.  Prints one JSON line.
+consumer sustains through the ring: integrate launch + fences + semaphores +
+output block per integration.  "steady_*" leaves out the first 8 outputs
+(first-launch and producer start-up costs).  Prints one JSON line.
 
   python tools/bench_ring.py [--blocks 200] [--ndf 8192]
 """
@@ -64,12 +65,17 @@ def main():
             print("\n".join(e[-800:] for e in errs), file=sys.stderr)
             return 1
         log = open(os.path.join(d, "paf_baseband2power.log")).read()
+        if os.environ.get("BENCH_RING_KEEP_LOG"):
+            with open(os.environ["BENCH_RING_KEEP_LOG"], "w") as f:
+                f.write(log)
         per = [float(m) for m in re.findall(r"integration \d+: ([0-9.]+) ms", log)]
         m = re.search(r"FINISH PAF_PROCESS: (\d+) integrations.* ([0-9.]+) s from the first", log)
         steady = per[a.nbufs + 1:] or per
         med = statistics.median(steady) if steady else None  # the pipelined path logs no per-block time
         samples = a.ndf * 128 * nout * 2  # channels x pols x time, as bench.py counts
         n_int, el = (int(m.group(1)), float(m.group(2))) if m else (0, 0.0)
+        ms = re.search(r"([0-9.]+) s for the last (\d+)", log)
+        el_s, n_s = (float(ms.group(1)), int(ms.group(2))) if ms else (0.0, 0)
         print(json.dumps({
             "path": ("host ring -> paf_baseband2power (pinned H2D, overlapped)" if a.host else
                      "device ring (dada_db -g) -> paf_baseband2power in place"),
@@ -79,6 +85,10 @@ def main():
             "consumer_elapsed_s": el,
             "ring_Msamples_s": round(n_int * samples / el / 1e6, 1) if el else None,
             "ring_GBps": round(n_int * bufsz / el / 1e9, 1) if el else None,
+            "steady_blocks": n_s,
+            "steady_ms_per_block": round(el_s / n_s * 1e3, 4) if n_s else None,
+            "steady_Msamples_s": round(n_s * samples / el_s / 1e6, 1) if n_s else None,
+            "steady_GBps": round(n_s * bufsz / el_s / 1e9, 1) if n_s else None,
             "wall_s_incl_startup": round(wall, 2),
         }), flush=True)
         return 0
