@@ -265,6 +265,8 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   return B2P_OK;
 }
 
+static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out);
+
 int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (!out || !g) return set_err(nullptr, B2P_EINVAL, "null argument");
   *out = nullptr;
@@ -318,6 +320,11 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "hipStreamCreate"));
   c->stream = c->own_stream;
+  // fence events up front: the first event a process creates can take tens
+  // of ms, which must not land on the first integration of a pipeline
+  for (auto &e : c->fence_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return fail(set_err(c, B2P_EHIP, "hipEventCreate"));
   // two replica sets, then the two 4-B tickets (zeroed together; every
   // finalize leaves its set and ticket zero again)
   const size_t set_words = (size_t)c->nrep * c->nout;
@@ -331,6 +338,12 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (hipMemsetAsync(c->d_rep, 0, rep_bytes, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "zero replicas"));
+  // load the code object now: a process's first kernel launch costs tens of
+  // ms (40 ms measured in paf_baseband2power), which belongs to start-up,
+  // not to the first integration.  An empty span runs the chosen kernel on
+  // no rows and adds nothing.
+  if ((rc = enqueue_span(c, c->d_rep, 0, nullptr)) != B2P_OK) return fail(rc);
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(set_err(c, B2P_EHIP, "warm-up launch"));
 
   *out = c;
   return B2P_OK;
