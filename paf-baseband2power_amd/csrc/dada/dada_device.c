@@ -17,6 +17,10 @@
  *    their own stream synchronisation: a writer's kernels are complete
  *    before ipcbuf_mark_filled, a reader's before ipcbuf_mark_cleared.
  *
+ * The creator forks: call dada_db_create_work from a single-threaded program
+ * (the dada_db tool does; paf_b2p.dada runs that tool rather than forking a
+ * threaded Python process).
+ *
  * HIP is reached through dlopen of libamdhip64.so.7, so libpafdada still
  * loads (and host rings still work) on machines without ROCm; in a process
  * that already mapped a HIP runtime (torch, libpafb2p) the same one is used.
@@ -24,6 +28,7 @@
 #include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <pthread.h>
 #include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -156,7 +161,7 @@ int dev_create_blocks(int syncid, ipcsync_t *s, int device) {
   sigaddset(&set, SIGTERM);
   sigaddset(&set, SIGINT);
   sigaddset(&set, SIGHUP);
-  sigprocmask(SIG_BLOCK, &set, &old);
+  pthread_sigmask(SIG_BLOCK, &set, &old);
   pid_t mid = fork();
   if (mid == 0) {
     close(fds[0]);
@@ -173,7 +178,7 @@ int dev_create_blocks(int syncid, ipcsync_t *s, int device) {
     }
     holder(syncid, s, device, fds[1]);
   }
-  sigprocmask(SIG_SETMASK, &old, NULL);
+  pthread_sigmask(SIG_SETMASK, &old, NULL);
   close(fds[1]);
   if (mid < 0) {
     close(fds[0]);
