@@ -229,17 +229,26 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
     uint32_t best = 0;
     for (uint32_t b = maxT / 64 * 64; b >= 64; b -= 64)
       if (c->CP % b == 0) { best = b; break; }
-    if (!best)
-      for (uint32_t b = maxT; b >= 128; --b)
-        if (c->CP % b == 0) { best = b; break; }
-    if (!best) return set_err(c, B2P_EINVAL, "no workgroup shape divides the %u-vector frame", c->CP);
     if (const char *e = getenv("B2P_THREADS")) {  // tuning knob: exact divisor
       int v = atoi(e);
       if (v >= 64 && v <= 1024 && c->CP % (uint32_t)v == 0) best = (uint32_t)v;
     }
-    c->B = best;
-    c->S = c->CP;
-    c->NC = c->CP / c->B;
+    if (best) {
+      c->B = best;
+      c->S = c->CP;
+      c->NC = c->CP / c->B;
+    } else {
+      // no whole-wave divisor (e.g. 61 chunks x 11 vectors): rows of
+      // lcm(frame, 64) vectors, split into whole-wave columns (64 always
+      // divides), so every lane still keeps its channels
+      const uint64_t rowv = (uint64_t)c->CP / gcd_u(c->CP, 64) * 64;
+      if (rowv > 0x7fffffffull) return set_err(c, B2P_EINVAL, "frame of %u vectors too large", c->CP);
+      uint32_t b = maxT / 64 * 64;
+      while (b > 64 && rowv % b) b -= 64;
+      c->B = b;
+      c->S = (uint32_t)rowv;
+      c->NC = (uint32_t)(rowv / b);
+    }
   }
   c->Bpad = (c->B + 63) / 64 * 64;
   // one workgroup per CU: with ~32 KiB of loads in flight per CU more

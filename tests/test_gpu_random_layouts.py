@@ -1,0 +1,58 @@
+"""Property-based GPU parity: hypothesis draws layouts the C ABI accepts
+(b2p_geom_check) -- int8 / int16 LE / int16 BE, 1..64 chunks, odd channel
+counts, 1..N samples per frame, 1 or 2 output pols, sum or mean -- plus a
+random split of the integration into pushes, and checks the HIP result
+against the oracle bit for bit.  One Integrator per example, all in this
+one process (the GPU box allows few processes)."""
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import b2p_oracle as npo
+import oracle_c as co
+import paf_b2p
+
+pytestmark = pytest.mark.gpu
+
+
+@st.composite
+def layouts(draw):
+    nbit = draw(st.sampled_from([8, 16]))
+    big_endian = draw(st.booleans()) if nbit == 16 else False
+    word = 4 * nbit // 8
+    nchunk = draw(st.integers(1, 64))
+    nchan_chunk = draw(st.integers(1, 96))
+    # smallest nsamp_df that makes a chunk a whole number of 16-B vectors
+    base = 1
+    while (base * nchan_chunk * word) % 16:
+        base *= 2
+    nsamp_df = base * draw(st.integers(1, 4))
+    npol_out = draw(st.sampled_from([1, 2]))
+    nchunk = min(nchunk, 8192 // (nchan_chunk * npol_out))  # b2p_geom_check: nout <= 8192
+    frame = nchunk * nsamp_df * nchan_chunk * word
+    nframes = draw(st.integers(1, max(1, (3 << 20) // frame)))
+    g = npo.Geom(nbit=nbit, big_endian=int(big_endian), nchunk=nchunk, nsamp_df=nsamp_df,
+                 nchan_chunk=nchan_chunk, npol_out=npol_out, nsamp_int=nframes * nsamp_df,
+                 mean=int(draw(st.booleans())))
+    cuts = sorted(draw(st.lists(st.integers(1, max(1, nframes - 1)), max_size=3, unique=True)))
+    cuts = [c for c in cuts if 0 < c < nframes]
+    seed = draw(st.integers(0, 2 ** 32 - 1))
+    return g, cuts, seed
+
+
+@settings(max_examples=120, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(layouts())
+def test_random_layouts_match_oracle(gpu, case):
+    g, cuts, seed = case
+    buf = co.fill_synthetic(g, g.block_bytes, seed, seed % 7, seed % 5)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        d = it.upload(buf)
+        bounds = [0] + [c * g.frame_bytes for c in cuts] + [g.block_bytes]
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            it.push((d, a, b - a))
+        out = it.finish()
+        d.free()
+    want = co.power(g, buf, nthreads=8)
+    assert np.array_equal(out.view(np.uint32), want.view(np.uint32)), (g, cuts, seed)

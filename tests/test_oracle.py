@@ -180,3 +180,37 @@ def test_hdr_pin_live_reference_if_present():
         L.hdr_keys(buf.ctypes.data, h)
         assert [h.valid, h.idf, h.sec, h.epoch, h.beam] == [int(x) for x in
                                                              d["valid_idf_sec_epoch_beam"][i]]
+
+
+# ---- the two restatements agree on random layouts (hypothesis) -----------------
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@st.composite
+def _layouts(draw):
+    nbit = draw(st.sampled_from([8, 16]))
+    be = int(draw(st.booleans())) if nbit == 16 else 0
+    word = 4 * nbit // 8
+    ncc = draw(st.integers(1, 40))
+    base = 1
+    while (base * ncc * word) % 16:
+        base *= 2
+    nsdf = base * draw(st.integers(1, 3))
+    nchunk = draw(st.integers(1, 12))
+    frames = draw(st.integers(1, 12))
+    return npo.Geom(nbit=nbit, big_endian=be, nchunk=nchunk, nsamp_df=nsdf, nchan_chunk=ncc,
+                    npol_out=draw(st.sampled_from([1, 2])), nsamp_int=frames * nsdf,
+                    mean=int(draw(st.booleans()))), draw(st.integers(0, 2 ** 32 - 1))
+
+
+@settings(max_examples=150, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow])
+@given(_layouts())
+def test_c_and_numpy_restatements_agree(case):
+    g, seed = case
+    buf = co.fill_synthetic(g, g.block_bytes, seed, seed % 3, seed % 11)
+    assert np.array_equal(buf, npo.fill_synthetic(g, g.block_bytes, seed, seed % 3, seed % 11))
+    acc = npo.integrate(g, buf)
+    assert np.array_equal(co.integrate(g, buf), acc)
+    assert np.array_equal(co.finalize(g, acc).view(np.uint32), npo.finalize(g, acc).view(np.uint32))
