@@ -1,0 +1,422 @@
+/*
+ * paf_capture -- receive BMF data frames over UDP into a GPU-resident ring
+ * (the reference's paf_capture.c:46-189, capture.c,
+ * sync.c).
+ *
+ * The reference runs one thread per port, copies each payload into the host
+ * ring block at (idf*NCHK_NIC + chunk)*7168 (capture.c:536-541), parks
+ * frames that belong to the next block in a temp buffer
+ * (capture.c:464-531) and lets a spin loop switch blocks and advance the
+ * reference header (sync.c:95-175).  Here one receive thread gathers frames
+ * (recvmmsg over every port) and decodes each header on the host only to
+ * sort it by time (capture.c:562-568 frame index): frames of the current
+ * block go to a pinned batch, frames of later blocks to a spill buffer (the
+ * temp buffer's role), frames of past blocks are dropped (capture.c:464-466).
+ * The GPU places the payloads: each batch is uploaded once and scattered by
+ * b2p_assemble into the current block of a dada_db -g ring.  When the block
+ * switches, the spill is sorted again against the new reference.
+ *
+ *   paf_capture -a key -f header_file [-c rbuf_ndf] [-j seconds | -n blocks]
+ *               [-I ip] [-P 17100] [-N 6] [-m ip | -m freq:F0]
+ *               [-x ref_idf -s ref_sec] [-t idle_s] [-k dir] [-Z]
+ *   paf_capture -o frames.df -O chunks.u8 ...      (no GPU: record what arrives)
+ *
+ * Chunk of a frame: -m ip (default) derives it from the sender address as
+ * acquire_ifreq does (capture.c:570-584); -m freq:F0 uses round(freq - F0)
+ * from the frame header (test senders on one host).  The reference time is
+ * the first frame received unless -x/-s give it.  A block is closed once a
+ * frame arrives TBUF_NDF (256, capture.h:35) frames past its end, or when
+ * the stream goes idle.
+ */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
+#include <arpa/inet.h>
+#include <errno.h>
+#include <getopt.h>
+#include <inttypes.h>
+#include <math.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "b2p.h"
+#include "b2p_dada.h"
+#include "b2p_df.h"
+
+#define MAXPORT 16
+#define RECV_BATCH 64
+#define TBUF_NDF 256 /* capture.h:35 */
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+typedef struct cap_t {
+  /* ring / GPU */
+  dada_hdu_t *hdu;
+  b2p_ctx_t *ctx;
+  char *blk;
+  uint64_t bufsz, block_ndf, nblk_done, nblk_max;
+  int nchunk, nozero;
+  void *d_frames, *d_chunks; /* the uploaded batch */
+  unsigned long long *d_cnt;
+  uint64_t placed_all, dropped_late, dropped_spill;
+  /* host: frames of the current block, and of later ones */
+  unsigned char *hf, *hc, *sf, *sc;
+  uint64_t hn, cap_frames, sn, spill_cap;
+  /* time */
+  b2p_df_hdr_t ref; /* reference of the current block */
+  int have_ref;
+  int64_t max_rel;  /* furthest frame seen, relative to ref */
+  multilog_t *log;
+} cap_t;
+
+/* file one received frame by its index relative to the current block */
+static void file_frame(cap_t *c, const unsigned char *df, unsigned char chunk, int64_t rel) {
+  if (rel < 0) {
+    c->dropped_late++; /* behind the block (capture.c:464-466) */
+  } else if (rel < (int64_t)c->block_ndf || !c->spill_cap) {
+    if (c->hn < c->cap_frames) {
+      memcpy(c->hf + c->hn * B2P_DF_BYTES, df, B2P_DF_BYTES);
+      c->hc[c->hn++] = chunk;
+    }
+  } else if (c->sn < c->spill_cap) {
+    memcpy(c->sf + c->sn * B2P_DF_BYTES, df, B2P_DF_BYTES);
+    c->sc[c->sn++] = chunk;
+  } else {
+    c->dropped_spill++; /* too far ahead: the reference forces a switch first */
+  }
+}
+
+/* upload the batch and scatter it into the current block */
+static int flush_batch(cap_t *c) {
+  if (!c->hn) return 0;
+  if (b2p_memcpy(c->ctx, c->d_frames, c->hf, c->hn * B2P_DF_BYTES, 1) != B2P_OK ||
+      b2p_memcpy(c->ctx, c->d_chunks, c->hc, c->hn, 1) != B2P_OK)
+    return -1;
+  const int rc = b2p_assemble(c->ctx, c->d_frames, c->hn, B2P_DF_BYTES, c->d_chunks, c->ref.idf,
+                              c->ref.sec, c->blk, c->block_ndf, (uint32_t)c->nchunk, c->d_cnt);
+  c->hn = 0;
+  return rc == B2P_OK ? 0 : -1;
+}
+
+static int open_block(cap_t *c) {
+  uint64_t bid;
+  c->blk = ipcio_open_block_write(c->hdu->data_block, &bid);
+  if (!c->blk) return -1;
+  if (!c->nozero && b2p_memset(c->ctx, c->blk, 0, c->bufsz) != B2P_OK) return -1;
+  if (b2p_memset(c->ctx, c->d_cnt, 0, (c->nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) return -1;
+  /* the spill, sorted again against this block's reference */
+  const uint64_t n = c->sn;
+  c->sn = 0;
+  c->max_rel = -1;
+  for (uint64_t i = 0; i < n; i++) {
+    const unsigned char *df = c->sf + i * B2P_DF_BYTES;
+    b2p_df_hdr_t h;
+    b2p_df_decode(df, &h);
+    const int64_t rel = b2p_df_index(&h, &c->ref);
+    if (rel > c->max_rel) c->max_rel = rel;
+    if (rel >= (int64_t)c->block_ndf) { /* still ahead: compact in place */
+      memmove(c->sf + c->sn * B2P_DF_BYTES, df, B2P_DF_BYTES);
+      c->sc[c->sn++] = c->sc[i];
+    } else {
+      file_frame(c, df, c->sc[i], rel);
+    }
+  }
+  return 0;
+}
+
+static int close_block(cap_t *c) {
+  if (flush_batch(c) < 0) return -1;
+  unsigned long long cnt[256 + 3];
+  if (b2p_sync(c->ctx) != B2P_OK ||
+      b2p_memcpy(c->ctx, cnt, c->d_cnt, (c->nchunk + 3) * sizeof(unsigned long long), 2) != B2P_OK)
+    return -1;
+  uint64_t placed = 0;
+  for (int i = 0; i < c->nchunk; i++) placed += cnt[i];
+  const uint64_t expect = c->block_ndf * (uint64_t)c->nchunk;
+  multilog(c->log, LOG_INFO, "block %" PRIu64 ": %" PRIu64 " of %" PRIu64 " frames (%.3f%% lost), %llu with a "
+           "bad chunk", c->nblk_done, placed, expect, 100.0 * (double)(expect - placed) / (double)expect,
+           cnt[c->nchunk + 2]);
+  c->placed_all += placed;
+  ipcio_close_block_write(c->hdu->data_block, c->bufsz);
+  c->blk = NULL;
+  c->nblk_done++;
+  b2p_df_ref_advance(&c->ref, c->block_ndf); /* sync.c:119-125 */
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  key_t key = 0;
+  int have_key = 0, port0 = 17100, nport = 6, arg, nozero = 0;
+  const char *hfile = NULL, *ip = "0.0.0.0", *mapping = "ip", *ofile = NULL, *ocfile = NULL,
+             *logdir = NULL;
+  uint64_t rbuf_ndf = 8192, nblocks = 0, ref_idf = 0, ref_sec = 0;
+  int have_ref = 0;
+  double length = 0, idle_s = 2.0, freq = 0;
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:i:j:k:I:P:N:m:x:s:n:t:o:O:Zh")) != -1) {
+    switch (arg) {
+      case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
+      case 'b': case 'd': break; /* sod / record-header flags: accepted (paf_capture.c:75-85) */
+      case 'c': rbuf_ndf = strtoull(optarg, NULL, 10); break;
+      case 'f': hfile = optarg; break;
+      case 'i': freq = atof(optarg); break;
+      case 'j': length = atof(optarg); break;
+      case 'k': logdir = optarg; break;
+      case 'I': ip = optarg; break;
+      case 'P': port0 = atoi(optarg); break;
+      case 'N': nport = atoi(optarg); break;
+      case 'm': mapping = optarg; break;
+      case 'x': ref_idf = strtoull(optarg, NULL, 10); have_ref = 1; break;
+      case 's': ref_sec = strtoull(optarg, NULL, 10); have_ref = 1; break;
+      case 'n': nblocks = strtoull(optarg, NULL, 10); break;
+      case 't': idle_s = atof(optarg); break;
+      case 'o': ofile = optarg; break;
+      case 'O': ocfile = optarg; break;
+      case 'Z': nozero = 1; break;
+      default:
+        fprintf(stdout,
+                "paf_capture -a key -f header [-c rbuf_ndf] [-j seconds | -n blocks] [-I ip] [-P port0]\n"
+                "            [-N nports] [-m ip|freq:F0] [-x ref_idf -s ref_sec] [-t idle_s] [-k dir] [-Z]\n"
+                "paf_capture -o frames.df -O chunks.u8 [-I ip] [-P port0] [-N nports] [-m ...] [-t idle_s]\n");
+        return EXIT_FAILURE;
+    }
+  }
+  const int record = ofile != NULL;
+  if ((!record && (!have_key || !hfile)) || (record && !ocfile) || nport < 1 || nport > MAXPORT) {
+    fprintf(stderr, "paf_capture: -a and -f (or -o and -O) are required, 1 <= -N <= %d\n", MAXPORT);
+    return EXIT_FAILURE;
+  }
+  double freq0 = 0;
+  const int by_freq = !strncmp(mapping, "freq:", 5);
+  if (by_freq) freq0 = atof(mapping + 5);
+  else if (strcmp(mapping, "ip")) {
+    fprintf(stderr, "paf_capture: -m ip or -m freq:F0\n");
+    return EXIT_FAILURE;
+  }
+  (void)freq;
+
+  cap_t c;
+  memset(&c, 0, sizeof c);
+  c.log = multilog_open("paf_capture", 0);
+  multilog_add(c.log, stderr);
+  FILE *logf = NULL;
+  if (logdir) {
+    char p[4096];
+    snprintf(p, sizeof p, "%s/paf_capture.log", logdir);
+    if ((logf = fopen(p, "w"))) multilog_add(c.log, logf);
+  }
+  int status = EXIT_FAILURE, locked = 0;
+  int socks[MAXPORT];
+  for (int p = 0; p < nport; p++) socks[p] = -1;
+  FILE *fo = NULL, *fco = NULL;
+
+  /* sockets: one per port (capture.c:146-176), large receive buffers */
+  for (int p = 0; p < nport; p++) {
+    socks[p] = socket(AF_INET, SOCK_DGRAM, 0);
+    int rcv = 256 << 20;
+    setsockopt(socks[p], SOL_SOCKET, SO_RCVBUF, &rcv, sizeof rcv);
+    struct sockaddr_in sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)(port0 + p));
+    if (inet_pton(AF_INET, ip, &sa.sin_addr) != 1 || bind(socks[p], (struct sockaddr *)&sa, sizeof sa) < 0) {
+      multilog(c.log, LOG_ERR, "cannot bind %s:%d (%s)", ip, port0 + p, strerror(errno));
+      goto done;
+    }
+  }
+
+  if (record) {
+    fo = fopen(ofile, "wb");
+    fco = fopen(ocfile, "wb");
+    if (!fo || !fco) goto done;
+  } else {
+    c.hdu = dada_hdu_create(c.log);
+    dada_hdu_set_key(c.hdu, key);
+    if (dada_hdu_connect(c.hdu) < 0 || dada_hdu_lock_write(c.hdu) < 0) {
+      multilog(c.log, LOG_ERR, "cannot attach/lock ring %x", (unsigned)key);
+      goto done;
+    }
+    locked = 1;
+    ipcbuf_t *db = &c.hdu->data_block->buf;
+    if (ipcbuf_get_device(db) < 0) {
+      multilog(c.log, LOG_ERR, "ring %x is not GPU-resident (dada_db -g)", (unsigned)key);
+      goto done;
+    }
+    c.bufsz = ipcbuf_get_bufsz(db);
+    c.nchunk = (int)(c.bufsz / ((uint64_t)rbuf_ndf * B2P_DF_PAYLOAD_BYTES));
+    if (!c.nchunk || c.nchunk > 256 || c.bufsz != rbuf_ndf * (uint64_t)c.nchunk * B2P_DF_PAYLOAD_BYTES) {
+      multilog(c.log, LOG_ERR, "ring block %" PRIu64 " B is not %" PRIu64 " frames x chunks x 7168 B",
+               c.bufsz, rbuf_ndf);
+      goto done;
+    }
+    c.block_ndf = rbuf_ndf;
+    c.nozero = nozero;
+    c.nblk_max = nblocks ? nblocks
+                         : (length > 0 ? (uint64_t)ceil(length / (rbuf_ndf * B2P_DF_TSAMP_SEC)) : UINT64_MAX);
+    b2p_geom_t g;
+    b2p_geom_bmf(&g);
+    g.nchunk = (uint32_t)c.nchunk;
+    g.nsamp_int = rbuf_ndf * g.nsamp_df;
+    if (b2p_open(&c.ctx, &g, ipcbuf_get_device(db)) != B2P_OK) {
+      multilog(c.log, LOG_ERR, "b2p_open: %s", b2p_last_error(NULL));
+      goto done;
+    }
+    if (b2p_dev_alloc(c.ctx, &c.d_frames, rbuf_ndf * c.nchunk * B2P_DF_BYTES) != B2P_OK ||
+        b2p_dev_alloc(c.ctx, &c.d_chunks, rbuf_ndf * c.nchunk) != B2P_OK)
+      goto done;
+    if (b2p_dev_alloc(c.ctx, (void **)&c.d_cnt, (c.nchunk + 3) * sizeof(unsigned long long)) != B2P_OK)
+      goto done;
+    char *hb = ipcbuf_get_next_write(c.hdu->header_block);
+    if (!hb || fileread(hfile, hb, DADA_DEFAULT_HEADER_SIZE) < 0 ||
+        ipcbuf_mark_filled(c.hdu->header_block, DADA_DEFAULT_HEADER_SIZE) < 0) {
+      multilog(c.log, LOG_ERR, "cannot pass header %s", hfile);
+      goto done;
+    }
+  }
+  /* host batch: one block's worth of frames at most (GPU mode), pinned */
+  c.cap_frames = record ? 4096 : rbuf_ndf * (uint64_t)c.nchunk;
+  c.hf = malloc(c.cap_frames * B2P_DF_BYTES);
+  c.hc = malloc(c.cap_frames);
+  /* spill: frames up to the forced switch plus slack, for every chunk */
+  c.spill_cap = record ? 0 : (uint64_t)(2 * TBUF_NDF) * (uint64_t)c.nchunk;
+  c.sf = c.spill_cap ? malloc(c.spill_cap * B2P_DF_BYTES) : NULL;
+  c.sc = c.spill_cap ? malloc(c.spill_cap) : NULL;
+  if (!c.hf || !c.hc || (c.spill_cap && (!c.sf || !c.sc))) goto done;
+  if (c.ctx) b2p_register_host(c.ctx, c.hf, c.cap_frames * B2P_DF_BYTES);
+  if (have_ref) {
+    c.ref.idf = ref_idf;
+    c.ref.sec = ref_sec;
+    c.have_ref = 1;
+    if (!record && open_block(&c) < 0) goto done;
+  }
+
+  {
+    unsigned char *rx = malloc((size_t)RECV_BATCH * B2P_DF_BYTES);
+    if (!rx) goto done;
+    struct pollfd pfd[MAXPORT];
+    for (int p = 0; p < nport; p++) pfd[p] = (struct pollfd){socks[p], POLLIN, 0};
+    uint64_t got_all = 0, bad = 0;
+    double last_rx = now_s(), t_first = 0;
+    int stop = 0;
+    while (!stop) {
+      int pr = poll(pfd, (nfds_t)nport, 20);
+      if (pr < 0 && errno != EINTR) break;
+      int any = 0;
+      for (int p = 0; p < nport && pr > 0; p++) {
+        if (!(pfd[p].revents & POLLIN)) continue;
+        for (;;) { /* drain this port in recvmmsg batches */
+          if (!record && c.hn == c.cap_frames) break; /* batch full: flush first */
+          struct mmsghdr msg[RECV_BATCH];
+          struct iovec iov[RECV_BATCH];
+          struct sockaddr_in from[RECV_BATCH];
+          for (unsigned i = 0; i < RECV_BATCH; i++) {
+            iov[i].iov_base = rx + (size_t)i * B2P_DF_BYTES;
+            iov[i].iov_len = B2P_DF_BYTES;
+            memset(&msg[i], 0, sizeof msg[i]);
+            msg[i].msg_hdr.msg_iov = &iov[i];
+            msg[i].msg_hdr.msg_iovlen = 1;
+            msg[i].msg_hdr.msg_name = &from[i];
+            msg[i].msg_hdr.msg_namelen = sizeof from[i];
+          }
+          int r = recvmmsg(socks[p], msg, RECV_BATCH, MSG_DONTWAIT, NULL);
+          if (r <= 0) break;
+          any = 1;
+          for (int i = 0; i < r; i++) {
+            if (msg[i].msg_len != B2P_DF_BYTES || (msg[i].msg_hdr.msg_flags & MSG_TRUNC)) { /* not a data frame */
+              bad++;
+              continue;
+            }
+            const unsigned char *df = rx + (size_t)i * B2P_DF_BYTES;
+            b2p_df_hdr_t h;
+            b2p_df_decode(df, &h);
+            int chunk = by_freq ? (int)lround(h.freq - freq0)
+                                : b2p_df_chunk_from_ip((uint32_t)from[i].sin_addr.s_addr);
+            const unsigned char ck = (unsigned char)(chunk < 0 || chunk > 255 ? 255 : chunk);
+            got_all++;
+            if (record) {
+              if (fwrite(df, B2P_DF_BYTES, 1, fo) != 1 || fwrite(&ck, 1, 1, fco) != 1) goto done;
+              continue;
+            }
+            if (t_first == 0) t_first = now_s();
+            if (!c.have_ref) { /* the first frame fixes the reference (align_df role) */
+              c.ref = h;
+              c.have_ref = 1;
+              multilog(c.log, LOG_INFO, "reference: idf %" PRIu64 ", sec %" PRIu64, h.idf, h.sec);
+              if (open_block(&c) < 0) goto done;
+            }
+            const int64_t rel = b2p_df_index(&h, &c.ref);
+            if (rel > c.max_rel) c.max_rel = rel;
+            file_frame(&c, df, ck, rel);
+          }
+        }
+      }
+      const double t = now_s();
+      if (any) last_rx = t;
+      if (record) {
+        if (got_all && t - last_rx > idle_s) stop = 1;
+        continue;
+      }
+      if (!c.have_ref) {
+        if (t - last_rx > idle_s * 5) {
+          multilog(c.log, LOG_ERR, "no data frame in %.1f s", idle_s * 5);
+          goto done;
+        }
+        continue;
+      }
+      const int idle = t - last_rx > idle_s;
+      if (c.hn == c.cap_frames || (c.hn && !any)) /* a full batch, or the sockets ran dry */
+        if (flush_batch(&c) < 0) goto done;
+      /* the block is over once frames run TBUF_NDF past its end (the
+       * reference's forced switch, capture.c:510-524) or the stream stops */
+      while (c.blk && (c.max_rel >= (int64_t)(c.block_ndf + TBUF_NDF) || idle)) {
+        if (close_block(&c) < 0) goto done;
+        if (c.nblk_done >= c.nblk_max || (idle && !c.sn)) {
+          stop = 1;
+          break;
+        }
+        if (open_block(&c) < 0) goto done;
+        if (idle) { /* drain what the spill still holds, then stop */
+          if (flush_batch(&c) < 0) goto done;
+        }
+      }
+    }
+    free(rx);
+    const double el = now_s() - t_first;
+    multilog(c.log, LOG_INFO, "capture: %" PRIu64 " frames received (%" PRIu64 " not frames), %" PRIu64
+             " blocks, %" PRIu64 " frames placed, %" PRIu64 " behind their block, %" PRIu64
+             " past the spill, %.3f s from the first frame", got_all, bad, c.nblk_done, c.placed_all,
+             c.dropped_late, c.dropped_spill, record ? 0.0 : el);
+  }
+  status = EXIT_SUCCESS;
+
+done:
+  if (locked) dada_hdu_unlock_write(c.hdu);
+  if (c.hdu) dada_hdu_destroy(c.hdu);
+  if (c.ctx) {
+    if (c.d_frames) b2p_dev_free(c.ctx, c.d_frames);
+    if (c.d_chunks) b2p_dev_free(c.ctx, c.d_chunks);
+    if (c.d_cnt) b2p_dev_free(c.ctx, c.d_cnt);
+    if (c.hf) b2p_unregister_host(c.ctx, c.hf);
+    b2p_close(c.ctx);
+  }
+  for (int p = 0; p < nport; p++)
+    if (socks[p] >= 0) close(socks[p]);
+  if (fo) fclose(fo);
+  if (fco) fclose(fco);
+  free(c.hf);
+  free(c.hc);
+  free(c.sf);
+  free(c.sc);
+  multilog_close(c.log);
+  if (logf) fclose(logf);
+  return status;
+}

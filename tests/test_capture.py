@@ -1,0 +1,70 @@
+"""UDP capture on the loopback interface: paf_dfsend
+replays a paf_dfgen frame stream to several ports, paf_capture -o records
+what arrives (no GPU).  Every frame arrives once, unchanged, with the chunk
+the -m freq mapping gives."""
+import os
+import subprocess
+import time
+
+import numpy as np
+
+import b2p_oracle as npo
+from paf_b2p import dada
+
+BIN = dada.BIN_DIR
+
+
+def make_stream(tmp_path, nchunk=4, nblk=3, block_ndf=32, window=48, seed=3):
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=block_ndf * 128)
+    payload = npo.fill_synthetic(g, g.block_bytes * nblk, 7, 0, 0)
+    src = tmp_path / "in.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
+    subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(nchunk),
+                    "-c", str(ck), "-x", "249990", "-s", "54", "-f", "1300", "-r", str(seed),
+                    "-w", str(window)], check=True, capture_output=True)
+    return g, payload, df, ck
+
+
+def test_capture_records_every_frame(tmp_path):
+    g, _, df, ck = make_stream(tmp_path)
+    port = 21000 + (os.getpid() % 500) * 8
+    out, outc = tmp_path / "r.df", tmp_path / "r.chunks"
+    cap = subprocess.Popen([os.path.join(BIN, "paf_capture"), "-o", str(out), "-O", str(outc),
+                            "-P", str(port), "-N", "3", "-m", "freq:1300", "-t", "1"],
+                           stderr=subprocess.PIPE, text=True)
+    time.sleep(0.5)
+    snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck),
+                          "-P", str(port), "-N", "3", "-r", "100"], capture_output=True, text=True)
+    assert snd.returncode == 0, snd.stderr
+    _, err = cap.communicate(timeout=60)
+    assert cap.returncode == 0, err
+    sent = np.fromfile(df, np.uint8).reshape(-1, npo.DF_BYTES)
+    sent_ck = np.fromfile(ck, np.uint8)
+    got = np.fromfile(out, np.uint8).reshape(-1, npo.DF_BYTES)
+    got_ck = np.fromfile(outc, np.uint8)
+    assert got.shape == sent.shape, err
+    # arrival order across ports may differ: compare as sets of (frame, chunk)
+    key = lambda a, c: sorted(zip((r.tobytes() for r in a), c.tolist()))  # noqa: E731
+    assert key(got, got_ck) == key(sent, sent_ck)
+    assert f"capture: {sent.shape[0]} frames received (0 not frames)" in err
+
+
+def test_capture_flags_non_frames(tmp_path):
+    # datagrams of the wrong size are counted, not recorded
+    import socket
+    port = 23000 + (os.getpid() % 500) * 8
+    out, outc = tmp_path / "r.df", tmp_path / "r.chunks"
+    cap = subprocess.Popen([os.path.join(BIN, "paf_capture"), "-o", str(out), "-O", str(outc),
+                            "-P", str(port), "-N", "1", "-m", "freq:1300", "-t", "0.5"],
+                           stderr=subprocess.PIPE, text=True)
+    time.sleep(0.5)
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    for n in (100, 7232, 9000):
+        s.sendto(bytes(n), ("127.0.0.1", port))
+    s.close()
+    _, err = cap.communicate(timeout=60)
+    assert cap.returncode == 0, err
+    assert "capture: 1 frames received (2 not frames)" in err
+    assert os.path.getsize(out) == 7232
