@@ -42,7 +42,8 @@ def layouts(draw):
 
 
 @settings(max_examples=120, deadline=None, derandomize=True,
-          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
 @given(layouts())
 def test_random_layouts_match_oracle(gpu, case):
     g, cuts, seed = case
