@@ -306,6 +306,7 @@ int main(int argc, char **argv) {
     for (int p = 0; p < nport; p++) pfd[p] = (struct pollfd){socks[p], POLLIN, 0};
     uint64_t got_all = 0, bad = 0;
     double last_rx = now_s(), t_first = 0;
+    const double start_s = idle_s * 5 > 30 ? idle_s * 5 : 30; /* first frame within */
     int stop = 0;
     while (!stop) {
       int pr = poll(pfd, (nfds_t)nport, 20);
@@ -365,9 +366,9 @@ int main(int argc, char **argv) {
         if (got_all && t - last_rx > idle_s) stop = 1;
         continue;
       }
-      if (!c.have_ref) {
-        if (t - last_rx > idle_s * 5) {
-          multilog(c.log, LOG_ERR, "no data frame in %.1f s", idle_s * 5);
+      if (!got_all) { /* nothing yet: wait for the stream to start */
+        if (t - last_rx > start_s) {
+          multilog(c.log, LOG_ERR, "no data frame in %.1f s", start_s);
           goto done;
         }
         continue;
@@ -390,7 +391,7 @@ int main(int argc, char **argv) {
       }
     }
     free(rx);
-    const double el = now_s() - t_first;
+    const double el = t_first > 0 ? now_s() - t_first : 0.0;
     multilog(c.log, LOG_INFO, "capture: %" PRIu64 " frames received (%" PRIu64 " not frames), %" PRIu64
              " blocks, %" PRIu64 " frames placed, %" PRIu64 " behind their block, %" PRIu64
              " past the spill, %.3f s from the first frame", got_all, bad, c.nblk_done, c.placed_all,
