@@ -391,10 +391,10 @@ int main(int argc, char **argv) {
       }
     }
     free(rx);
-    const double el = t_first > 0 ? now_s() - t_first : 0.0;
+    const double el = t_first > 0 ? last_rx - t_first : 0.0;
     multilog(c.log, LOG_INFO, "capture: %" PRIu64 " frames received (%" PRIu64 " not frames), %" PRIu64
              " blocks, %" PRIu64 " frames placed, %" PRIu64 " behind their block, %" PRIu64
-             " past the spill, %.3f s from the first frame", got_all, bad, c.nblk_done, c.placed_all,
+             " past the spill, %.3f s from the first frame to the last", got_all, bad, c.nblk_done, c.placed_all,
              c.dropped_late, c.dropped_spill, record ? 0.0 : el);
   }
   status = EXIT_SUCCESS;

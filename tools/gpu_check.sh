@@ -68,6 +68,7 @@ for s in $STEPS; do
              run knob_$i 300 env $kv python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 2 &&
              run knob16_$i 300 env $kv python3 tools/perf_matrix.py --steps 20 --only "int16 LE 256ch" --npol-out 1 || exit $?
            done ;;
+    capture) run bench_capture 600 python3 tools/bench_capture.py ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
