@@ -79,23 +79,6 @@ typedef struct cap_t {
   multilog_t *log;
 } cap_t;
 
-/* file one received frame by its index relative to the current block */
-static void file_frame(cap_t *c, const unsigned char *df, unsigned char chunk, int64_t rel) {
-  if (rel < 0) {
-    c->dropped_late++; /* behind the block (capture.c:464-466) */
-  } else if (rel < (int64_t)c->block_ndf || !c->spill_cap) {
-    if (c->hn < c->cap_frames) {
-      memcpy(c->hf + c->hn * B2P_DF_BYTES, df, B2P_DF_BYTES);
-      c->hc[c->hn++] = chunk;
-    }
-  } else if (c->sn < c->spill_cap) {
-    memcpy(c->sf + c->sn * B2P_DF_BYTES, df, B2P_DF_BYTES);
-    c->sc[c->sn++] = chunk;
-  } else {
-    c->dropped_spill++; /* too far ahead: the reference forces a switch first */
-  }
-}
-
 /* upload the batch and scatter it into the current block */
 static int flush_batch(cap_t *c) {
   if (!c->hn) return 0;
@@ -106,6 +89,23 @@ static int flush_batch(cap_t *c) {
                               c->ref.sec, c->blk, c->block_ndf, (uint32_t)c->nchunk, c->d_cnt);
   c->hn = 0;
   return rc == B2P_OK ? 0 : -1;
+}
+
+/* file one received frame by its index relative to the current block */
+static int file_frame(cap_t *c, const unsigned char *df, unsigned char chunk, int64_t rel) {
+  if (rel < 0) {
+    c->dropped_late++; /* behind the block (capture.c:464-466) */
+  } else if (rel < (int64_t)c->block_ndf || !c->spill_cap) {
+    if (c->hn == c->cap_frames && flush_batch(c) < 0) return -1; /* a full batch goes first */
+    memcpy(c->hf + c->hn * B2P_DF_BYTES, df, B2P_DF_BYTES);
+    c->hc[c->hn++] = chunk;
+  } else if (c->sn < c->spill_cap) {
+    memcpy(c->sf + c->sn * B2P_DF_BYTES, df, B2P_DF_BYTES);
+    c->sc[c->sn++] = chunk;
+  } else {
+    c->dropped_spill++; /* too far ahead: the reference forces a switch first */
+  }
+  return 0;
 }
 
 static int open_block(cap_t *c) {
@@ -127,8 +127,8 @@ static int open_block(cap_t *c) {
     if (rel >= (int64_t)c->block_ndf) { /* still ahead: compact in place */
       memmove(c->sf + c->sn * B2P_DF_BYTES, df, B2P_DF_BYTES);
       c->sc[c->sn++] = c->sc[i];
-    } else {
-      file_frame(c, df, c->sc[i], rel);
+    } else if (file_frame(c, df, c->sc[i], rel) < 0) {
+      return -1;
     }
   }
   return 0;
@@ -315,7 +315,6 @@ int main(int argc, char **argv) {
       for (int p = 0; p < nport && pr > 0; p++) {
         if (!(pfd[p].revents & POLLIN)) continue;
         for (;;) { /* drain this port in recvmmsg batches */
-          if (!record && c.hn == c.cap_frames) break; /* batch full: flush first */
           struct mmsghdr msg[RECV_BATCH];
           struct iovec iov[RECV_BATCH];
           struct sockaddr_in from[RECV_BATCH];
@@ -356,7 +355,7 @@ int main(int argc, char **argv) {
             }
             const int64_t rel = b2p_df_index(&h, &c.ref);
             if (rel > c.max_rel) c.max_rel = rel;
-            file_frame(&c, df, ck, rel);
+            if (file_frame(&c, df, ck, rel) < 0) goto done;
           }
         }
       }

@@ -84,7 +84,9 @@ def main():
                               "loss_pct": round(100.0 * (sent - got) / sent, 3) if sent else None,
                               "capture_s": el,
                               "captured_GBps": round(got * 7232 / el / 1e9, 2) if el else None,
-                              "rc": [p.returncode for p in procs]}), flush=True)
+                              "rc": [p.returncode for p in procs],
+                              "capture_summary": cap.strip().splitlines()[-1][22:] if cap.strip() else ""}),
+                  flush=True)
         finally:
             for p in procs:
                 if p.poll() is None:
