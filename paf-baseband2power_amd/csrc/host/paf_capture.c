@@ -327,6 +327,7 @@ int main(int argc, char **argv) {
             msg[i].msg_hdr.msg_name = &from[i];
             msg[i].msg_hdr.msg_namelen = sizeof from[i];
           }
+          if (stop) break;
           int r = recvmmsg(socks[p], msg, RECV_BATCH, MSG_DONTWAIT, NULL);
           if (r <= 0) break;
           any = 1;
@@ -356,6 +357,17 @@ int main(int argc, char **argv) {
             const int64_t rel = b2p_df_index(&h, &c.ref);
             if (rel > c.max_rel) c.max_rel = rel;
             if (file_frame(&c, df, ck, rel) < 0) goto done;
+            /* forced switch as soon as a frame runs TBUF_NDF past the block
+             * (capture.c:510-524), before the spill can overflow */
+            while (c.blk && c.max_rel >= (int64_t)(c.block_ndf + TBUF_NDF)) {
+              if (close_block(&c) < 0) goto done;
+              if (c.nblk_done >= c.nblk_max) {
+                stop = 1;
+                break;
+              }
+              if (open_block(&c) < 0) goto done;
+            }
+            if (stop) break;
           }
         }
       }
