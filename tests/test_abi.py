@@ -110,3 +110,13 @@ def test_open_without_gpu_fails_cleanly(have_gpu):
     assert e.value.code == L.B2P_ENODEV
     with pytest.raises(paf_b2p.B2PError):
         paf_b2p.Integrator(paf_b2p.generic_geom(256), device=-1)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    # no CPU fallback: without libpafb2p.so every entry point raises
+    monkeypatch.setattr(L, "_lib", None)
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "absent" / "libpafb2p.so"))
+    with pytest.raises(ImportError, match="no CPU fallback"):
+        paf_b2p.Integrator(paf_b2p.bmf_geom())
+    with pytest.raises(ImportError):
+        L.lib()
