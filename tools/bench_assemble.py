@@ -120,7 +120,8 @@ def main():
                          "frac": round(moved / asm_s / 1e9 / HBM_PEAK_GBS, 4),
                          "algorithmic_bytes_per_launch": moved},
             "stream_to_spectrum_us": round(both_s * 1e6, 1),
-            "stream_to_spectrum_Msamples_s": round(a.ndf * 128 * it.nout / both_s / 1e6, 1),
+            # channels x pols x time, as bench.py counts samples
+            "stream_to_spectrum_Msamples_s": round(a.ndf * 128 * it.nout * 2 / both_s / 1e6, 1),
             "host_stream_build_s": round(prep, 1),
             "variant": os.environ.get("B2P_ASM_VARIANT", "0"),
             "grid": os.environ.get("B2P_ASM_GRID", "default"),
