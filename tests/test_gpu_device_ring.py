@@ -79,8 +79,8 @@ def test_device_ring_bytes_cross_processes(gpu, tmp_path):
 def test_pipeline_with_device_input_ring(gpu, tmp_path):
     from test_gpu_pipeline import spectra, write_conf
     g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=64 * 128)
-    nblk = 3
-    payload = co.fill_synthetic(g, g.block_bytes * nblk, SEED, 0, 11)
+    nblk = 3  # three whole integrations, then a partial one the consumer must skip
+    payload = co.fill_synthetic(g, g.block_bytes * nblk + g.block_bytes // 2, SEED, 0, 11)
     src = tmp_path / "bmf.dada"
     dada.write_dada_file(str(src), "NBIT 16\n", payload)
     conf = tmp_path / "p.conf"
@@ -94,7 +94,8 @@ def test_pipeline_with_device_input_ring(gpu, tmp_path):
         blk = payload[i * g.block_bytes:(i + 1) * g.block_bytes]
         assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk, nthreads=8).view(np.uint32))
     log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
-    assert "GPU-resident" in log and "FINISH PAF_PROCESS: 3 integrations" in log
+    assert "GPU-resident" in log and "two blocks in flight" in log
+    assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log
 
 
 def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz, device=0):
