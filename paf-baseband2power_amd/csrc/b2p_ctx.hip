@@ -274,8 +274,6 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   return B2P_OK;
 }
 
-static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out);
-
 int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   if (!out || !g) return set_err(nullptr, B2P_EINVAL, "null argument");
   *out = nullptr;
@@ -349,10 +347,9 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
     return fail(set_err(c, B2P_EHIP, "zero replicas"));
   // load the code object now: a process's first kernel launch costs tens of
   // ms (40 ms measured in paf_baseband2power), which belongs to start-up,
-  // not to the first integration.  An empty span runs the chosen kernel on
-  // no rows and adds nothing.
-  if ((rc = enqueue_span(c, c->d_rep, 0, nullptr)) != B2P_OK) return fail(rc);
-  if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(set_err(c, B2P_EHIP, "warm-up launch"));
+  // not to the first integration
+  if (launch_warm(c->stream) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+    return fail(set_err(c, B2P_EHIP, "warm-up launch"));
 
   *out = c;
   return B2P_OK;

@@ -97,6 +97,7 @@ struct AssembleArgs {
 };
 hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s);
 hipError_t launch_convert(const ConvertArgs &a, hipStream_t s);
+hipError_t launch_warm(hipStream_t s);
 hipError_t launch_sum_rows(const SumRowsArgs &a, hipStream_t s);
 
 // which instantiation of the integrate kernel runs
