@@ -150,3 +150,21 @@ def test_dfgen_shuffled_lossy_stream_reassembles(tmp_path):
         gidf = int(h["idf"][0]) + (int(h["sec"][0]) - 27) // 27 * 250000 - 249996
         hit[gidf * nchunk + chunk[i]] = True
     assert np.array_equal(got[hit], src[hit]) and not got[~hit].any()
+
+
+def test_single_field_decoders_match_reference_hdr_c():
+    # hdr_idf / hdr_sec / hdr_freq (hdr.c:30-55) against our full decode, on
+    # random headers -- live, when oracle/_ref holds the reference's hdr.c
+    L = co.ref_hdr_lib()
+    if L is None:
+        pytest.skip("oracle/_ref/libhdr_ref.so not built (no /root/reference here)")
+    import ctypes as C
+    L.hdr_idf.argtypes = L.hdr_sec.argtypes = L.hdr_freq.argtypes = [C.c_void_p]
+    L.hdr_idf.restype = L.hdr_sec.restype = C.c_uint64
+    L.hdr_freq.restype = C.c_double
+    rng = np.random.default_rng(11)
+    for _ in range(500):
+        raw = rng.integers(0, 256, 64, dtype=np.uint8)
+        h = dada.df_decode(raw.tobytes())
+        p = raw.ctypes.data
+        assert (L.hdr_idf(p), L.hdr_sec(p), L.hdr_freq(p)) == (h.idf, h.sec, h.freq)
