@@ -67,7 +67,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
     -t N, SURVEY.md 8e second mode)."""
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
-                             timeout, hfname)
+                             timeout, hfname, device_ring)
     c = read_conf(conf_path)
     hdr = hfname or c["diskdb_hfname"]
     if not os.path.isabs(hdr):
@@ -165,7 +165,7 @@ def _wait_all(procs, timeout):
 
 
 def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, mean, timeout,
-                  hfname):
+                  hfname, device_ring=False):
     c = read_conf(conf_path)
     hdr = _resolve_header(c, conf_path, hfname)
     os.makedirs(directory, exist_ok=True)
@@ -178,7 +178,8 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
         for r in range(nsub):
             kin = c["diskdb_key"] + 0x10 * r
             dada.destroy_ring(kin)
-            dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"])
+            dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"],
+                             device=(gpu + r) if device_ring else -1)
             keys.append(kin)
         out = os.path.join(directory, "power.dada")
         procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],

@@ -164,3 +164,34 @@ def test_replay_reuses_blocks(gpu, tmp_path, device):
     want = [co.power(g, co.fill_synthetic(g, g.block_bytes, SEED, 0, i)) for i in range(nbufs)]
     for i in range(nrep):
         assert np.array_equal(sp[i].view(np.uint32), want[i % nbufs].view(np.uint32))
+
+
+def test_gathered_subbands_on_device_rings(gpu, tmp_path):
+    # paf_baseband2power -n 2 with both input rings GPU-resident (one GPU on
+    # the test box: both rings and both contexts on device 0, peer-copy gather)
+    from test_gpu_pipeline import write_conf
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 14)
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\nTSAMP 0.84375\n")
+    files, payloads = [], []
+    for r in range(2):
+        p = co.fill_synthetic(g, g.block_bytes * 2, SEED, r, 4)
+        f = tmp_path / f"sb{r}.dada"
+        dada.write_dada_file(str(f), "x 1\n", p)
+        files.append(str(f))
+        payloads.append(p)
+    kin, kout = fresh_key(), fresh_key()
+    dada.destroy_ring(kin + 0x10)
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 14, 1, 1024, 256, kin, kout, str(hfile))
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, files, nsub=2, gather=True,
+                        device_ring=True, timeout=600)
+    _, data = dada.read_dada_file(outs[0])
+    sp = data.view(np.float32).reshape(-1, 2, 256)
+    assert sp.shape[0] == 2
+    for i in range(2):
+        for r in range(2):
+            blk = payloads[r][i * g.block_bytes:(i + 1) * g.block_bytes]
+            assert np.array_equal(sp[i, r].view(np.uint32), co.power(g, blk).view(np.uint32))
+    log = open(str(tmp_path / "out" / "paf_baseband2power.log")).read()
+    assert log.count("GPU-resident (device 0)") == 2
