@@ -53,6 +53,15 @@ def _bin(name: str) -> str:
     return os.path.join(dada.BIN_DIR, name)
 
 
+def _ring_device(gpu: int, r: int) -> int:
+    """GPU of sub-band r's input ring: the same (d + r) mod visible-devices
+    rule paf_baseband2power applies to its contexts (paf_baseband2power.cu:
+    89-90 picks 0 with one GPU).  torch counts devices without starting HIP."""
+    import torch
+    n = torch.cuda.device_count()
+    return (gpu + r) % n if n > 0 else gpu + r
+
+
 def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
@@ -86,7 +95,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
             dada.destroy_ring(kin)
             dada.destroy_ring(kout)
             dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"],
-                             device=(gpu + r) if device_ring else -1)
+                             device=_ring_device(gpu, r) if device_ring else -1)
             keys.append(kin)
             obytes = c["b2p_rbufsz"] * npol_out
             dada.create_ring(kout, c["b2p_nbuf"], obytes, c["b2p_nreader"])
@@ -179,7 +188,7 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
             kin = c["diskdb_key"] + 0x10 * r
             dada.destroy_ring(kin)
             dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"],
-                             device=(gpu + r) if device_ring else -1)
+                             device=_ring_device(gpu, r) if device_ring else -1)
             keys.append(kin)
         out = os.path.join(directory, "power.dada")
         procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
