@@ -2,7 +2,10 @@
 # One GPU-box session: smoke -> gpu tests -> bench -> rocprofv3 kernel trace.
 # Each GPU step has its own time limit; a fault/abort/timeout (exit other
 # than 0 or 1) ends the script at once -- nothing further touches the GPU.
-#   usage: tools/gpu_check.sh [steps...]   steps: smoke tests bench prof pmc
+#   usage: tools/gpu_check.sh [steps...]
+#   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 benchsplit
+#          prof pmc profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
+#          probe skew tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
