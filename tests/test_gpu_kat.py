@@ -57,3 +57,15 @@ def test_int8_lane_order_and_extremes(gpu):
     buf = w.view(np.uint8).reshape(-1)
     want = np.tile(np.array([25.0, 32768.0]) * g.nsamp_int, 256).astype(np.float32)
     assert same_bits(gpu_power(g, buf), want)
+
+
+@pytest.mark.parametrize("nbit,be", [(8, 0), (16, 1)])
+def test_largest_output_count(gpu, nbit, be):
+    # nout = 8192 (the ABI's limit, 64 KiB of LDS sums): 64 chunks x 64
+    # channels x 2 output pols, against the oracle
+    g = npo.Geom(nbit=nbit, big_endian=be, nchunk=64, nsamp_df=4, nchan_chunk=64, npol_out=2,
+                 nsamp_int=4 * 24)
+    assert g.nout == 8192
+    import oracle_c as co
+    buf = co.fill_synthetic(g, g.block_bytes, 99, 1, 2)
+    assert same_bits(gpu_power(g, buf), co.power(g, buf, nthreads=8))
