@@ -5,7 +5,7 @@
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 benchsplit
 #          prof pmc profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
-#          probe skew tune tunebmf
+#          probe skew overlap tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -74,6 +74,7 @@ for s in $STEPS; do
     capture) run bench_capture 600 python3 tools/bench_capture.py ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
+    overlap) run overlap_probe 300 paf-baseband2power_amd/bin/overlap_probe 40 ;;
     tune) run tune_c2 600 python3 tools/tune.py --config c2 &&
           run tune_c5 600 python3 tools/tune.py --config c5 --quick &&
           run tune_bmf 600 python3 tools/tune.py --config bmf --quick ;;
