@@ -9,6 +9,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+import numpy as np
+
 from ._lib import PKG_DIR
 
 DADA_LIB = os.path.join(PKG_DIR, "lib", "libpafdada.so")
@@ -204,6 +206,22 @@ class Hdu:
             raise OSError("copy out of block")
         L.ipcio_close_block_read(self.data, n.value)
         return buf.raw
+
+    def view_block(self):
+        """zero-copy uint8 view of the next block of a HOST ring, or None at
+        end of data; valid until release_block(len(view))"""
+        L = dlib()
+        n, bid = C.c_uint64(), C.c_uint64()
+        p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
+        if not p:
+            return None
+        if not n.value:
+            return np.empty(0, dtype=np.uint8)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n.value,))
+
+    def release_block(self, nbytes: int) -> None:
+        if dlib().ipcio_close_block_read(self.data, nbytes) != 0:
+            raise OSError("close_block_read")
 
     def set_read_depth(self, depth: int) -> None:
         """hold up to `depth` blocks at once (extension, include/b2p_dada.h)"""

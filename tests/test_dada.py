@@ -122,6 +122,30 @@ def test_ring_roundtrip_and_short_block_eod(ring):
     assert got[1:] == blocks
 
 
+def test_ring_zero_copy_view(ring):
+    """view_block / release_block: the reader sees each block in place"""
+    k = ring(2, 4096)
+    blocks = [bytes([i]) * 4096 for i in range(5)] + [b"y" * 10]
+    got = []
+
+    def reader():
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            while (v := r.view_block()) is not None:
+                got.append(v.tobytes())
+                r.release_block(len(v))
+
+    t = threading.Thread(target=reader)
+    t.start()
+    with dada.Hdu(k, "W") as w:
+        w.write_header(TEMPLATE)
+        for b in blocks:
+            w.write_block(b)
+    t.join(30)
+    assert not t.is_alive()
+    assert got == blocks
+
+
 def test_ring_full_last_block_then_empty_eod(ring):
     k = ring(2, 1024)
     out = []
