@@ -83,11 +83,16 @@ int main(int argc, char **argv) {
   std::vector<unsigned long long> h((size_t)2 * 2 * ncu * K);
 
   struct V { int nstreams; unsigned lds_kib; int grid_mul; };
-  const V vars[] = {{1, 0, 1}, {1, 96, 1}, {2, 0, 1}, {2, 96, 1}, {3, 96, 1}, {2, 64, 1},
-                    {1, 0, 2}, {2, 96, 2}};
+  const V all_vars[] = {{1, 0, 1}, {1, 96, 1}, {2, 0, 1}, {2, 96, 1}, {3, 96, 1}, {2, 64, 1},
+                        {1, 0, 2}, {2, 96, 2}};
+  // "dist": one stream only, plus the distribution of per-launch spans
+  const bool dist = argc > 2 && argv[2][0] == 'd';
+  const int nvars = dist ? 1 : (int)(sizeof all_vars / sizeof all_vars[0]);
+  const V *vars = all_vars;
   printf("{\"cu\": %d, \"launches\": %d, \"bytes_per_launch\": %zu, \"results\": [\n", ncu, K, bytes);
   for (int rep = 0; rep < 3; ++rep)
-    for (const V &v : vars) {
+    for (int vi = 0; vi < nvars; ++vi) {
+      const V &v = vars[vi];
       const int grid = ncu * v.grid_mul;
       const size_t lds = (size_t)v.lds_kib * 1024 + 16;
       // warm
@@ -118,6 +123,7 @@ int main(int argc, char **argv) {
         }
         ov += ((double)end_k - (double)start_n) / 100.0;
       }
+      std::vector<double> spans;
       for (int k = 0; k < K; ++k) {
         unsigned long long s0 = ~0ull, e0 = 0;
         for (int i = 0; i < grid; ++i) {
@@ -125,6 +131,16 @@ int main(int argc, char **argv) {
           e0 = std::max(e0, h[(size_t)2 * grid * k + 2 * i + 1]);
         }
         span += (e0 - s0) / 100.0;
+        spans.push_back((e0 - s0) / 100.0);
+      }
+      if (dist) {
+        std::vector<double> so = spans;
+        std::sort(so.begin(), so.end());
+        printf(" {\"span_us_min\": %.2f, \"p10\": %.2f, \"median\": %.2f, \"p90\": %.2f, \"max\": %.2f, "
+               "\"over_153\": %d, \"spans\": [", so[0], so[K / 10], so[K / 2], so[K * 9 / 10], so[K - 1],
+               (int)std::count_if(so.begin(), so.end(), [](double x) { return x > 153.0; }));
+        for (int k = 0; k < K; ++k) printf("%s%.1f", k ? ", " : "", spans[k]);
+        printf("]},\n");
       }
       printf(" {\"streams\": %d, \"lds_kib\": %u, \"grid\": %d, \"rep\": %d, \"us_per_launch\": %.2f, "
              "\"GBps\": %.1f, \"launch_span_us\": %.2f, \"overlap_us\": %.2f},\n",
