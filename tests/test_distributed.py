@@ -50,7 +50,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 8])
 def test_gloo_gather_and_max(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
