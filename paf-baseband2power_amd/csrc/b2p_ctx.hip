@@ -448,11 +448,11 @@ static hipEvent_t pool_event(b2p_ctx_t *c) {
   return e;
 }
 
-// Enqueue one integrate launch over a device span (frame-aligned).  With
 static size_t pend_bytes(const b2p_ctx_t *c) {
   return (size_t)c->nout * (c->pend.raw ? sizeof(unsigned long long) : sizeof(float));
 }
 
+// Enqueue one integrate launch over a device span (frame-aligned).  With
 // fused_out set, the launch also emits the integration (last workgroup).
 static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out) {
   IntegrateArgs a;
