@@ -159,6 +159,13 @@ def main():
     # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
     it = paf_b2p.Integrator(geom, device=D.device_of(local))
     nout, bb = it.nout, it.block_bytes
+    if rccl:
+        # one stream for the integrator and torch: the collective after the
+        # loop is stream-ordered behind the last finalize, with no host wait
+        # in between (b2p_set_stream; torch's NCCL work waits on this stream)
+        ts = torch.cuda.Stream()
+        torch.cuda.set_stream(ts)
+        it.set_stream(ts.cuda_stream)
 
     if split:
         # exact partial sums, K x nout uint64 (as int64 for torch), reduced
@@ -168,7 +175,7 @@ def main():
         out_ptr = sums_t.data_ptr()
     elif rccl:
         # finalize writes the K spectra straight into torch device memory;
-        # the gather runs after one it.sync() at the end of the timed loop
+        # the gather follows the last finalize on the shared stream
         out_t = torch.zeros((a.steps, nout), dtype=torch.float32, device="cuda")
         out_ptr = out_t.data_ptr()
     else:
@@ -231,11 +238,11 @@ def main():
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(a.warmup + k, k)
-    it.set_timing(0)  # records the closing event right behind the last launch
-    it.sync()
+    it.set_timing(0)  # records the closing event right behind the last launch (no wait)
+    if not rccl:
+        it.sync()
     if split:
         if dist_on:
-            torch.cuda.synchronize()
             if rccl:
                 total = D.reduce_sums(sums_t)  # RCCL reduce (SUM) of K x nout partials
             else:  # gloo rehearsal: partials through host memory

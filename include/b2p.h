@@ -215,7 +215,8 @@ int b2p_group_close(b2p_group_t *grp);
  *   between set_timing(ctx, 2) and set_timing(ctx, 0); kernel_ms is the
  *   region's elapsed time (inter-launch gaps and finalizes included), i.e.
  *   an upper bound of the summed launch durations, with no per-launch cost.
- * mode 0: off (closes a mode-2 region). */
+ * mode 0: off.  Closing a mode-2 region records its end event and returns
+ *   without waiting; b2p_get_stats waits for it and adds the region. */
 int b2p_set_timing(b2p_ctx_t *ctx, int mode);
 int b2p_get_stats(b2p_ctx_t *ctx, b2p_stats_t *stats); /* synchronises */
 int b2p_reset_stats(b2p_ctx_t *ctx);

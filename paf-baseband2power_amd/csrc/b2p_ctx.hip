@@ -77,6 +77,7 @@ struct b2p_ctx {
   int timing = 0;
   hipEvent_t region_a = nullptr, region_b = nullptr;
   uint64_t region_launches = 0, region_bytes = 0, region_finalizes = 0;
+  int region_closed = 0;  // closing event recorded, not read yet (read by drain_timing)
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> ev_pool;
   b2p_stats_t stats{};
@@ -356,6 +357,18 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
 }
 
 static void drain_timing(b2p_ctx_t *c) {
+  if (c->region_closed) {  // a closed mode-2 region: its elapsed time
+    float ms = 0.f;
+    if (hipEventSynchronize(c->region_b) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->region_a, c->region_b) == hipSuccess) {
+      c->stats.launches += c->region_launches;
+      c->stats.bytes += c->region_bytes;
+      c->stats.finalizes += c->region_finalizes;
+      c->stats.kernel_ms += ms;  // the whole region, gaps and finalizes included
+    }
+    c->region_launches = c->region_bytes = c->region_finalizes = 0;
+    c->region_closed = 0;
+  }
   for (auto &p : c->pending) {
     float ms = 0.f;
     if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
@@ -722,17 +735,13 @@ int b2p_set_timing(b2p_ctx_t *c, int mode) {
   if (c->timing == 2 && mode != 2) {  // close the region, last finalize included
     int rc = flush_pending(c);
     if (rc != B2P_OK) return rc;
+    // no host wait: work enqueued next (a collective) follows the region on
+    // the stream at once; b2p_get_stats reads the time
     CK(c, hipEventRecord(c->region_b, c->stream));
-    CK(c, hipEventSynchronize(c->region_b));
-    float ms = 0.f;
-    CK(c, hipEventElapsedTime(&ms, c->region_a, c->region_b));
-    c->stats.launches += c->region_launches;
-    c->stats.bytes += c->region_bytes;
-    c->stats.finalizes += c->region_finalizes;
-    c->stats.kernel_ms += ms;  // the whole region, gaps and finalizes included
-    c->region_launches = c->region_bytes = c->region_finalizes = 0;
+    c->region_closed = 1;
   }
   if (mode == 2 && c->timing != 2) {  // open a region
+    drain_timing(c);  // an earlier region still unread
     if (!c->region_a) CK(c, hipEventCreate(&c->region_a));
     if (!c->region_b) CK(c, hipEventCreate(&c->region_b));
     CK(c, hipEventRecord(c->region_a, c->stream));

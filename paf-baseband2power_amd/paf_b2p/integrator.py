@@ -66,8 +66,9 @@ class Integrator:
     # ---- hot path ------------------------------------------------------------
     def push(self, buf, nbytes: int | None = None, is_device: bool | None = None) -> None:
         """Accumulate a whole number of frames.  ``buf``: numpy uint8 array
-        (host), ``DeviceBuffer`` / ``(DeviceBuffer, offset, nbytes)`` (device),
-        or a raw pointer int with ``nbytes`` and ``is_device``."""
+        (host), ``DeviceBuffer`` / ``(DeviceBuffer, offset, nbytes)`` /
+        ``(device pointer, nbytes)`` (device), or a raw pointer int with
+        ``nbytes`` and ``is_device``."""
         ptr, n, dev = self._span(buf, nbytes, is_device)
         L.check(L.lib().b2p_push(self._ctx, C.c_void_p(ptr), n, int(dev)), self._ctx)
 
@@ -197,6 +198,8 @@ class Integrator:
     def _span(self, buf, nbytes, is_device):
         if isinstance(buf, DeviceBuffer):
             return buf.ptr, buf.nbytes if nbytes is None else nbytes, True
+        if isinstance(buf, tuple) and len(buf) == 2 and isinstance(buf[0], int):
+            return buf[0], buf[1], True  # (device pointer, nbytes), e.g. a torch tensor's
         if isinstance(buf, tuple):
             d, off, n = buf
             return d.ptr + off, n, True

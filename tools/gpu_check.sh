@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit; a fault/abort/timeout (exit other
 # than 0 or 1) ends the script at once -- nothing further touches the GPU.
 #   usage: tools/gpu_check.sh [steps...]
-#   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 benchsplit
+#   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 distcost benchsplit
 #          prof pmc profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns diskdb tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
@@ -42,6 +42,12 @@ for s in $STEPS; do
     benchdist1) run bench_dist1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist ;;
+    distcost) for r in 1 2; do
+                run dc_plain_r$r 300 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 &&
+                run dc_dist_r$r 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                  --master-addr 127.0.0.1 --master-port $((29520 + r)) bench.py --steps 50 --warmup 5 \
+                  --cpu-seconds 0 --force-dist || exit $?
+              done ;;
     benchsplit) run bench_split1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29513 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist --split time &&
