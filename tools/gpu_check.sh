@@ -5,7 +5,7 @@
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 distcost benchsplit
 #          prof pmc profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
-#          probe skew overlap spikes patterns diskdb tune tunebmf
+#          probe skew overlap spikes patterns h2d diskdb tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -80,6 +80,7 @@ for s in $STEPS; do
     spikes) run overlap_dist 300 paf-baseband2power_amd/bin/overlap_probe 200 dist &&
             run prof_spikes 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_spikes" -o run \
               -- python3 bench.py --steps 200 --warmup 5 --cpu-seconds 0 ;;
+    h2d) run h2d_probe 300 paf-baseband2power_amd/bin/h2d_probe ;;
     patterns) run read_patterns 300 paf-baseband2power_amd/bin/read_pattern_probe 40 ;;
     diskdb) run bench_diskdb 600 python3 tools/bench_diskdb.py --nint 8 --threads 16 ;;
     capture) run bench_capture 600 python3 tools/bench_capture.py ;;
