@@ -70,6 +70,26 @@ for s in $STEPS; do
          run pmc_write_asm 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm ;;
     matrix) run perf_matrix 600 python3 tools/perf_matrix.py --steps 20 ;;
+    idlerep) run idle_rep0 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
+             run idle_rep3 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 \
+               --sleep 3 &&
+             run idle_rep0b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 ;;
+    keeprep) run keep_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep &&
+             run free_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
+             run keep_rep_b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep ;;
+    idlerep) run idle_rep0 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
+             run idle_rep3 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 \
+               --sleep 3 &&
+             run idle_rep0b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 ;;
+    keeprep) run keep_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep &&
+             run free_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
+             run keep_rep_b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep ;;
+    allocrep) run alloc_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
+              run alloc_rep5 300 python3 tools/perf_matrix.py --steps 10 --only "int8 1024ch" --npol-out 1 --repeat 3 &&
+              run alloc_rep_contig 300 env B2P_ALLOC_CONTIG=1 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" \
+                --npol-out 1 --repeat 4 &&
+              run alloc_rep5_contig 300 env B2P_ALLOC_CONTIG=1 python3 tools/perf_matrix.py --steps 10 \
+                --only "int8 1024ch" --npol-out 1 --repeat 3 ;;
     knobs) i=0
            for kv in "B2P_UNROLL=8" "B2P_UNROLL=16" "B2P_MAX_THREADS=448" "B2P_MAX_THREADS=256" \
                      "B2P_INTERLEAVE=1" "B2P_INTERLEAVE=0" "B2P_WG_PER_CU=2" "B2P_NT=0"; do

@@ -12,6 +12,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                 "paf-baseband2power_amd"))
@@ -33,7 +34,10 @@ CASES = [
 ]
 
 
-def run(name, geom, steps):
+KEEP = []  # --keep: buffers are never freed (diagnostic: no hipFree between runs)
+
+
+def run(name, geom, steps, keep=False):
     it = paf_b2p.Integrator(geom)
     bb = it.block_bytes
     blocks = []
@@ -56,6 +60,9 @@ def run(name, geom, steps):
     res = {"case": name, "npol_out": geom.npol_out, "bytes": bb, "us_per_integration": round(us, 1),
            "GBps": round(bb / us / 1e3, 1), "threads": it.info.threads, "unroll": it.info.unroll,
            "row_groups": it.info.row_groups, "columns": it.info.columns}
+    if keep:
+        KEEP.append((it, blocks, out))
+        return res
     for d in blocks + [out]:
         d.free()
     it.close()
@@ -67,16 +74,26 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", default="", help="substring of the case names to run")
     ap.add_argument("--npol-out", type=int, default=0, help="1 or 2 (default both)")
+    ap.add_argument("--repeat", type=int, default=1, help="run each case this many times")
+    ap.add_argument("--sleep", type=float, default=2.0,
+                    help="idle seconds before each run: the previous run freed GiBs, and launches "
+                         "in the next seconds run 2-8 %% slower (profiles/r01_free_effect.txt)")
+    ap.add_argument("--keep", action="store_true", help="never free a run's buffers")
     a = ap.parse_args()
     knobs = {k: v for k, v in os.environ.items() if k.startswith("B2P_")}
     for name, mk in CASES:
         if a.only and a.only not in name:
             continue
         for npo in ((a.npol_out,) if a.npol_out else (1, 2)):
-            r = run(name, mk(npol_out=npo), a.steps)
-            if knobs:
-                r["env"] = knobs
-            print(json.dumps(r), flush=True)
+            for rep in range(a.repeat):
+                if a.sleep > 0:
+                    time.sleep(a.sleep)
+                r = run(name, mk(npol_out=npo), a.steps, a.keep)
+                if knobs:
+                    r["env"] = knobs
+                if a.repeat > 1:
+                    r["rep"] = rep
+                print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
