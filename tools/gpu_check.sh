@@ -5,7 +5,7 @@
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 distcost benchsplit
 #          prof pmc profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
-#          probe skew overlap spikes patterns h2d diskdb tune tunebmf
+#          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -77,19 +77,6 @@ for s in $STEPS; do
     keeprep) run keep_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep &&
              run free_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
              run keep_rep_b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep ;;
-    idlerep) run idle_rep0 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
-             run idle_rep3 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 \
-               --sleep 3 &&
-             run idle_rep0b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 ;;
-    keeprep) run keep_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep &&
-             run free_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
-             run keep_rep_b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep ;;
-    allocrep) run alloc_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
-              run alloc_rep5 300 python3 tools/perf_matrix.py --steps 10 --only "int8 1024ch" --npol-out 1 --repeat 3 &&
-              run alloc_rep_contig 300 env B2P_ALLOC_CONTIG=1 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" \
-                --npol-out 1 --repeat 4 &&
-              run alloc_rep5_contig 300 env B2P_ALLOC_CONTIG=1 python3 tools/perf_matrix.py --steps 10 \
-                --only "int8 1024ch" --npol-out 1 --repeat 3 ;;
     knobs) i=0
            for kv in "B2P_UNROLL=8" "B2P_UNROLL=16" "B2P_MAX_THREADS=448" "B2P_MAX_THREADS=256" \
                      "B2P_INTERLEAVE=1" "B2P_INTERLEAVE=0" "B2P_WG_PER_CU=2" "B2P_NT=0"; do
