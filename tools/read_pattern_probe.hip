@@ -10,6 +10,7 @@
 //   wave       each wave owns a contiguous 1/(8G): 8x more, shorter streams
 //   lane64     slice, but a lane reads 64 contiguous bytes (4 loads) of a
 //              32-KiB row instead of 16 B of 4 rows
+// Also copy variants (read + write, the bound of b2p_assemble).
 // Prints GB/s per variant and repetition as JSON.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -75,6 +76,30 @@ __global__ void __launch_bounds__(512) read_kernel(const u32x4 *data, unsigned l
   if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// copy variants (the bound of b2p_assemble): MODE 0 slice (a workgroup
+// copies a contiguous 1/G in 8-KiB rows, U in flight), 1 sweep (row r of
+// every workgroup is r*G + g: the whole grid moves front to back together)
+template <int MODE, int U>
+__global__ void __launch_bounds__(512) copy_kernel(const u32x4 *src, u32x4 *dst, unsigned long long nvec) {
+  const unsigned t = threadIdx.x, S = 512;
+  const unsigned long long rows = nvec / S, G = gridDim.x, g = blockIdx.x;
+  unsigned long long r0, r1, step;
+  if (MODE == 0) {
+    r0 = g * rows / G, r1 = (g + 1) * rows / G, step = 1;
+  } else {
+    r0 = g, r1 = rows, step = G;
+  }
+  unsigned long long r = r0;
+  for (; r + (U - 1) * step < r1; r += U * step) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + (r + u * step) * S + t);
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(v[u], dst + (r + u * step) * S + t);
+  }
+  for (; r < r1; r += step) __builtin_nontemporal_store(__builtin_nontemporal_load(src + r * S + t), dst + r * S + t);
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -114,6 +139,26 @@ int main(int argc, char **argv) {
       CK(hipEventElapsedTime(&ms, a, b));
       printf(" {\"variant\": \"%s\", \"rep\": %d, \"us_per_launch\": %.2f, \"GBps\": %.1f},\n", v.name, rep,
              ms * 1e3 / K, (double)bytes * K / (ms * 1e-3) / 1e9);
+      fflush(stdout);
+    }
+  // copies: 1 GiB -> 1 GiB over rotating buffer pairs, grid = 1 or 2 per CU
+  struct CV { const char *name; void (*f)(const u32x4 *, u32x4 *, unsigned long long); int per_cu; };
+  const CV cvars[] = {{"copy_slice_u4", copy_kernel<0, 4>, 1}, {"copy_slice_u2", copy_kernel<0, 2>, 1},
+                      {"copy_slice_u4_x2", copy_kernel<0, 4>, 2}, {"copy_sweep_u4", copy_kernel<1, 4>, 1},
+                      {"copy_sweep_u2_x2", copy_kernel<1, 2>, 2}};
+  for (int rep = 0; rep < 3; ++rep)
+    for (const CV &v : cvars) {
+      const int grid = ncu * v.per_cu;
+      for (int k = 0; k < 4; ++k) hipLaunchKernelGGL(v.f, grid, 512, 0, 0, bufs[k % 4], bufs[(k + 1) % 4], nvec);
+      CK(hipStreamSynchronize(0));
+      CK(hipEventRecord(a, 0));
+      for (int k = 0; k < K; ++k) hipLaunchKernelGGL(v.f, grid, 512, 0, 0, bufs[k % 4], bufs[(k + 2) % 4], nvec);
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      printf(" {\"variant\": \"%s\", \"rep\": %d, \"us_per_launch\": %.2f, \"GBps_read_plus_write\": %.1f},\n",
+             v.name, rep, ms * 1e3 / K, 2.0 * bytes * K / (ms * 1e-3) / 1e9);
       fflush(stdout);
     }
   printf(" {}]}\n");
