@@ -4,7 +4,7 @@
 # than 0 or 1) ends the script at once -- nothing further touches the GPU.
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 distcost benchsplit
-#          prof pmc profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
+#          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
@@ -104,6 +104,12 @@ for s in $STEPS; do
             -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
             -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
+    pmc5) run pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run \
+            -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 &&
+         run pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run \
+            -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 &&
+         run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run \
+            -- python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
     profbmf) run prof_bmf 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bmf" -o run \
             -- python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
     pmcbmf) run pmc_fetch_bmf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_bmf" -o run \
