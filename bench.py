@@ -3,21 +3,40 @@
 
 One "step" = one full 1024x1024-sample integration (README.md:2) of one
 sub-band per GPU: the HBM-resident block is unpacked, detected and
-time-integrated by the gfx950 kernel and the fp32 spectrum is emitted
-(finalize kernel).  Default workload = BASELINE.json configs[1]: 256 chans
-x 2 pols int8 (1 GiB per integration).  Inputs are synthetic (counter-based
-generator) and rotate over 4 distinct 1-GiB blocks per GPU so the
-256 MiB Infinity Cache cannot serve repeats.
+time-integrated by the gfx950 kernel and the fp32 spectrum is emitted.
+Default workload = BASELINE.json configs[1]: 256 chans x 2 pols int8 (1 GiB
+per integration).  Inputs are synthetic (counter-based generator)
+and rotate over 4 distinct blocks per GPU so the 256 MiB Infinity Cache
+cannot serve repeats.
 
-Multi-GPU (torchrun, one process per GPU): sub-band r on GPU r, no data-path
-collective; the K spectra of every rank are gathered to rank 0 over RCCL
-(torch.distributed "nccl") inside the timed region (configs[3]/[4]).
-value = all ranks' samples / max-over-ranks time  (weak scaling).
---split time instead cuts ONE sub-band's integration along time across the
-ranks (second mode): each rank integrates its share, emits
-exact uint64 partials, and one RCCL reduce (SUM) of the K x nout partials
-brings them to rank 0, which rounds once to fp32 (strong scaling; value =
-one sub-band's samples / max-over-ranks time).
+Ranks.  `--gpus N` is the number of ranks, one process per GPU:
+  * under torch.distributed.run (WORLD_SIZE set) every rank checks that
+    WORLD_SIZE == --gpus and exits 2 otherwise;
+  * without a launcher and N > 1, this process starts
+    `python3 -m torch.distributed.run --nproc-per-node N bench.py ...` as a
+    child BEFORE touching the GPU, waits for it and exits with its code (rank
+    0 prints the JSON line).  RCCL needs N visible GPUs; `--dist-backend
+    gloo` rehearses N ranks sharing fewer GPUs (spectra gathered on the host).
+Sub-band r lives on GPU r, no data-path collective; the K spectra of every
+rank are gathered to rank 0 (torch.distributed gather; "nccl" = RCCL)
+inside each timed region (configs[3]/[4]).  value = all ranks' samples /
+max-over-ranks time (weak scaling).  `--split time` instead cuts ONE
+sub-band's integration along time across the ranks (second
+mode): exact uint64 partials, one reduce (SUM) to rank 0, one fp32 rounding
+there (strong scaling).
+
+Timing.  A timed region is EXACTLY --steps integrations bracketed by a
+barrier + device synchronize on both sides, its collective included.  The
+region is repeated until --min-seconds of timed work has accumulated (a
+20-step region of configs[1] is only 3 ms); every rank's region times are
+max-reduced per repeat and `value` / `ms_per_step` come from the median
+repeat (all repeats' range is reported).
+
+Verification.  After timing, every rank downloads each input block its last
+region integrated and checks every spectrum that region emitted bit for bit
+against the C oracle (outside the timed region; the oracle is the checker,
+never the measured path); rank 0 also checks that the gathered spectra equal
+what each rank holds.  `verified` is in the JSON line and a mismatch exits 3.
 
 Prints ONE JSON line on rank 0.  Options beyond the driver contract:
   --config c2|c5|bmf|c3   workload (c3 = pinned host buffer, H2D overlapped;
@@ -28,39 +47,39 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(REPO, "paf-baseband2power_amd"))
-
-import torch  # noqa: E402  (first: one HIP runtime per process, see paf_b2p/_lib.py)
-import torch.distributed as dist  # noqa: E402
-
-import paf_b2p  # noqa: E402
-from paf_b2p import distributed as D  # noqa: E402
-from paf_b2p.geometry import CONFIGS, samples_per_block  # noqa: E402
+PKG = os.path.join(REPO, "paf-baseband2power_amd")
+ORACLE = os.path.join(REPO, "oracle")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 try:  # the metric string exactly as BASELINE.json names it
     METRIC = json.load(open(os.path.join(REPO, "BASELINE.json"), encoding="utf-8"))["metric"]
 except (OSError, ValueError, KeyError):
-    METRIC = "baseband Msamples/s integrated + % HBM-read roofline, 1024\u00d71024 accum"
+    METRIC = "baseband Msamples/s integrated + % HBM-read roofline, 1024×1024 accum"
 SEED = 20181105
 NBLOCKS = 4
+BASELINE_CONFIG = {"c2": "configs[1]", "c5": "configs[4]", "c3": "configs[2]", "bmf": "reference-native"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks, one process per GPU")
+    ap.add_argument("--steps", type=int, default=50, help="integrations per timed region")
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--min-seconds", type=float, default=0.5,
+                    help="repeat the K-step region until this much timed work has run")
     ap.add_argument("--config", default="c2", choices=["c2", "c5", "bmf", "c3"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="gloo: rehearse N ranks on one GPU (spectra gathered on the host)")
+                    help="gloo: rehearse N ranks on fewer GPUs (spectra gathered on the host)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise torch.distributed even at world size 1 (rehearses the "
                          "RCCL gather path on one GPU)")
@@ -68,7 +87,86 @@ def parse():
                     help="time: one integration split across the ranks (strong scaling)")
     ap.add_argument("--no-fuse", action="store_true",
                     help="use b2p_push + b2p_finish_async instead of b2p_integrate")
-    return ap.parse_args()
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-timing oracle check")
+    a = ap.parse_args(argv)
+    if a.gpus < 1 or a.steps < 1 or a.warmup < 0:
+        ap.error("--gpus and --steps must be >= 1, --warmup >= 0")
+    return a
+
+
+# --------------------------------------------------------------------------
+# launcher: N ranks without an external torch.distributed.run
+# --------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(a, argv: list[str], port: int) -> list[str]:
+    """the torch.distributed.run command line that starts a.gpus ranks of
+    this script with the same arguments"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__), *argv]
+
+
+def visible_gpus() -> int:
+    """device count without initialising HIP (true of torch.cuda.device_count
+    on this image)"""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(a, argv: list[str]) -> int:
+    """Start a.gpus ranks as ONE child process tree and wait for it.  Called
+    before anything in this process touches the GPU; this process never
+    initialises HIP and never execs."""
+    if a.dist_backend == "nccl":
+        n = visible_gpus()
+        if n < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} over RCCL needs {a.gpus} visible GPUs, found {n} "
+                  "(RCCL refuses two ranks on one device; --dist-backend gloo rehearses)",
+                  file=sys.stderr)
+            return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["BENCH_LAUNCHED_RANKS"] = str(a.gpus)
+    return subprocess.run(launcher_cmd(a, argv, _free_port()), env=env).returncode
+
+
+def check_world(a, world: int) -> str | None:
+    """None if the launched world matches --gpus, else the reason to refuse"""
+    if world != a.gpus:
+        return (f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}; refusing to report "
+                f"{world} rank(s) as {a.gpus} GPU(s)")
+    return None
+
+
+# --------------------------------------------------------------------------
+# labels
+# --------------------------------------------------------------------------
+def workload_label(config: str, geom_desc: str, world: int, split: bool, host_mode: bool) -> str:
+    where = "pinned host buffer, H2D overlapped" if host_mode else "HBM-resident"
+    if split:
+        return (f"1 sub-band, {geom_desc}, {where}; one integration split by time over "
+                f"{world} MI355X, exact partials reduced to rank 0")
+    return (f"{world} sub-band(s), {geom_desc} each, {where}, 1 per MI355X over {world} MI355X"
+            + (", spectra gathered to rank 0" if world > 1 else ""))
+
+
+def parallelism_label(world: int, split: bool, dist_on: bool, rccl: bool) -> str:
+    if split:
+        s = f"time split x{world}"
+        if dist_on:
+            s += ", RCCL reduce (SUM) of uint64 partials" if rccl else ", gloo reduce (rehearsal)"
+        return s
+    s = f"sub-band sharding x{world}"
+    if dist_on:
+        s += ", RCCL gather of spectra to rank 0" if rccl else ", gloo gather to rank 0 (rehearsal)"
+    return s
 
 
 def pmc_traffic(config: str):
@@ -81,65 +179,87 @@ def pmc_traffic(config: str):
     try:
         d = json.load(open(p))
         return d.get("hbm_bytes_per_launch"), os.path.relpath(p, REPO)
-    except Exception:
+    except (OSError, ValueError):
         return None, None
 
 
-def _host_cpu() -> dict:
-    """model / logical CPUs / NUMA nodes of the box (SURVEY.md 8d asks for them)"""
-    model = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    try:
-        numa = len([d for d in os.listdir("/sys/devices/system/node") if d.startswith("node")])
-    except OSError:
-        numa = None
-    return {"model": model, "logical_cpus": os.cpu_count(), "numa_nodes": numa}
+# --------------------------------------------------------------------------
+# CPU baseline and verification (the oracle's only uses; outside any timing)
+# --------------------------------------------------------------------------
+def cpu_threads() -> int:
+    sys.path.insert(0, ORACLE)
+    import cpu_baseline as cb
+    return cb.effective_cpus()
 
 
-def cpu_baseline(geom, seconds: float, threads: int):
-    """The oracle's C restatement (oracle/b2p_oracle.c), OpenMP over host
-    threads, on a bounded sample of the same workload held in host RAM;
-    a quarter of the budget times it on one thread as well."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import b2p_oracle as npo  # noqa: E402
-    import oracle_c as co  # noqa: E402
-    g = npo.Geom(**geom.as_dict())
-    sample_bytes = min(g.block_bytes, 256 << 20) // g.frame_bytes * g.frame_bytes
-    buf = co.fill_synthetic(g, sample_bytes, SEED, 0, 0)
-    if threads <= 0:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-
-    def timed(nthreads, budget):
-        co.integrate(g, buf[: g.frame_bytes * 64], nthreads=nthreads)  # warm
-        passes, t0 = 0, time.perf_counter()
-        while True:
-            co.integrate(g, buf, nthreads=nthreads)
-            passes += 1
-            el = time.perf_counter() - t0
-            if el >= budget or passes >= 100000:
-                return passes, el
-
-    passes, el = timed(threads, seconds * 0.75)
-    p1, e1 = timed(1, seconds * 0.25)
-    per_pass = sample_bytes // g.word_bytes * g.npol
-    return {"value": round(passes * per_pass / el / 1e6, 2), "unit": "Msamples/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{passes} passes over {sample_bytes >> 20} MiB of the same synthetic "
-                      f"{g.nchan}-chan int{g.nbit} block ({el:.1f} s, host RAM, no file I/O)",
-            "value_1thread": round(p1 * per_pass / e1 / 1e6, 2),
-            "host": _host_cpu()}
+def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
+    """The C restatement timed in a child process (its own OpenMP binding),
+    at every CPU this job may use and at 1 thread, on one full block."""
+    sys.path.insert(0, ORACLE)
+    import cpu_baseline as cb
+    threads = cb.effective_cpus()
+    r = subprocess.run([sys.executable, os.path.join(ORACLE, "cpu_baseline.py"), json.dumps(geom_dict),
+                        str(seconds), str(SEED)], env=cb.child_env(threads), capture_output=True,
+                       text=True, timeout=max(120, seconds * 10))
+    if r.returncode != 0:
+        print(f"bench.py: cpu baseline failed ({r.returncode}): {r.stderr[-500:]}", file=sys.stderr)
+        return None
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def main():
-    a = parse()
+def oracle_spectrum(geom_dict: dict, read_chunk, nbytes: int, threads: int):
+    """oracle fp32 spectrum of a block, fed in whole-frame chunks (exact
+    uint64 sums accumulate across chunks)"""
+    sys.path.insert(0, ORACLE)
+    import numpy as np
+
+    import b2p_oracle as npo
+    import oracle_c as co
+    g = npo.Geom(**geom_dict)
+    step = max(1, (256 << 20) // g.frame_bytes) * g.frame_bytes
+    acc = np.zeros(g.nout, dtype=np.uint64)
+    for off in range(0, nbytes, step):
+        n = min(step, nbytes - off)
+        co.integrate(g, read_chunk(off, n), nthreads=threads, acc=acc)
+    return co.finalize(g, acc)
+
+
+def synthetic_reader(geom_dict: dict, subband: int, block: int, threads: int):
+    """chunks of a synthetic block regenerated on the host by the oracle's
+    C generator (the same counter-based stream as b2p_fill_synthetic)"""
+    sys.path.insert(0, ORACLE)
+    import b2p_oracle as npo
+    import oracle_c as co
+    g = npo.Geom(**geom_dict)
+    esz = g.nbit // 8
+
+    def rd(off, n):
+        return co.fill_synthetic(g, n, SEED, subband, block, elem0=off // esz)
+    return rd
+
+
+# --------------------------------------------------------------------------
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)
+
+    sys.path.insert(0, PKG)
+    from paf_b2p import distributed as D
     rank, world, local = D.env_ranks()
-    n_gpus = max(world, 1)
+    bad = check_world(a, world)
+    if bad:
+        print(bad, file=sys.stderr)
+        return 2
+
+    import numpy as np
+    import torch  # first: one HIP runtime per process, see paf_b2p/_lib.py
+    import torch.distributed as dist
+
+    import paf_b2p
+    from paf_b2p.geometry import CONFIGS, samples_per_block
+
     cfg = CONFIGS[a.config]
     geom = cfg["geom"]()
     dist_on = world > 1 or a.force_dist
@@ -147,15 +267,19 @@ def main():
     if dist_on:
         D.init(a.dist_backend, local)
     split = a.split == "time"
+    host_mode = a.config == "c3"
     subband = 0 if split else D.subband_of(rank)
     spb = samples_per_block(geom)  # one sub-band's integration
+    full_geom = {f: int(getattr(geom, f)) for f, _ in geom._fields_ if f != "reserved"}
     elem0 = 0
     if split:  # this rank's share of the integration's frames
         first, nf = D.time_share(rank, world, geom.nsamp_int // geom.nsamp_df)
         full_nsamp = geom.nsamp_int
-        geom = paf_b2p.make_geom(**{f: getattr(geom, f) for f, _ in geom._fields_ if f != "reserved"})
+        geom = paf_b2p.make_geom(**full_geom)
         geom.nsamp_int = nf * geom.nsamp_df
         elem0 = first * paf_b2p.geometry.frame_bytes(geom) // (geom.nbit // 8)
+    my_geom = {f: int(getattr(geom, f)) for f, _ in geom._fields_ if f != "reserved"}
+    K = a.steps
     # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
     it = paf_b2p.Integrator(geom, device=D.device_of(local))
     nout, bb = it.nout, it.block_bytes
@@ -169,23 +293,21 @@ def main():
 
     if split:
         # exact partial sums, K x nout uint64 (as int64 for torch), reduced
-        # to rank 0 after the loop; rank 0 then rounds them to fp32
-        sums_t = torch.zeros((max(a.steps, 1), nout), dtype=torch.int64, device="cuda")
-        spec_t = torch.zeros((max(a.steps, 1), nout), dtype=torch.float32, device="cuda")
+        # to rank 0 after each region; rank 0 then rounds them to fp32
+        sums_t = torch.zeros((K, nout), dtype=torch.int64, device="cuda")
+        spec_t = torch.zeros((K, nout), dtype=torch.float32, device="cuda")
         out_ptr = sums_t.data_ptr()
     elif rccl:
         # finalize writes the K spectra straight into torch device memory;
         # the gather follows the last finalize on the shared stream
-        out_t = torch.zeros((a.steps, nout), dtype=torch.float32, device="cuda")
+        out_t = torch.zeros((K, nout), dtype=torch.float32, device="cuda")
         out_ptr = out_t.data_ptr()
     else:
-        out_buf = it.alloc(max(a.steps, 1) * nout * 4)
+        out_buf = it.alloc(K * nout * 4)
         out_ptr = out_buf.ptr
 
-    host_mode = a.config == "c3"
     blocks = []
     if host_mode:
-        import numpy as np
         hb = np.empty(bb, dtype=np.uint8)
         d = it.alloc(bb)
         it.fill_synthetic(d, SEED, subband, 0, elem0=elem0)
@@ -201,111 +323,196 @@ def main():
     it.sync()
 
     def step(k, out_row):
+        blk = blocks[k % len(blocks)]
         if split:  # this rank's share -> exact partial sums (row out_row)
-            it.push(blocks[k % len(blocks)])
-            it.finish_partial(out_ptr + (out_row or 0) * nout * 8, True)
+            it.push(blk)
+            it.finish_partial(out_ptr + out_row * nout * 8, True)
             return
-        dst = out_ptr + (out_row or 0) * nout * 4
+        dst = out_ptr + out_row * nout * 4
         if a.no_fuse or host_mode:  # the push / finish_async pair
-            it.push(blocks[k % len(blocks)])
+            it.push(blk)
             it.finish_async(dst, True)
         else:  # b2p_integrate: one integrate launch per integration (its
             # finalize rides on the next launch)
-            it.integrate(blocks[k % len(blocks)], dst, True)
+            it.integrate(blk, dst, True)
 
-    for w in range(a.warmup):
-        step(w, None)
-    it.sync()
-    if dist_on:
-        if rccl:
-            torch.cuda.synchronize()
-        # the first collective of a communicator sets up its channels; run
-        # the timed region's collective once here, on same-shaped buffers
+    def collective():
+        """the region's exchange: spectra gathered (or partials reduced) to
+        rank 0; returns what rank 0 holds"""
         if split:
-            D.reduce_sums(sums_t if rccl else sums_t.cpu())
-        elif rccl:
-            D.gather_spectra(out_t)
-        else:
-            D.gather_spectra(torch.zeros((a.steps, nout), dtype=torch.float32))
+            if dist_on:
+                if rccl:
+                    total = D.reduce_sums(sums_t)  # RCCL reduce (SUM) of K x nout partials
+                else:  # gloo rehearsal: partials through host memory
+                    host_total = D.reduce_sums(sums_t.cpu())
+                    total = host_total.cuda() if host_total is not None else None
+            else:
+                total = sums_t
+            if rank == 0:
+                it.finalize_sums(total.data_ptr(), K, spec_t.data_ptr(), full_nsamp)
+                it.sync()
+            return None
         if rccl:
+            return D.gather_spectra(out_t)  # RCCL gather of K x nout fp32 to rank 0
+        if dist_on:
+            host = it.download(out_buf, nbytes=K * nout * 4).view("float32").reshape(K, nout)
+            return D.gather_spectra(torch.from_numpy(host.copy()))
+        return None
+
+    def fence():
+        it.sync()
+        if rccl or split:
             torch.cuda.synchronize()
-        dist.barrier()
+        if dist_on:
+            dist.barrier()
+
+    kk = 0
+    for _ in range(a.warmup):
+        step(kk, 0)
+        kk += 1
+    it.sync()
+    if dist_on:  # a communicator's first collective sets up its channels
+        collective()
+    fence()
+
+    def region():
+        nonlocal kk
+        fence()
+        t0 = time.perf_counter()
+        it.set_timing(2)  # one event pair on the integrator's stream around the K launches
+        for k in range(K):
+            step(kk, k)
+            kk += 1
+        it.set_timing(0)  # records the closing event right behind the last launch (no wait)
+        if not rccl:  # host-side exchange (gloo) reads what the integrator's stream wrote
+            it.sync()
+        got = collective()
+        fence()
+        return time.perf_counter() - t0, got
 
     it.reset_stats()
-    # one event pair on the integrator's stream around the K launches (per-
-    # launch events would put a few us of event plumbing between kernels)
-    it.set_timing(2)
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        step(a.warmup + k, k)
-    it.set_timing(0)  # records the closing event right behind the last launch (no wait)
-    if not rccl:
-        it.sync()
-    if split:
-        if dist_on:
-            if rccl:
-                total = D.reduce_sums(sums_t)  # RCCL reduce (SUM) of K x nout partials
-            else:  # gloo rehearsal: partials through host memory
-                host_total = D.reduce_sums(sums_t.cpu())
-                total = host_total.cuda() if host_total is not None else None
-        else:
-            total = sums_t
-        if rank == 0:
-            it.finalize_sums(total.data_ptr(), a.steps, spec_t.data_ptr(), full_nsamp)
-            it.sync()
-        torch.cuda.synchronize()
-    elif rccl:
-        gathered = D.gather_spectra(out_t)  # RCCL all-gather of K x nout fp32
-        torch.cuda.synchronize()
-    elif dist_on:
-        host = it.download(out_buf, nbytes=a.steps * nout * 4).view("float32").reshape(a.steps, nout)
-        gathered = D.gather_spectra(torch.from_numpy(host.copy()))
+    el0, gathered = region()
+    el0_max = D.max_over_ranks(el0, "cuda" if rccl else "cpu") if dist_on else el0
+    repeats = max(1, min(100000, math.ceil(a.min_seconds / max(el0_max, 1e-9))))
+    els = [el0]
+    for _ in range(repeats - 1):
+        el, gathered = region()
+        els.append(el)
+    last_k0 = kk - K  # first step of the last region
     if dist_on:
-        dist.barrier()
-    el = time.perf_counter() - t0
+        t = torch.tensor(els, dtype=torch.float64, device="cuda" if rccl else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        els_max = t.cpu().tolist()
+        mine = torch.tensor([statistics.median(els)], dtype=torch.float64,
+                            device="cuda" if rccl else "cpu")
+        per_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+        per_rank_ms = [round(float(x.item()) / K * 1e3, 4) for x in per_rank]
+    else:
+        els_max, per_rank_ms = els, [round(statistics.median(els) / K * 1e3, 4)]
+    el_med = statistics.median(els_max)
     st = it.stats()
 
-    el_max = D.max_over_ranks(el, "cuda" if rccl else "cpu") if dist_on else el
-    if dist_on and rank == 0 and not split:
-        assert len(gathered) == world and all(g.shape == (a.steps, nout) for g in gathered)
+    # ---- verification (outside timing) ------------------------------------
+    verified = None
+    vinfo = {}
+    if not a.no_verify:
+        vthreads = max(1, cpu_threads() // world)
+        rows_ok = True
+        blocks_of_rows = {}
+        for j in range(K):
+            blocks_of_rows.setdefault((last_k0 + j) % len(blocks), []).append(j)
+        if split:
+            if rank == 0:
+                spec = spec_t.cpu().numpy()
+                for b, rows in blocks_of_rows.items():
+                    ref = oracle_spectrum(full_geom, synthetic_reader(full_geom, 0, b, vthreads),
+                                          paf_b2p.geometry.block_bytes(paf_b2p.make_geom(**full_geom)),
+                                          vthreads)
+                    rows_ok &= all(np.array_equal(spec[j].view(np.uint32), ref.view(np.uint32))
+                                   for j in rows)
+        else:
+            if rccl:
+                local_spec = out_t.cpu().numpy()
+            else:
+                local_spec = it.download(out_buf, nbytes=K * nout * 4).view(np.float32).reshape(K, nout)
+            for b, rows in blocks_of_rows.items():
+                blk = blocks[b]
+                if host_mode:
+                    def rd(off, n, blk=blk):
+                        return blk[off:off + n]
+                else:
+                    def rd(off, n, blk=blk):
+                        return it.download(blk, nbytes=n, offset=off)
+                ref = oracle_spectrum(my_geom, rd, bb, vthreads)
+                rows_ok &= all(np.array_equal(local_spec[j].view(np.uint32), ref.view(np.uint32))
+                               for j in rows)
+            if dist_on:  # rank 0 holds exactly what every rank emitted
+                csum = torch.tensor([int(np.sum(local_spec.view(np.uint32), dtype=np.uint64))],
+                                    dtype=torch.int64, device="cuda" if rccl else "cpu")
+                sums = [torch.zeros_like(csum) for _ in range(world)]
+                dist.all_gather(sums, csum)
+                if rank == 0:
+                    g_ok = len(gathered) == world and all(
+                        tuple(gt.shape) == (K, nout) and
+                        int(np.sum(gt.cpu().numpy().view(np.uint32), dtype=np.uint64)) == int(s.item())
+                        for gt, s in zip(gathered, sums))
+                    rows_ok &= g_ok
+                    vinfo["gather"] = "rank 0 holds every rank's K spectra" if g_ok else "MISMATCH"
+        ok_t = torch.tensor([1 if rows_ok else 0], dtype=torch.int64, device="cuda" if rccl else "cpu")
+        if dist_on:
+            dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        verified = bool(ok_t.item())
+        vinfo.update(what=(f"every spectrum of the last timed region ({K}) against the C oracle of "
+                           f"its input block ({len(blocks_of_rows)} distinct block(s)"
+                           + (", regenerated on the host" if split else ", downloaded from HBM")
+                           + f"), bit for bit, {'rank 0' if split else 'every rank'}"),
+                     threads=vthreads)
 
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
     achieved = bytes_per_launch / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
     traffic, traffic_src = pmc_traffic(a.config)
 
+    rc = 0
     if rank == 0:
-        value = D.aggregate_rate(1 if split else n_gpus, a.steps, spb, el_max)
+        value = D.aggregate_rate(1 if split else world, K, spb, el_med)
+        geom_desc = (f"{paf_b2p.geometry.nchan(geom)} ch x {geom.npol} pol int{geom.nbit}"
+                     + (" BE TFTFP" if geom.big_endian else ""))
         res = {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "Msamples/s",
-            "n_gpus": n_gpus,
-            "steps": a.steps,
+            "n_gpus": world,
+            "steps": K,
             "warmup": a.warmup,
-            "ms_per_step": round(el_max / max(a.steps, 1) * 1e3, 4),
+            "ms_per_step": round(el_med / K * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if split else "weak",
             "vs_baseline": None,
             "dtype": f"int{geom.nbit}" + ("-be" if geom.big_endian else ""),
             "data": "synthetic (counter-based SplitMix64 Gaussian, seed 20181105, sub-band = rank)",
+            "verified": verified,
+            "verification": vinfo or None,
+            "ranks": world,
+            "rccl_ranks": world if rccl else 0,
+            "timed_regions": len(els_max),
+            "timed_seconds": round(sum(els_max), 4),
+            "ms_per_step_range": [round(min(els_max) / K * 1e3, 4), round(max(els_max) / K * 1e3, 4)],
+            "per_rank_ms_per_step": per_rank_ms,
             "config": {
-                "workload": cfg["what"] + (
-                    f"; ONE integration split by time over {world} GPU(s), exact partials reduced"
-                    if split else ("" if world == 1 else f"; {world} sub-bands, 1 per GPU")),
-                "baseline_config": {"c2": "configs[1]", "c5": "configs[4]", "c3": "configs[2]",
-                                    "bmf": "reference-native"}[a.config],
-                "nchan": int(geom.nchunk * geom.nchan_chunk),
+                "workload": workload_label(a.config, geom_desc, world, split, host_mode),
+                "baseline_config": BASELINE_CONFIG[a.config],
+                "nchan": int(paf_b2p.geometry.nchan(geom)),
                 "npol": int(geom.npol),
-                "nsamp_int": int(geom.nsamp_int),
+                "nsamp_int": int(full_nsamp if split else geom.nsamp_int),
                 "bytes_per_integration": int(bb * (world if split else 1)),
                 "input": "pinned host buffer, H2D overlapped (PCIe-inclusive)" if host_mode
-                         else f"HBM-resident, {NBLOCKS} rotating blocks",
-                "parallelism": (f"time split x{n_gpus}" + (
-                    (", RCCL reduce (SUM) of uint64 partials" if rccl else ", gloo reduce (rehearsal)")
-                    if dist_on else "")) if split else (f"sub-band sharding x{n_gpus}" + (
-                    (", RCCL all-gather of spectra" if rccl else ", gloo gather (rehearsal)")
-                    if dist_on else "")),
+                         else f"HBM-resident, {NBLOCKS} rotating blocks per GPU",
+                "parallelism": parallelism_label(world, split, dist_on, rccl),
+                "launcher": ("bench.py --gpus spawned torch.distributed.run"
+                             if os.environ.get("BENCH_LAUNCHED_RANKS") else
+                             ("torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")),
                 "launch": {"threads": it.info.threads, "columns": it.info.columns,
                            "row_groups": it.info.row_groups, "replicas": it.info.replicas,
                            "unroll": it.info.unroll, "nt_loads": bool(it.info.nontemporal)},
@@ -321,16 +528,20 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "avg_launch_us": round(kern_avg_s * 1e6, 2),
-                "timing": "HIP events on the integrator stream bracketing the timed launches "
-                          "(region / launches: gaps and finalizes included, an upper bound)",
+                "launches_timed": int(st["launches"]),
+                "timing": "HIP events on the integrator stream bracketing each timed region's "
+                          "launches (region / launches: gaps and finalizes included, an upper bound)",
                 "finalizes": ("carried by the next integrate launch; "
-                              f"{st['finalizes']} standalone finalize launch(es) inside the region"),
+                              f"{st['finalizes']} standalone finalize launch(es) inside the regions"),
             },
             "cpu_baseline": None,
         }
         if world == 1 and a.cpu_seconds > 0 and not host_mode:
-            res["cpu_baseline"] = cpu_baseline(geom, a.cpu_seconds, a.cpu_threads)
+            res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)
         print(json.dumps(res), flush=True)
+    if verified is False:
+        print(f"bench.py: rank {rank}: spectra differ from the oracle", file=sys.stderr)
+        rc = 3
 
     for b in blocks:
         if hasattr(b, "free"):
@@ -340,7 +551,8 @@ def main():
     it.close()
     if dist_on:
         dist.destroy_process_group()
+    return rc
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

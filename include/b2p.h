@@ -40,6 +40,14 @@ extern "C" {
 #define B2P_EHIP (-6)         /* HIP runtime error; text in b2p_last_error()    */
 #define B2P_ENOMEM (-7)       /* device or host allocation failed              */
 #define B2P_EALIGN (-8)       /* buffer not 16-byte aligned                    */
+#define B2P_EFAILED (-9)      /* an earlier call failed after part of its work
+                                 was enqueued, so the running sums are unknown;
+                                 every later call that enqueues work or emits a
+                                 result (push, integrate, finish*, sync, fence*,
+                                 finalize_sums, assemble, set_stream,
+                                 set_timing) returns this until b2p_close;
+                                 cleanup (dev_free, unregister_host, close) and
+                                 b2p_last_error (the first failure) still work */
 
 /*
  * Layout of one input ring block:
@@ -144,7 +152,9 @@ int b2p_unregister_host(b2p_ctx_t *ctx, void *base);
  * is_device = 0: buf is host memory (register it for full PCIe rate); it is
  *   copied in frame-aligned chunks on a copy stream overlapped with the
  *   kernel, and b2p_push returns once every byte has been copied, so the
- *   caller may release / close the DADA block. */
+ *   caller may release / close the DADA block.  If a host-span push fails
+ *   after its first chunk was enqueued, the context is marked failed
+ *   (B2P_EFAILED from then on, see above). */
 int b2p_push(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device);
 /* Emit the integration: out[nout] (host memory), blocking.  Returns B2P_OK
  * if exactly nsamp_int samples were pushed, B2P_EPARTIAL otherwise (the
@@ -234,7 +244,8 @@ int b2p_dev_alloc(b2p_ctx_t *ctx, void **dev, size_t bytes);
  * (idf_rel * nchunk + chunk) * 7168, idf_rel computed from each header
  * relative to the reference frame (ref_idf, ref_sec) exactly as
  * capture.c:566 does, chunk = chunk_of_df[i] (device, capture.c:571-584).
- * Frames outside [0, block_ndf) or with chunk >= nchunk are not placed.
+ * Frames outside [0, block_ndf) or with chunk >= nchunk are not placed;
+ * nchunk is 1..255, so a chunk byte of 255 always means "no chunk".
  * counts (device, nchunk + 3 uint64, accumulated): frames placed per
  * chunk, then frames before the block, after it, with a bad chunk.  Slots
  * no frame reaches keep their previous bytes (as in the capture ring).

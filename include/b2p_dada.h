@@ -17,7 +17,10 @@
  *    shared-memory segment per block (ids kept in the sync segment), and one
  *    semaphore set (clear / full-per-reader / lock semaphores);
  *  - a block filled with fewer than bufsz bytes ends the transfer (EOD),
- *    exactly as PSRDADA's ipcbuf_mark_filled does;
+ *    exactly as PSRDADA's ipcbuf_mark_filled does.  The EOD
+ *    mark is kept per block, so a ring carries any number of transfers: a
+ *    reader stops at its transfer's EOD block and takes the next transfer
+ *    (header, then data) after unlock_read + lock_read;
  *  - wire compatibility with libpsrdada's own segment layout is NOT claimed:
  *    processes on both sides of a ring must use this library.
  */
@@ -60,8 +63,10 @@ typedef struct ipcbuf {
   uint64_t cur_index;     /* the block opened last */
   int read_depth;         /* reader: blocks it may hold at once (0 = 1, PSRDADA) */
   int eod_pending;        /* reader: the empty EOD block waits behind open ones */
+  int eod_seen;           /* reader: took this transfer's EOD block (reset by lock_read) */
+  int wrote_eod;          /* writer: this session ended its transfer (reset by lock_write) */
 } ipcbuf_t;
-#define IPCBUF_INIT {0, 0, -1, -1, NULL, NULL, 0, 0, -1, 0, 0, 0, 0, 0}
+#define IPCBUF_INIT {0, 0, -1, -1, NULL, NULL, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0}
 
 int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers);
 /* device_id >= 0: blocks in that GPU's memory, owned by a holder process and

@@ -1,0 +1,138 @@
+"""oracle/cpu_baseline.py -- TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).
+
+Times the C restatement (oracle/b2p_oracle.c, OpenMP) on one FULL integration
+block of the bench's workload held in host RAM (no file I/O), so the passes
+stream from DRAM rather than the L3 (the EPYC 9575F host has 512 MiB of L3;
+a 1 GiB block does not fit).  SURVEY.md 8(d) "CPU baseline": the reference has
+no CPU path, so the baseline is the port, at 1 thread and at every CPU this
+process may use.
+
+Run as a child process of bench.py (never imported into the GPU process), so
+that OpenMP reads OMP_PROC_BIND / OMP_PLACES / OMP_NUM_THREADS from an
+environment set for it alone:
+
+    python3 oracle/cpu_baseline.py '<geom json>' SECONDS SEED
+
+and prints ONE JSON object.  Threads are bound one per physical core, packed
+from core 0 (OMP_PLACES=cores, OMP_PROC_BIND=close); the block is filled by the
+same threads first, so its pages sit on the NUMA node those cores belong to.
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import sys
+import time
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def cgroup_cpus() -> float | None:
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), None if
+    unlimited or absent.  On the GPU box nproc shows the whole 256-CPU host
+    while cpu.max grants this job 16 CPUs."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+    except (OSError, ValueError):
+        return None
+    if q == "max":
+        return None
+    return int(q) / int(p)
+
+
+def effective_cpus() -> int:
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpus()
+    if q is not None:
+        n = min(n, max(1, int(q)))
+    return n
+
+
+def numa_nodes() -> dict:
+    """{node: set(cpu ids)} from sysfs"""
+    base = "/sys/devices/system/node"
+    out = {}
+    try:
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                cpus = set()
+                for part in open(os.path.join(base, d, "cpulist")).read().strip().split(","):
+                    if not part:
+                        continue
+                    a, _, b = part.partition("-")
+                    cpus.update(range(int(a), int(b or a) + 1))
+                out[int(d[4:])] = cpus
+    except OSError:
+        pass
+    return out
+
+
+def host_cpu() -> dict:
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "logical_cpus": os.cpu_count(), "numa_nodes": len(numa_nodes()) or None,
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus()}
+
+
+def child_env(threads: int) -> dict:
+    env = dict(os.environ)
+    env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores",
+               OMP_WAIT_POLICY="active")
+    return env
+
+
+def run(geom: dict, seconds: float, seed: int) -> dict:
+    sys.path.insert(0, _HERE)
+    import numpy as np
+
+    import b2p_oracle as npo
+    import oracle_c as co
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    host = host_cpu()  # before OpenMP binds this thread to its first place
+    first = min(os.sched_getaffinity(0))
+    g = npo.Geom(**geom)
+    buf = np.empty(g.block_bytes, dtype=np.uint8)
+    co.fill_synthetic(g, g.block_bytes, seed, 0, 0, out=buf)   # first touch by the bound threads
+    per_pass = g.block_bytes // g.word_bytes * g.npol          # complex samples in the block
+
+    def timed(nt: int, budget: float, min_passes: int = 3):
+        co.integrate(g, buf[: g.frame_bytes * max(1, (64 << 20) // g.frame_bytes)], nthreads=nt)
+        rates, t_all = [], time.perf_counter()
+        while len(rates) < min_passes or time.perf_counter() - t_all < budget:
+            t0 = time.perf_counter()
+            co.integrate(g, buf, nthreads=nt)
+            rates.append(per_pass / (time.perf_counter() - t0) / 1e6)
+            if len(rates) >= 10000:
+                break
+        return rates, time.perf_counter() - t_all
+
+    r_n, el_n = timed(threads, seconds * 0.7)
+    r_1, el_1 = timed(1, seconds * 0.3)
+    nodes = numa_nodes()
+    node = next((n for n, c in nodes.items() if first in c), None)
+    return {
+        "value": round(statistics.median(r_n), 2), "unit": "Msamples/s", "cores": threads,
+        "kind": "port",
+        "sample": (f"{len(r_n)} passes ({el_n:.1f} s) at {threads} threads and {len(r_1)} passes "
+                   f"({el_1:.1f} s) at 1 thread over one full {g.block_bytes >> 20} MiB "
+                   f"{g.nchan}-chan int{g.nbit} integration block in host RAM (no file I/O); "
+                   "value = median pass"),
+        "value_1thread": round(statistics.median(r_1), 2),
+        "passes_range": [round(min(r_n), 2), round(max(r_n), 2)],
+        "numa": {"node": node, "binding": "OMP_PLACES=cores OMP_PROC_BIND=close, packed from the "
+                                          "first allowed CPU; block first-touched by the same threads"},
+        "host": host,
+    }
+
+
+if __name__ == "__main__":
+    geom = json.loads(sys.argv[1])
+    print(json.dumps(run(geom, float(sys.argv[2]), int(sys.argv[3]))), flush=True)

@@ -84,6 +84,11 @@ struct b2p_ctx {
   // b2p_fence tickets: event ring
   hipEvent_t fence_ev[8] = {};
   uint64_t fence_next = 0;
+  // sticky failure: a call failed after part of its work was enqueued
+  // (b2p_push's host-span loop), so the running sums are unknown; only
+  // b2p_close is meaningful afterwards (B2P_EFAILED)
+  int failed = 0;
+  long inject_push_fail = -1;  // test hook: B2P_INJECT_PUSH_FAIL=<chunk index>
   char err[256] = {0};
 };
 
@@ -95,6 +100,13 @@ static int set_err(b2p_ctx_t *c, int code, const char *fmt, ...) {
   va_end(ap);
   return code;
 }
+
+// entry guard of every call that touches a context's stream or sums; the
+// first failure's text stays in c->err
+#define LIVE(c)                                 \
+  do {                                          \
+    if ((c) && (c)->failed) return B2P_EFAILED; \
+  } while (0)
 
 #define CK(c, call)                                                            \
   do {                                                                         \
@@ -132,6 +144,7 @@ const char *b2p_strerror(int code) {
     case B2P_EHIP: return "HIP runtime error";
     case B2P_ENOMEM: return "out of memory";
     case B2P_EALIGN: return "buffer not 16-byte aligned";
+    case B2P_EFAILED: return "context failed part-way through an earlier call; close it";
   }
   return "unknown error";
 }
@@ -311,6 +324,7 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   c->interleave = g->nbit == 16 ? 1 : 0;
   if (const char *e = getenv("B2P_INTERLEAVE")) c->interleave = atoi(e) != 0;
   if (const char *e = getenv("B2P_FUSE")) c->fuse = atoi(e) != 0;
+  if (const char *e = getenv("B2P_INJECT_PUSH_FAIL")) c->inject_push_fail = atol(e);
   c->block_bytes = b2p_block_bytes(g);
   int rc;
   int ncu = 256;
@@ -430,6 +444,7 @@ int b2p_get_info(const b2p_ctx_t *c, b2p_info_t *info) {
 
 int b2p_set_stream(b2p_ctx_t *c, void *s) {
   if (!c) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   CK(c, hipStreamSynchronize(c->stream));
   c->stream = s ? (hipStream_t)s : c->own_stream;
@@ -570,8 +585,34 @@ static int ensure_staging(b2p_ctx_t *c) {
   return B2P_OK;
 }
 
+// A host span through the two staging buffers: chunk k is copied on the
+// copy stream while chunk k-1 is integrated.  Returns once every copy has
+// landed (the caller may release the span).  A failure after the first
+// chunk leaves part of the span summed.
+static int push_host(b2p_ctx_t *c, const uint8_t *h, uint64_t nbytes) {
+  int last = -1;
+  long k = 0;
+  for (uint64_t off = 0; off < nbytes; off += c->stage_bytes, ++k) {
+    const uint64_t n = std::min<uint64_t>(c->stage_bytes, nbytes - off);
+    const int i = (int)(c->stage_next++ & 1);
+    if (k == c->inject_push_fail)
+      return set_err(c, B2P_EHIP, "injected failure at staging chunk %ld (B2P_INJECT_PUSH_FAIL)", k);
+    CK(c, hipStreamWaitEvent(c->copy_stream, c->ev_consumed[i], 0));
+    CK(c, hipMemcpyAsync(c->d_stage[i], h + off, n, hipMemcpyHostToDevice, c->copy_stream));
+    CK(c, hipEventRecord(c->ev_copied[i], c->copy_stream));
+    CK(c, hipStreamWaitEvent(c->stream, c->ev_copied[i], 0));
+    int rc = enqueue_span(c, c->d_stage[i], n, nullptr);
+    if (rc != B2P_OK) return rc;
+    CK(c, hipEventRecord(c->ev_consumed[i], c->stream));
+    last = i;
+  }
+  if (last >= 0) CK(c, hipEventSynchronize(c->ev_copied[last]));
+  return B2P_OK;
+}
+
 int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
   if (!c) return B2P_EINVAL;
+  LIVE(c);
   if (nbytes == 0) return B2P_OK;
   if (!buf) return set_err(c, B2P_EINVAL, "null buffer");
   if (nbytes % c->frame_bytes)
@@ -588,21 +629,12 @@ int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
     if ((rc = enqueue_span(c, buf, nbytes, nullptr)) != B2P_OK) return rc;
   } else {
     if ((rc = ensure_staging(c)) != B2P_OK) return rc;
-    const uint8_t *h = (const uint8_t *)buf;
-    int last = -1;
-    for (uint64_t off = 0; off < nbytes; off += c->stage_bytes) {
-      const uint64_t n = std::min<uint64_t>(c->stage_bytes, nbytes - off);
-      const int i = (int)(c->stage_next++ & 1);
-      CK(c, hipStreamWaitEvent(c->copy_stream, c->ev_consumed[i], 0));
-      CK(c, hipMemcpyAsync(c->d_stage[i], h + off, n, hipMemcpyHostToDevice, c->copy_stream));
-      CK(c, hipEventRecord(c->ev_copied[i], c->copy_stream));
-      CK(c, hipStreamWaitEvent(c->stream, c->ev_copied[i], 0));
-      if ((rc = enqueue_span(c, c->d_stage[i], n, nullptr)) != B2P_OK) return rc;
-      CK(c, hipEventRecord(c->ev_consumed[i], c->stream));
-      last = i;
+    rc = push_host(c, (const uint8_t *)buf, nbytes);
+    if (rc != B2P_OK) {
+      // part of the span may already be summed: the integration is unknown
+      c->failed = 1;
+      return rc;
     }
-    // the caller may release the host span once every copy has landed
-    if (last >= 0) CK(c, hipEventSynchronize(c->ev_copied[last]));
   }
   c->samples += samples;
   return B2P_OK;
@@ -624,6 +656,7 @@ extern "C" {
 
 static int finish_common(b2p_ctx_t *c, void *out, int out_is_device, int raw) {
   if (!c || !out) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   int rc = flush_pending(c);  // two finishes in a row: the first runs alone
   if (rc != B2P_OK) return rc;
@@ -653,6 +686,7 @@ int b2p_finish_partial_async(b2p_ctx_t *c, uint64_t *sums, int sums_is_device) {
 int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64_t nsamp_total,
                       float *out) {
   if (!c || !sums || !out) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   int rc = flush_pending(c);  // sums this context still owes come first
   if (rc != B2P_OK) return rc;
@@ -668,6 +702,7 @@ int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64
 
 int b2p_fence(b2p_ctx_t *c, uint64_t *ticket) {
   if (!c || !ticket) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   const int slot = (int)(c->fence_next % 8);
   if (!c->fence_ev[slot]) CK(c, hipEventCreateWithFlags(&c->fence_ev[slot], hipEventDisableTiming));
@@ -678,6 +713,7 @@ int b2p_fence(b2p_ctx_t *c, uint64_t *ticket) {
 
 int b2p_fence_wait(b2p_ctx_t *c, uint64_t ticket) {
   if (!c || ticket >= c->fence_next) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   if (c->fence_next - ticket > 8) {  // its event was recorded again since
     CK(c, hipStreamSynchronize(c->stream));
@@ -689,6 +725,7 @@ int b2p_fence_wait(b2p_ctx_t *c, uint64_t ticket) {
 
 int b2p_sync(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   int rc = flush_pending(c);
   if (rc != B2P_OK) return rc;
@@ -706,6 +743,7 @@ int b2p_finish(b2p_ctx_t *c, float *out) {
 int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, float *out,
                   int out_is_device) {
   if (!c || !out) return B2P_EINVAL;
+  LIVE(c);
   if (c->samples != 0) return set_err(c, B2P_EINVAL, "b2p_integrate with a push pending");
   if (nbytes != c->block_bytes)
     return set_err(c, nbytes % c->frame_bytes ? B2P_ERAGGED : B2P_EINVAL,
@@ -719,6 +757,12 @@ int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, f
   if (!buf) return set_err(c, B2P_EINVAL, "null buffer");
   if ((uintptr_t)buf % 16) return set_err(c, B2P_EALIGN, "device span not 16-B aligned");
   CK(c, hipSetDevice(c->device));
+  // a deferred finalize that lands in d_out (host output of an earlier
+  // finish_async) must not ride on a launch that writes d_out itself
+  if (!out_is_device && c->pend.valid && c->pend.dev_out == c->d_out) {
+    int rf = flush_pending(c);
+    if (rf != B2P_OK) return rf;
+  }
   // the launch finalizes its own set in its last workgroup; a deferred
   // finalize of the previous integration rides on it as well
   int rc = enqueue_span(c, buf, nbytes, out_is_device ? out : c->d_out);
@@ -731,6 +775,7 @@ int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, f
 
 int b2p_set_timing(b2p_ctx_t *c, int mode) {
   if (!c || mode < 0 || mode > 2) return B2P_EINVAL;
+  LIVE(c);
   CK(c, hipSetDevice(c->device));
   if (c->timing == 2 && mode != 2) {  // close the region, last finalize included
     int rc = flush_pending(c);
@@ -790,8 +835,10 @@ int b2p_assemble(b2p_ctx_t *c, const void *dfs, uint64_t ndf, uint32_t df_bytes,
                  const uint8_t *chunk_of_df, uint64_t ref_idf, uint64_t ref_sec, void *block,
                  uint64_t block_ndf, uint32_t nchunk, unsigned long long *counts) {
   if (!c || (ndf && (!dfs || !chunk_of_df)) || !block || !counts) return B2P_EINVAL;
-  if (df_bytes != 7232 || !nchunk || nchunk > 256 || !block_ndf)
-    return set_err(c, B2P_EINVAL, "b2p_assemble: 7232-B frames, 1..256 chunks");
+  LIVE(c);
+  // chunk byte 255 always marks "no chunk" (paf_capture), so at most 255
+  if (df_bytes != 7232 || !nchunk || nchunk > 255 || !block_ndf)
+    return set_err(c, B2P_EINVAL, "b2p_assemble: 7232-B frames, 1..255 chunks");
   if ((uintptr_t)dfs % 16 || (uintptr_t)block % 16)
     return set_err(c, B2P_EALIGN, "b2p_assemble: 16-B aligned buffers");
   CK(c, hipSetDevice(c->device));

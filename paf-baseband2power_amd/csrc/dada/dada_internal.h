@@ -8,7 +8,7 @@
 #include "b2p_dada.h"
 
 #define SYNC_MAGIC 0x50414642u /* "PAFB" */
-#define SYNC_VERSION 2u
+#define SYNC_VERSION 3u
 #define DEV_HANDLE_BYTES 64 /* HIP_IPC_HANDLE_SIZE, hip_runtime_api.h */
 
 /* semaphore set layout */
@@ -25,7 +25,6 @@ struct ipcsync {
   int32_t semid;
   uint64_t w_count;                  /* blocks filled so far            */
   uint64_t r_count[IPCBUF_READERS];  /* blocks cleared by each reader   */
-  uint64_t eod_count;                /* transfer ends after this many   */
   int32_t sod;
   int32_t pad;
   uint64_t s_buf, s_byte;
@@ -34,21 +33,23 @@ struct ipcsync {
   int32_t holder_state;              /* 0 starting, 1 serving, 2 gone    */
   int32_t pad2;
   /* followed by: int32 shmid[nbufs]; uint32 clear_cnt[nbufs];
+   *              uint32 eod[nbufs] (1: the block ends its transfer);
    *              uint64 nbytes[nbufs] (8-aligned);
    *              uint8 handle[nbufs][DEV_HANDLE_BYTES] (device rings)    */
 };
 
 static inline int32_t *sync_shmids(ipcsync_t *s) { return (int32_t *)(s + 1); }
 static inline uint32_t *sync_clear(ipcsync_t *s) { return (uint32_t *)(sync_shmids(s) + s->nbufs); }
+static inline uint32_t *sync_eod(ipcsync_t *s) { return sync_clear(s) + s->nbufs; }
 static inline uint64_t *sync_nbytes(ipcsync_t *s) {
-  uintptr_t p = (uintptr_t)(sync_clear(s) + s->nbufs);
+  uintptr_t p = (uintptr_t)(sync_eod(s) + s->nbufs);
   return (uint64_t *)((p + 7) & ~(uintptr_t)7);
 }
 static inline unsigned char *sync_handles(ipcsync_t *s) {
   return (unsigned char *)(sync_nbytes(s) + s->nbufs);
 }
 static inline size_t sync_size(uint64_t nbufs) {
-  return sizeof(ipcsync_t) + nbufs * (sizeof(int32_t) + sizeof(uint32_t)) + 8 +
+  return sizeof(ipcsync_t) + nbufs * (sizeof(int32_t) + 2 * sizeof(uint32_t)) + 8 +
          nbufs * sizeof(uint64_t) + nbufs * DEV_HANDLE_BYTES;
 }
 

@@ -251,6 +251,7 @@ int ipcbuf_lock_write(ipcbuf_t *id) {
   if (sem_do(id->semid, SEM_WLOCK, -1, SEM_UNDO | IPC_NOWAIT) < 0) return -1;
   id->state = 2;
   id->xfer_count = id->sync->w_count;
+  id->wrote_eod = 0;
   return 0;
 }
 
@@ -268,6 +269,7 @@ int ipcbuf_lock_read(ipcbuf_t *id) {
       id->iread = (int)r;
       id->state = 3;
       id->xfer_count = id->sync->r_count[r];
+      id->eod_seen = 0; /* the next transfer starts after the last EOD taken */
       return 0;
     }
   }
@@ -294,7 +296,8 @@ int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {
   if (!id || id->state != 2 || !id->cur_open || nbytes > id->bufsz) return -1;
   ipcsync_t *s = id->sync;
   sync_nbytes(s)[id->cur_index] = nbytes;
-  if (nbytes < id->bufsz) s->eod_count = s->w_count + 1; /* short block = EOD */
+  sync_eod(s)[id->cur_index] = nbytes < id->bufsz; /* short block = EOD */
+  if (nbytes < id->bufsz) id->wrote_eod = 1;
   __atomic_store_n(&s->w_count, s->w_count + 1, __ATOMIC_RELEASE);
   id->cur_open = 0;
   id->xfer_count++;
@@ -305,14 +308,9 @@ int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {
 
 int ipcbuf_enable_eod(ipcbuf_t *id) {
   if (!id || id->state != 2) return -1;
-  if (id->sync->eod_count && id->sync->eod_count == id->sync->w_count) return 0;
+  if (id->wrote_eod) return 0; /* this session's transfer already ended */
   if (!ipcbuf_get_next_write(id)) return -1;
   return ipcbuf_mark_filled(id, 0);
-}
-
-static int reader_at_eod(ipcbuf_t *id) {
-  uint64_t eod = __atomic_load_n(&id->sync->eod_count, __ATOMIC_ACQUIRE);
-  return eod && id->sync->r_count[id->iread] + (uint64_t)id->cur_open >= eod;
 }
 
 int ipcbuf_set_read_depth(ipcbuf_t *id, int depth) {
@@ -324,10 +322,11 @@ int ipcbuf_set_read_depth(ipcbuf_t *id, int depth) {
 char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {
   if (!id || id->state != 3) return NULL;
   if (id->cur_open >= (id->read_depth > 1 ? id->read_depth : 1)) return NULL;
-  if (reader_at_eod(id)) return NULL;
+  if (id->eod_seen) return NULL; /* this transfer is over */
   if (sem_do(id->semid, SEM_FULL(id->iread), -1, 0) < 0) return NULL;
   id->cur_index = (id->sync->r_count[id->iread] + (uint64_t)id->cur_open) % id->nbufs;
   id->cur_open++;
+  if (sync_eod(id->sync)[id->cur_index]) id->eod_seen = 1;
   if (bytes) *bytes = sync_nbytes(id->sync)[id->cur_index];
   return id->buffer[id->cur_index];
 }
@@ -374,8 +373,7 @@ int ipcbuf_sod(ipcbuf_t *id) { return id && id->sync ? id->sync->sod : 0; }
 
 int ipcbuf_eod(ipcbuf_t *id) {
   if (!id || !id->sync || id->iread < 0) return 0;
-  uint64_t eod = __atomic_load_n(&id->sync->eod_count, __ATOMIC_ACQUIRE);
-  return eod && id->sync->r_count[id->iread] + (uint64_t)id->cur_open >= eod;
+  return id->eod_seen;
 }
 
 uint64_t ipcbuf_get_bufsz(ipcbuf_t *id) { return id ? id->bufsz : 0; }

@@ -17,6 +17,13 @@
  * ring key_in + 0x10*r and GPU d + r, one host thread + one stream each; after
  * every integration the N spectra are gathered to GPU d over RCCL
  * (b2p_group_gather) and written as one N*NCHAN block to key_out.
+ *
+ * DADA library: built by default against libpafdada (include/b2p_dada.h).
+ * With -DB2P_PSRDADA it includes PSRDADA's own headers and calls only the
+ * PSRDADA subset the reference's hosts use plus
+ * ipcbuf_get_nbufs, so it links against the real libpsrdada
+ * (INTEGRATION.md); GPU-resident rings and two blocks in flight, both
+ * libpafdada extensions, are then off.
  */
 #include <getopt.h>
 #include <inttypes.h>
@@ -28,7 +35,18 @@
 #include <unistd.h>
 
 #include "b2p.h"
+#ifdef B2P_PSRDADA
+#include "ascii_header.h"
+#include "dada_def.h"
+#include "dada_hdu.h"
+#include "futils.h"
+#include "ipcio.h"
+#include "multilog.h"
+#define DEVICE_RINGS 0
+#else
 #include "b2p_dada.h"
+#define DEVICE_RINGS 1
+#endif
 
 #define MSTR_LEN 512 /* paf_baseband2power.cuh:4 */
 #define TSAMP_BMF_US (27.0 / 32.0) /* README.md:2 */
@@ -51,6 +69,8 @@ typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
   key_t key;
   int device;
   dada_hdu_t *in;
+  char *hdr;         /* the input ring's header block, copied */
+  uint64_t hdr_size;
   b2p_ctx_t *ctx;
   b2p_geom_t g;
   double tsamp_us;
@@ -158,6 +178,41 @@ static int pick_geometry(const conf_t *conf, const char *hdr, uint64_t rbufsz, b
   return 0;
 }
 
+/* data block of a ring as the ipcbuf_t PSRDADA puts first in ipcio_t */
+static ipcbuf_t *data_buf(dada_hdu_t *h) { return (ipcbuf_t *)h->data_block; }
+
+/* Reader side of the header ring, in PSRDADA calls: take the next header
+ * block, copy it, release it. */
+static int read_header(dada_hdu_t *h, char **hdr, uint64_t *size) {
+  uint64_t n = 0;
+  char *p = ipcbuf_get_next_read(h->header_block, &n);
+  if (!p) return -1;
+  const uint64_t hsz = ipcbuf_get_bufsz(h->header_block);
+  *hdr = calloc(1, hsz + 1);
+  if (!*hdr) return -1;
+  memcpy(*hdr, p, n < hsz ? n : hsz);
+  *size = hsz;
+  return ipcbuf_mark_cleared(h->header_block);
+}
+
+/* ring location of an input ring's blocks: -1 host, else the HIP device */
+static int ring_device(dada_hdu_t *h) {
+#if DEVICE_RINGS
+  return ipcbuf_get_device(data_buf(h));
+#else
+  (void)h;
+  return -1;
+#endif
+}
+
+/* next input block, or NULL at the end of the transfer (checked with
+ * ipcbuf_eod first, so a reader never waits on a ring whose transfer ended) */
+static char *next_block(dada_hdu_t *h, uint64_t *bytes) {
+  uint64_t bid = 0;
+  if (ipcbuf_eod(data_buf(h))) return NULL;
+  return ipcio_open_block_read(h->data_block, bytes, &bid);
+}
+
 /* ---- the integration loop, one thread per sub-band ---------------------- */
 
 typedef struct shared_t {
@@ -204,8 +259,8 @@ static void *worker(void *arg) {
   shared_t *sh = w->sh;
   sub_t *s = &sh->sub[w->r];
   for (;;) {
-    uint64_t bytes = 0, bid = 0;
-    char *blk = ipcio_open_block_read(s->in->data_block, &bytes, &bid);
+    uint64_t bytes = 0;
+    char *blk = next_block(s->in, &bytes);
     sh->have[w->r] = !blk ? -1 : (bytes == s->rbufsz ? 1 : 0);
     pthread_barrier_wait(&sh->bar); /* all sub-bands agree on this round */
     int stop = sh->failed, skip = 0;
@@ -275,6 +330,7 @@ static void *worker(void *arg) {
   return NULL;
 }
 
+#if DEVICE_RINGS
 /* One sub-band on a GPU-resident ring: two blocks in flight.  Block k's
  * launch is enqueued before block k-1 is released, so the GPU never waits
  * on the host between integrations.  Block k-1 goes back to the ring once
@@ -341,6 +397,7 @@ static void run_device_pipelined(shared_t *sh) {
   b2p_unregister_host(s->ctx, spec);
   free(spec);
 }
+#endif
 
 /* -t N: member r integrates bytes [r*share, (r+1)*share) of every block of
  * the one input ring; member 0 reduces the exact partial sums (RCCL
@@ -352,9 +409,8 @@ static void *worker_split(void *arg) {
   sub_t *s0 = &sh->sub[0];
   for (;;) {
     if (w->r == 0) {
-      uint64_t bid = 0;
       sh->blk_bytes = 0;
-      sh->blk = ipcio_open_block_read(s0->in->data_block, &sh->blk_bytes, &bid);
+      sh->blk = next_block(s0->in, &sh->blk_bytes);
       sh->have[0] = !sh->blk ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
     }
     pthread_barrier_wait(&sh->bar);
@@ -519,12 +575,12 @@ int main(int argc, char *argv[]) {
       goto done;
     }
     s->locked = 1;
-    if (dada_hdu_open_read(s->in) < 0) {
+    if (read_header(s->in, &s->hdr, &s->hdr_size) < 0) {
       multilog(log, LOG_ERR, "no header on input ring %x", (unsigned)s->key);
       goto done;
     }
-    s->rbufsz = ipcbuf_get_bufsz(&s->in->data_block->buf);
-    if (pick_geometry(&conf, s->in->header, s->rbufsz, &s->g, &s->tsamp_us, log) < 0) goto done;
+    s->rbufsz = ipcbuf_get_bufsz(data_buf(s->in));
+    if (pick_geometry(&conf, s->hdr, s->rbufsz, &s->g, &s->tsamp_us, log) < 0) goto done;
     if (split) { /* every member's context integrates one time share */
       const uint64_t frames = s->g.nsamp_int / s->g.nsamp_df;
       if (frames % (uint64_t)conf.nsplit) {
@@ -545,7 +601,7 @@ int main(int argc, char *argv[]) {
       multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
       goto done;
     }
-    const int ring_dev = ipcbuf_get_device(&s->in->data_block->buf);
+    const int ring_dev = ring_device(s->in);
     s->ondev = ring_dev >= 0;
     if (s->ondev && split) {
       multilog(log, LOG_ERR, "-t splits host rings (one PCIe link per GPU); ring %x is on a GPU",
@@ -564,8 +620,8 @@ int main(int argc, char *argv[]) {
                (unsigned)s->key, ring_dev);
     }
     /* pin the input ring's blocks for DMA (dada_cuda_dbregister role) */
-    for (uint64_t i = 0; !s->ondev && i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
-      if (b2p_register_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i), s->rbufsz) != B2P_OK)
+    for (uint64_t i = 0; !s->ondev && i < ipcbuf_get_nbufs(data_buf(s->in)); i++)
+      if (b2p_register_host(s->ctx, data_buf(s->in)->buffer[i], s->rbufsz) != B2P_OK)
         multilog(log, LOG_INFO, "register block %" PRIu64 ": %s", i, b2p_last_error(s->ctx));
   }
   b2p_info_t info;
@@ -587,10 +643,10 @@ int main(int argc, char *argv[]) {
     goto done;
   }
   out_locked = 1;
-  if (ipcbuf_get_bufsz(&out->data_block->buf) != sh.obytes) {
+  if (ipcbuf_get_bufsz(data_buf(out)) != sh.obytes) {
     /* same check as diskdb.cu:36-42, for the output ring (py:77-79) */
     multilog(log, LOG_ERR, "output ring block %" PRIu64 " B != NSUB x NCHAN x NPOL x 4 = %" PRIu64 " B",
-             ipcbuf_get_bufsz(&out->data_block->buf), sh.obytes);
+             ipcbuf_get_bufsz(data_buf(out)), sh.obytes);
     goto done;
   }
 
@@ -600,7 +656,7 @@ int main(int argc, char *argv[]) {
     uint64_t ohsz = ipcbuf_get_bufsz(out->header_block);
     if (!ohdr) goto done;
     memset(ohdr, 0, ohsz);
-    memcpy(ohdr, sub[0].in->header, sub[0].in->header_size < ohsz ? sub[0].in->header_size : ohsz);
+    memcpy(ohdr, sub[0].hdr, sub[0].hdr_size < ohsz ? sub[0].hdr_size : ohsz);
     ohdr[ohsz - 1] = 0;
     const uint64_t nsamp_out = split ? sh.nsamp_full : sub[0].g.nsamp_int;
     const double tsamp_out = sub[0].tsamp_us * (double)nsamp_out;
@@ -618,10 +674,12 @@ int main(int argc, char *argv[]) {
     ascii_header_set(ohdr, "POWER_MODE", "%s", sub[0].g.mean ? "MEAN" : "SUM");
     if (conf.nsub > 1) ascii_header_set(ohdr, "NSUBBAND", "%d", conf.nsub);
     if (split) ascii_header_set(ohdr, "NSPLIT", "%d", conf.nsplit);
+#ifndef B2P_PSRDADA /* input-layout keys (libpafdada extension; kept with PSRDADA) */
     ascii_header_del(ohdr, "NCHUNK");
     ascii_header_del(ohdr, "NCHAN_CHUNK");
     ascii_header_del(ohdr, "NSAMP_DF");
     ascii_header_del(ohdr, "BYTE_ORDER");
+#endif
     if (ipcbuf_mark_filled(out->header_block, ohsz) < 0) goto done;
   }
 
@@ -669,11 +727,13 @@ int main(int argc, char *argv[]) {
   }
 
   {
+#if DEVICE_RINGS
     if (!split && nmem == 1 && sub[0].ondev && !getenv("B2P_NO_PIPELINE")) {
       multilog(log, LOG_INFO, "GPU-resident input: two blocks in flight");
       run_device_pipelined(&sh);
       goto joined;
     }
+#endif
     pthread_barrier_init(&sh.bar, NULL, (unsigned)nmem);
     pthread_t th[MAX_SUB];
     worker_t wk[MAX_SUB];
@@ -685,7 +745,9 @@ int main(int argc, char *argv[]) {
     for (int r = 0; r < nmem; r++) pthread_join(th[r], NULL);
     pthread_barrier_destroy(&sh.bar);
   }
+#if DEVICE_RINGS
 joined:
+#endif
   status = sh.failed ? EXIT_FAILURE : EXIT_SUCCESS;
 
 done:
@@ -697,8 +759,8 @@ done:
       if (s->part_dev) b2p_dev_free(s->ctx, s->part_dev);
       if (r == 0 && sh.root_sum) b2p_dev_free(s->ctx, sh.root_sum);
       for (uint64_t i = 0; !s->ondev && s->in && s->in->data_block &&
-                           i < ipcbuf_get_nbufs(&s->in->data_block->buf); i++)
-        b2p_unregister_host(s->ctx, ipcbuf_get_buffer(&s->in->data_block->buf, i));
+                           i < ipcbuf_get_nbufs(data_buf(s->in)); i++)
+        b2p_unregister_host(s->ctx, data_buf(s->in)->buffer[i]);
       if (r == 0 && sh.spec_host) b2p_unregister_host(s->ctx, sh.spec_host);
       if (s->spec_dev) b2p_dev_free(s->ctx, s->spec_dev);
       if (r == 0 && sh.root_dev) b2p_dev_free(s->ctx, sh.root_dev);
@@ -706,6 +768,7 @@ done:
     }
     if (s->locked) dada_hdu_unlock_read(s->in);
     if (s->in) dada_hdu_destroy(s->in);
+    free(s->hdr);
   }
   free(sh.spec_host);
   dada_hdu_destroy(out);

@@ -68,7 +68,9 @@ typedef struct cap_t {
   int nchunk, nozero;
   void *d_frames, *d_chunks; /* the uploaded batch */
   unsigned long long *d_cnt;
-  uint64_t placed_all, dropped_late, dropped_spill;
+  uint64_t placed_all, dropped_late, dropped_spill, dropped_far;
+  uint64_t far_run; /* consecutive frames at or past far_rel */
+  int64_t far_rel;  /* block_ndf + max(block_ndf, 2 x TBUF_NDF) */
   /* host: frames of the current block, and of later ones */
   unsigned char *hf, *hc, *sf, *sc;
   uint64_t hn, cap_frames, sn, spill_cap;
@@ -253,12 +255,13 @@ int main(int argc, char **argv) {
     }
     c.bufsz = ipcbuf_get_bufsz(db);
     c.nchunk = (int)(c.bufsz / ((uint64_t)rbuf_ndf * B2P_DF_PAYLOAD_BYTES));
-    if (!c.nchunk || c.nchunk > 256 || c.bufsz != rbuf_ndf * (uint64_t)c.nchunk * B2P_DF_PAYLOAD_BYTES) {
+    if (!c.nchunk || c.nchunk > 255 || c.bufsz != rbuf_ndf * (uint64_t)c.nchunk * B2P_DF_PAYLOAD_BYTES) {
       multilog(c.log, LOG_ERR, "ring block %" PRIu64 " B is not %" PRIu64 " frames x chunks x 7168 B",
                c.bufsz, rbuf_ndf);
       goto done;
     }
     c.block_ndf = rbuf_ndf;
+    c.far_rel = (int64_t)(rbuf_ndf + (rbuf_ndf > 2 * TBUF_NDF ? rbuf_ndf : 2 * TBUF_NDF));
     c.nozero = nozero;
     c.nblk_max = nblocks ? nblocks
                          : (length > 0 ? (uint64_t)ceil(length / (rbuf_ndf * B2P_DF_TSAMP_SEC)) : UINT64_MAX);
@@ -307,7 +310,7 @@ int main(int argc, char **argv) {
     uint64_t got_all = 0, bad = 0;
     double last_rx = now_s(), t_first = 0;
     const double start_s = idle_s * 5 > 30 ? idle_s * 5 : 30; /* first frame within */
-    int stop = 0;
+    int stop = 0, jumped = 0;
     while (!stop) {
       int pr = poll(pfd, (nfds_t)nport, 20);
       if (pr < 0 && errno != EINTR) break;
@@ -355,6 +358,26 @@ int main(int argc, char **argv) {
               if (open_block(&c) < 0) goto done;
             }
             const int64_t rel = b2p_df_index(&h, &c.ref);
+            /* far ahead of the current block: the reference quits the
+             * capture at two blocks ahead (capture.c:491-508); frames between
+             * block_ndf + TBUF_NDF and there force a block switch (:510-524).
+             * With blocks shorter than 2 x TBUF_NDF (tests) the far limit is
+             * kept past the spill's reach, block_ndf + 2 x TBUF_NDF.  One far
+             * frame (a corrupt timestamp) is dropped and must not drive block
+             * switches; a run of them, more than one per chunk, means the
+             * stream really jumped ahead, and the capture stops, as there */
+            if (rel >= c.far_rel) {
+              c.dropped_far++;
+              if (++c.far_run > (uint64_t)c.nchunk) {
+                multilog(c.log, LOG_ERR, "%" PRIu64 " consecutive frames %" PRId64 "+ frames ahead of "
+                         "the current block: the stream jumped, stopping (capture.c:491-508)", c.far_run,
+                         c.far_rel);
+                stop = jumped = 1;
+                break;
+              }
+              continue;
+            }
+            c.far_run = 0;
             if (rel > c.max_rel) c.max_rel = rel;
             if (file_frame(&c, df, ck, rel) < 0) goto done;
             /* forced switch as soon as a frame runs TBUF_NDF past the block
@@ -402,11 +425,13 @@ int main(int argc, char **argv) {
       }
     }
     free(rx);
+    if (jumped && c.blk && close_block(&c) < 0) goto done; /* deliver what arrived */
     const double el = t_first > 0 ? last_rx - t_first : 0.0;
     multilog(c.log, LOG_INFO, "capture: %" PRIu64 " frames received (%" PRIu64 " not frames), %" PRIu64
              " blocks, %" PRIu64 " frames placed, %" PRIu64 " behind their block, %" PRIu64
-             " past the spill, %.3f s from the first frame to the last", got_all, bad, c.nblk_done, c.placed_all,
-             c.dropped_late, c.dropped_spill, record ? 0.0 : el);
+             " past the spill, %" PRIu64 " far ahead, %.3f s from the first frame to the last", got_all,
+             bad, c.nblk_done, c.placed_all, c.dropped_late, c.dropped_spill, c.dropped_far, record ? 0.0 : el);
+    if (jumped) goto done; /* EXIT_FAILURE: the stream left the capture window */
   }
   status = EXIT_SUCCESS;
 

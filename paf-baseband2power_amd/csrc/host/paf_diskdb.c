@@ -13,6 +13,10 @@
  * Differences: a failing init stops the program (the reference ignored the
  * return value, paf_diskdb.cu:65), and -l names a log file (the reference's
  * conf.log was never initialised, paf_diskdb.cu:28).
+ *
+ * -DB2P_PSRDADA builds it against PSRDADA's own headers and the PSRDADA
+ * subset the reference calls, as the reference is
+ * built; GPU-resident rings (a libpafdada extension) are then off.
  */
 #include <getopt.h>
 #include <inttypes.h>
@@ -21,7 +25,16 @@
 #include <string.h>
 #include <time.h>
 
+#ifdef B2P_PSRDADA
+#include "ascii_header.h"
+#include "dada_def.h"
+#include "dada_hdu.h"
+#include "futils.h"
+#include "ipcio.h"
+#include "multilog.h"
+#else
 #include "b2p_dada.h"
+#endif
 
 #define MSTR_LEN 512
 #define DADA_HDR_SIZE 4096 /* diskdb.cuh:17 */
@@ -63,7 +76,7 @@ static int init_diskdb(conf_t *conf) {
     fprintf(stderr, "Can not connect to hdu %x\n", (unsigned)conf->key);
     return EXIT_FAILURE;
   }
-  ipcbuf_t *db = &conf->hdu->data_block->buf;
+  ipcbuf_t *db = (ipcbuf_t *)conf->hdu->data_block; /* diskdb.cu:33 */
   conf->rbufsz = ipcbuf_get_bufsz(db);
   conf->hdrsz = ipcbuf_get_bufsz(conf->hdu->header_block);
   if (conf->hdrsz != DADA_HDR_SIZE) {
@@ -98,13 +111,15 @@ static int do_diskdb(conf_t *conf) {
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);
   uint64_t block_id, total = 0, nblk = 0;
-  /* a GPU-resident ring (dada_db -g) takes each block through host staging */
-  ipcbuf_t *db = &conf->hdu->data_block->buf;
   char *stage = NULL;
+#ifndef B2P_PSRDADA
+  /* a GPU-resident ring (dada_db -g) takes each block through host staging */
+  ipcbuf_t *db = (ipcbuf_t *)conf->hdu->data_block;
   if (ipcbuf_get_device(db) >= 0 && !(stage = malloc(conf->rbufsz))) {
-    multilog(conf->log, LOG_ERR, "cannot allocate %" PRIu64 " B of staging", conf->rbufsz);
+    multilog(conf->log, LOG_ERR, "cannot allocate %zu B of staging", conf->rbufsz);
     return EXIT_FAILURE;
   }
+#endif
   while (!feof(conf->fp)) {
     char *curbuf = ipcio_open_block_write(conf->hdu->data_block, &block_id);
     if (!curbuf) {
@@ -112,11 +127,13 @@ static int do_diskdb(conf_t *conf) {
       return EXIT_FAILURE;
     }
     size_t n = fread(stage ? stage : curbuf, 1, conf->rbufsz, conf->fp);
+#ifndef B2P_PSRDADA
     if (stage && ipcbuf_copy_in(db, curbuf, stage, n) < 0) {
       multilog(conf->log, LOG_ERR, "copy into device block failed");
       free(stage);
       return EXIT_FAILURE;
     }
+#endif
     ipcio_close_block_write(conf->hdu->data_block, n);
     total += n;
     nblk++;

@@ -31,6 +31,7 @@ B2P_ENODEV = -5
 B2P_EHIP = -6
 B2P_ENOMEM = -7
 B2P_EALIGN = -8
+B2P_EFAILED = -9
 
 
 class B2PError(RuntimeError):

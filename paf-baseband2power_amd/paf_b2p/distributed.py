@@ -53,12 +53,16 @@ def init(backend: str, local_rank: int) -> None:
 
 def gather_spectra(local: torch.Tensor) -> list[torch.Tensor] | None:
     """All ranks' [K, nout] spectra, in rank (= sub-band) order, on rank 0;
-    None elsewhere.  all_gather (supported by both RCCL and gloo) into
-    preallocated buffers; rank 0 keeps them."""
+    None elsewhere.  A gather to rank 0 (configs[3]: "RCCL gather of
+    per-channel power to rank 0"; ncclGather, rccl.h:745): peers send and
+    receive nothing back."""
     world = dist.get_world_size()
-    bufs = [torch.empty_like(local) for _ in range(world)]
-    dist.all_gather(bufs, local.contiguous())
-    return bufs if dist.get_rank() == 0 else None
+    if dist.get_rank() == 0:
+        bufs = [torch.empty_like(local) for _ in range(world)]
+        dist.gather(local.contiguous(), gather_list=bufs, dst=0)
+        return bufs
+    dist.gather(local.contiguous(), dst=0)
+    return None
 
 
 def time_share(rank: int, world: int, nframes: int) -> tuple[int, int]:

@@ -1,0 +1,6 @@
+/* declarations only -- see README.txt */
+#ifndef __FUTILS_H
+#define __FUTILS_H
+#include <stdint.h>
+int64_t fileread(const char *filename, char *buffer, unsigned bufsz);
+#endif

@@ -96,7 +96,7 @@ def test_geometry_accepted():
 
 
 def test_strerror_covers_codes():
-    for code in range(0, -9, -1):
+    for code in range(0, -10, -1):
         s = L.lib().b2p_strerror(code).decode()
         assert s and s != "unknown error"
     assert L.lib().b2p_strerror(-99).decode() == "unknown error"

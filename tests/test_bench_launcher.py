@@ -1,0 +1,112 @@
+"""bench.py's rank plumbing, on CPU (no GPU is touched):
+
+* `--gpus N` without a launcher starts N ranks through torch.distributed.run
+  as a child (never exec), with the same arguments;
+* a launched rank whose WORLD_SIZE differs from --gpus refuses (exit 2)
+  before anything touches the GPU;
+* RCCL with fewer visible GPUs than ranks refuses rather than stacking ranks
+  on one device;
+* the labels name the world size actually running.
+"""
+import os
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+from conftest import REPO
+
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], env=env,
+                          capture_output=True, text=True, timeout=300, cwd=REPO)
+
+
+def test_world_mismatch_refused_before_gpu():
+    r = _run(["--gpus", "8", "--steps", "2"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2 but --gpus 8" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_rccl_needs_one_gpu_per_rank(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "visible_gpus", lambda: 1)
+    called = []
+    monkeypatch.setattr(bench.subprocess, "run", lambda *a, **k: called.append(a))
+    a = bench.parse(["--gpus", "2"])
+    assert bench.launch_ranks(a, ["--gpus", "2"]) == 2
+    assert called == []            # nothing was started
+
+
+def test_launcher_passes_arguments_through(monkeypatch):
+    seen = {}
+
+    class R:
+        returncode = 0
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return R()
+
+    monkeypatch.setattr(bench, "visible_gpus", lambda: 8)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    argv = ["--gpus", "8", "--steps", "20", "--warmup", "5", "--config", "c5"]
+    assert bench.launch_ranks(bench.parse(argv), argv) == 0
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-len(argv) - 1:] == [os.path.join(REPO, "bench.py"), *argv]
+    assert seen["env"]["BENCH_LAUNCHED_RANKS"] == "8"
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_launcher_really_starts_n_ranks(monkeypatch, tmp_path):
+    """the same torch.distributed.run line, pointed at a probe script, starts
+    N ranks that see WORLD_SIZE == N (gloo-free: no rendezvous beyond the
+    launcher's own)"""
+    probe = tmp_path / "probe.py"
+    out = tmp_path / "ranks"
+    out.mkdir()
+    probe.write_text(textwrap.dedent(f"""
+        import os
+        open(os.path.join({str(out)!r}, os.environ["RANK"]), "w").write(
+            os.environ["WORLD_SIZE"] + " " + os.environ.get("BENCH_LAUNCHED_RANKS", ""))
+    """))
+    real = bench.launcher_cmd
+
+    def cmd_for_probe(a, argv, port):
+        c = real(a, argv, port)
+        i = c.index(os.path.abspath(bench.__file__))
+        return c[:i] + [str(probe)]
+
+    monkeypatch.setattr(bench, "launcher_cmd", cmd_for_probe)
+    a = bench.parse(["--gpus", "3", "--dist-backend", "gloo"])
+    assert bench.launch_ranks(a, []) == 0
+    got = {p: (out / p).read_text() for p in os.listdir(out)}
+    assert got == {"0": "3 3", "1": "3 3", "2": "3 3"}
+
+
+@pytest.mark.parametrize("world,split", [(1, False), (2, False), (8, False), (4, True)])
+def test_labels_follow_world(world, split):
+    w = bench.workload_label("c5", "1024 ch x 2 pol int8", world, split, False)
+    p = bench.parallelism_label(world, split, world > 1, True)
+    assert f"over {world} MI355X" in w
+    assert f"x{world}" in p
+    if world == 1 and not split:
+        assert "gathered" not in w
+    if world > 1 and not split:
+        assert "gather of spectra to rank 0" in p
+
+
+def test_bad_counts_rejected():
+    for args in (["--gpus", "0"], ["--steps", "0"]):
+        r = _run(args)
+        assert r.returncode == 2 and "must be >= 1" in r.stderr

@@ -168,6 +168,37 @@ def test_ring_full_last_block_then_empty_eod(ring):
     assert out == [1024, 1024, 1024, "eod"]
 
 
+def test_ring_carries_several_transfers(ring):
+    """EOD is marked per block: a second transfer on the same ring is read in
+    full after the first one's EOD, and a reader that is behind stops at the
+    first transfer's (empty or short) EOD block instead of reading it as data
+    (PSRDADA rings carry one transfer after another)"""
+    k = ring(12, 1024)                   # 9 blocks in all: no reader runs meanwhile
+    with dada.Hdu(k, "W") as w:          # transfer 1 ends with a short block
+        w.write_header("XFER 1\n")
+        for i in range(3):
+            w.write_block(bytes([i]) * 1024)
+        w.write_block(b"a" * 10)
+    with dada.Hdu(k, "W") as w:          # transfer 2: unlock_write ends it (empty block)
+        w.write_header("XFER 2\n")
+        for i in range(2):
+            w.write_block(bytes([10 + i]) * 1024)
+    with dada.Hdu(k, "W") as w:          # transfer 3: full blocks then a 0-byte EOD
+        w.write_header("XFER 3\n")
+        w.write_block(b"z" * 1024)
+    got = []
+    for _ in range(3):                   # the reader was behind all three
+        with dada.Hdu(k, "R") as r:
+            h = r.read_header().split(b"\n")[0]
+            blocks = []
+            while (b := r.read_block()) is not None:
+                blocks.append(b)
+            got.append((h, [len(b) for b in blocks], [b[0] for b in blocks], r.eod()))
+    assert got == [(b"XFER 1", [1024, 1024, 1024, 10], [0, 1, 2, 97], True),
+                   (b"XFER 2", [1024, 1024], [10, 11], True),
+                   (b"XFER 3", [1024], [122], True)]
+
+
 def test_two_readers_each_see_every_block(ring):
     k = ring(2, 512, nreaders=2)
     res = {0: [], 1: []}

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 def test_bench_prints_one_contract_line(gpu):
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--cpu-seconds", "0.5"], capture_output=True, text=True, timeout=600, cwd=REPO)
+                        "--cpu-seconds", "1", "--min-seconds", "0.05"], capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
@@ -34,4 +34,25 @@ def test_bench_prints_one_contract_line(gpu):
     assert rf["traffic"] is None or rf["traffic"] > 0
     cb = d["cpu_baseline"]
     assert cb["unit"] == d["unit"] and cb["kind"] in ("port", "reference") and cb["cores"] >= 1
-    assert d["value"] > 0 and cb["value"] > 0
+    assert d["value"] > 0 and cb["value"] > 0 and cb["value_1thread"] > 0
+    assert d["verified"] is True and d["ranks"] == 1 and d["timed_regions"] >= 1
+    lo, hi = d["ms_per_step_range"]
+    assert lo <= d["ms_per_step"] <= hi
+
+
+def test_bench_gpus2_gloo_spawns_two_ranks(gpu):
+    """`bench.py --gpus 2` with no external launcher starts two ranks itself
+    (gloo: both share the box's one GPU) and reports them"""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--dist-backend", "gloo", "--min-seconds", "0.02"],
+                       capture_output=True, text=True, timeout=600, cwd=REPO,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks"] == 2 and d["rccl_ranks"] == 0
+    assert d["verified"] is True and d["verification"]["gather"].startswith("rank 0 holds")
+    assert "over 2 MI355X" in d["config"]["workload"]
+    assert d["config"]["launcher"].startswith("bench.py --gpus")
+    assert len(d["per_rank_ms_per_step"]) == 2 and d["cpu_baseline"] is None

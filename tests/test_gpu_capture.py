@@ -19,10 +19,29 @@ pytestmark = pytest.mark.gpu
 BIN = dada.BIN_DIR
 
 
-def test_udp_capture_to_spectra(gpu, tmp_path):
+def far_future_copy(df_path, ck_path, ahead):
+    """insert, mid-stream, a copy of one frame whose timestamp lies `ahead`
+    frames later (a corrupt or far-future header)"""
+    dfs = np.fromfile(df_path, np.uint8).reshape(-1, npo.DF_BYTES)
+    ck = np.fromfile(ck_path, np.uint8)
+    i = len(dfs) // 2
+    h = dada.df_decode(dfs[i].tobytes())
+    tot = h.idf + ahead
+    bad = dfs[i].copy()
+    bad[:64] = np.frombuffer(dada.df_encode(tot % 250000, h.sec + 27 * (tot // 250000), h.valid, h.epoch,
+                                            h.beam, h.freq), np.uint8)
+    np.concatenate([dfs[:i], bad[None], dfs[i:]]).tofile(df_path)
+    np.concatenate([ck[:i], ck[i:i + 1], ck[i:]]).tofile(ck_path)
+
+
+@pytest.mark.parametrize("inject", [False, True])
+def test_udp_capture_to_spectra(gpu, tmp_path, inject):
     nchunk, block_ndf, nblk = 8, 64, 4
     g, payload, df, ck = make_stream(tmp_path, nchunk=nchunk, nblk=nblk, block_ndf=block_ndf,
                                      window=block_ndf * nchunk * 3 // 2, seed=11)
+    if inject:  # one frame 10 blocks (640 frames) ahead, past the far limit 64 + 2 x 256:
+        # dropped, no block switch (capture.c:491-508)
+        far_future_copy(df, ck, 10 * block_ndf)
     hdr = tmp_path / "hdr.txt"
     hdr.write_text(f"HDR_SIZE 4096\nNBIT 16\nNDIM 2\nNPOL 2\nNCHAN {nchunk * 7}\nNCHUNK {nchunk}\n"
                    "NCHAN_CHUNK 7\nNSAMP_DF 128\nBYTE_ORDER BE\nTSAMP 0.84375\n")
@@ -66,6 +85,7 @@ def test_udp_capture_to_spectra(gpu, tmp_path):
     dfs = np.fromfile(df, np.uint8).reshape(-1, npo.DF_BYTES)
     chunk = np.fromfile(ck, np.uint8)
     assert sp.shape[0] == nblk, cap_log
+    assert f", {int(inject)} far ahead," in cap_log
     idf, sec = 249990, 54
     for b in range(nblk):
         want = np.zeros(g.block_bytes, np.uint8)

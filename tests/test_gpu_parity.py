@@ -405,3 +405,51 @@ def test_back_to_back_async_integrations(gpu, fuse):
         os.environ.pop("B2P_FUSE", None)
     for k in range(7):
         assert same_bits(got[k], co.power(g, hosts[k % 3])), k
+
+
+def test_push_failure_part_way_marks_context_failed(gpu, monkeypatch):
+    """A host-span push that fails after its first staging chunk was summed
+    leaves the integration unknown: the call reports the failure and every
+    later call on the context returns B2P_EFAILED until b2p_close (the
+    reference would have exit(-1)ed, cudautil.cuh:29-41).  The failure is
+    injected at staging chunk 2 of a 4-chunk span."""
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=4096)      # 4 MiB per integration
+    buf = co.fill_synthetic(g, g.block_bytes, SEED, 0, 0)
+    monkeypatch.setenv("B2P_STAGE_MIB", "1")
+    monkeypatch.setenv("B2P_INJECT_PUSH_FAIL", "2")
+    it = paf_b2p.Integrator(to_b2p(g))
+    with pytest.raises(paf_b2p.B2PError) as e:
+        it.push(buf)
+    assert e.value.code == L.B2P_EHIP and "injected" in str(e.value)
+    for call in (lambda: it.push(buf), lambda: it.finish(allow_partial=True), it.sync,
+                 lambda: it.set_timing(2), it.fence):
+        with pytest.raises(paf_b2p.B2PError) as e:
+            call()
+        assert e.value.code == L.B2P_EFAILED
+    assert "injected" in L.lib().b2p_last_error(it._ctx).decode()   # the first failure's text
+    it.close()
+    monkeypatch.delenv("B2P_INJECT_PUSH_FAIL")
+    with paf_b2p.Integrator(to_b2p(g)) as it2:                     # a fresh context is fine
+        it2.push(buf)
+        assert same_bits(it2.finish(), co.power(g, buf))
+
+
+def test_fused_host_output_after_finish_async_host(gpu, monkeypatch):
+    """B2P_FUSE=1: a fused integrate whose spectrum goes to the host follows
+    a finish_async to the host; the carried finalize of the first and the
+    fused finalize of the second must not share the staging output"""
+    monkeypatch.setenv("B2P_FUSE", "1")
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=8192)
+    bufs = [co.fill_synthetic(g, g.block_bytes, SEED, 5, k) for k in range(3)]
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        ds = [it.upload(b) for b in bufs]
+        outs = [np.zeros(g.nout, np.float32) for _ in range(3)]
+        it.push(ds[0])
+        it.finish_async(outs[0].ctypes.data, False)
+        it.integrate(ds[1], outs[1].ctypes.data, False)
+        it.integrate(ds[2], outs[2].ctypes.data, False)
+        it.sync()
+        for d in ds:
+            d.free()
+    for b, o in zip(bufs, outs):
+        assert same_bits(o, co.power(g, b))

@@ -1,0 +1,65 @@
+"""The hosts build against PSRDADA's own API (CPU, compile-only).
+
+INTEGRATION.md tells a maintainer who keeps PSRDADA's dada_db / dada_dbdisk
+to build paf_baseband2power and paf_diskdb against the real libpsrdada
+(-DB2P_PSRDADA, PSRDADA's include directory, -lpsrdada).  libpsrdada is not
+in this image, so this test compiles both hosts with -DB2P_PSRDADA against
+declarations-only stand-ins for PSRDADA's headers (tests/c/psrdada_api,
+restated from SURVEY.md Appendix A) and checks the objects' undefined DADA
+symbols: every one must be in the PSRDADA subset the reference's hosts call
+(Appendix A "writer subset" + "reader subset") or ipcbuf_get_nbufs; none of
+libpafdada's extensions (device rings, read depth, dada_hdu_open_read,
+ascii_header_del, ipcbuf_get_buffer) may remain.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HOSTS = os.path.join(REPO, "paf-baseband2power_amd", "csrc", "host")
+API = os.path.join(REPO, "tests", "c", "psrdada_api")
+
+# the calls the reference makes (writer) and the reader
+# half its baseband2power stage needs
+PSRDADA_SUBSET = {
+    "dada_hdu_create", "dada_hdu_set_key", "dada_hdu_connect", "dada_hdu_lock_write",
+    "dada_hdu_unlock_write", "dada_hdu_disconnect", "dada_hdu_destroy", "ipcbuf_get_bufsz",
+    "ipcbuf_enable_sod", "ipcbuf_disable_sod", "ipcbuf_get_next_write", "ipcbuf_mark_filled",
+    "ipcio_open_block_write", "ipcio_close_block_write", "fileread", "ascii_header_set",
+    "multilog_open", "multilog_add", "multilog_close", "multilog",
+    "dada_hdu_lock_read", "dada_hdu_unlock_read", "ipcbuf_get_next_read", "ipcbuf_mark_cleared",
+    "ipcio_open_block_read", "ipcio_close_block_read", "ipcbuf_eod", "ascii_header_get",
+    "ipcbuf_get_nbufs",  # PSRDADA ipcbuf.h; walks the blocks to pin them (dada_cuda_dbregister role)
+}
+DADA_PREFIX = re.compile(r"^(dada_|ipcbuf_|ipcio_|ascii_header_|multilog|fileread)")
+
+
+def undefined(obj):
+    out = subprocess.run(["nm", "-u", str(obj)], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+
+
+@pytest.mark.parametrize("host", ["paf_baseband2power", "paf_diskdb"])
+def test_host_compiles_against_psrdada_subset(host, tmp_path):
+    obj = tmp_path / f"{host}.o"
+    r = subprocess.run(["gcc", "-c", "-O2", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
+                        "-DB2P_PSRDADA", "-I", API, "-I", os.path.join(REPO, "include"),
+                        os.path.join(HOSTS, f"{host}.c"), "-o", str(obj)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    dada = {s for s in undefined(obj) if DADA_PREFIX.match(s)}
+    assert dada, "no DADA calls found"
+    assert dada <= PSRDADA_SUBSET, sorted(dada - PSRDADA_SUBSET)
+
+
+def test_default_build_still_uses_libpafdada_extensions(tmp_path):
+    # the default build keeps the GPU-resident ring path (ipcbuf_get_device,
+    # read depth 2), which the PSRDADA build drops
+    obj = tmp_path / "b2p.o"
+    subprocess.run(["gcc", "-c", "-O2", "-std=gnu11", "-D_GNU_SOURCE", "-I", os.path.join(REPO, "include"),
+                    os.path.join(HOSTS, "paf_baseband2power.c"), "-o", str(obj)], check=True)
+    u = undefined(obj)
+    assert {"ipcbuf_get_device", "ipcbuf_set_read_depth"} <= u

@@ -33,12 +33,11 @@ for s in $STEPS; do
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -q -rf ;;
     bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
+    benchdrv) run bench_drv 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchnf) run bench_nofuse 600 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-fuse ;;
     bench5) run bench_c5 600 python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
     benchbmf) run bench_bmf 600 python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
-    bench2gloo) run bench_2gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-            --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 10 --warmup 2 \
-            --dist-backend gloo ;;
+    bench2gloo) run bench_2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 2 --dist-backend gloo ;;
     benchdist1) run bench_dist1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist ;;
@@ -51,8 +50,7 @@ for s in $STEPS; do
     benchsplit) run bench_split1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29513 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist --split time &&
-          run bench_split2gloo 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-            --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --steps 10 --warmup 2 \
+          run bench_split2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 2 \
             --dist-backend gloo --split time ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
     asm) run bench_assemble 600 python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
