@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit; a fault/abort/timeout (exit other
 # than 0 or 1) ends the script at once -- nothing further touches the GPU.
 #   usage: tools/gpu_check.sh [steps...]
-#   steps: smoke tests bench benchnf bench5 benchbmf bench3 bench2gloo benchdist1 distcost benchsplit
+#   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf
 cd "$(dirname "$0")/.." || exit 2
@@ -38,6 +38,14 @@ for s in $STEPS; do
     bench5) run bench_c5 600 python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
     benchbmf) run bench_bmf 600 python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
     bench2gloo) run bench_2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 2 --dist-backend gloo ;;
+    bench4gloo) run bench_4gloo 600 python3 bench.py --gpus 4 --steps 10 --warmup 2 --dist-backend gloo ;;
+    cpunproc) NCPU=$(python3 -c 'import os; print(os.cpu_count())')  # nproc follows OMP_NUM_THREADS
+              run cpu_nproc 300 env OMP_NUM_THREADS=$NCPU OMP_PROC_BIND=close OMP_PLACES=threads \
+              OMP_WAIT_POLICY=passive python3 oracle/cpu_baseline.py \
+              '{"nbit":8,"nchan_chunk":256,"nsamp_df":1}' 6 20181105 &&
+              run cpu_16 300 env OMP_NUM_THREADS=16 OMP_PROC_BIND=close OMP_PLACES=cores \
+              OMP_WAIT_POLICY=active python3 oracle/cpu_baseline.py \
+              '{"nbit":8,"nchan_chunk":256,"nsamp_df":1}' 6 20181105 ;;
     benchdist1) run bench_dist1 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
             --master-addr 127.0.0.1 --master-port 29512 bench.py --steps 20 --warmup 2 \
             --cpu-seconds 0 --force-dist ;;
@@ -97,15 +105,15 @@ for s in $STEPS; do
           run tune_bmf 600 python3 tools/tune.py --config bmf --quick ;;
     tunebmf) run tune_bmf2 600 python3 tools/tune.py --config bmf --threads 168,256,336,448,512 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
-            -- python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 ;;
+            -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
-            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 &&
+            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
-            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 ;;
+            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
     pmc5) run pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run \
-            -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 &&
+            -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run \
-            -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 &&
+            -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run \
             -- python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
     profbmf) run prof_bmf 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bmf" -o run \
