@@ -69,6 +69,22 @@ NBLOCKS = 4
 BASELINE_CONFIG = {"c2": "configs[1]", "c5": "configs[4]", "c3": "configs[2]", "bmf": "reference-native"}
 
 
+def baseline_config(config: str, world: int, split: bool) -> str:
+    """which BASELINE.json config this run is: configs[1] is one 256-ch
+    sub-band on 1 GPU, configs[3] four of them gathered to rank 0,
+    configs[4] eight 1024-ch sub-bands; other world sizes run the same
+    per-GPU workload (weak scaling)"""
+    if split:
+        return f"{BASELINE_CONFIG[config]}, one integration split over {world} GPU(s)"
+    if world == 1:
+        return BASELINE_CONFIG[config]
+    if config == "c2":
+        return "configs[3]" if world == 4 else f"configs[1] per GPU x{world} (configs[3] is x4)"
+    if config == "c5":
+        return "configs[4]" if world == 8 else f"configs[4] per GPU x{world} (configs[4] is x8)"
+    return f"{BASELINE_CONFIG[config]} per GPU x{world}"
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1, help="ranks, one process per GPU")
@@ -500,9 +516,14 @@ def main(argv=None) -> int:
             "timed_seconds": round(sum(els_max), 4),
             "ms_per_step_range": [round(min(els_max) / K * 1e3, 4), round(max(els_max) / K * 1e3, 4)],
             "per_rank_ms_per_step": per_rank_ms,
+            # whole-job HBM read rate and its share of world x 8 TB/s
+            # ("% of 8x roofline" for configs[4])
+            "aggregate_hbm_gbs": round(value * 1e6 * (geom.nbit // 8) * 2 / 1e9, 1),
+            "aggregate_frac_of_world_peak": round(value * 1e6 * (geom.nbit // 8) * 2 / 1e9
+                                                  / (HBM_PEAK_GBS * (1 if split else world)), 4),
             "config": {
                 "workload": workload_label(a.config, geom_desc, world, split, host_mode),
-                "baseline_config": BASELINE_CONFIG[a.config],
+                "baseline_config": baseline_config(a.config, world, split),
                 "nchan": int(paf_b2p.geometry.nchan(geom)),
                 "npol": int(geom.npol),
                 "nsamp_int": int(full_nsamp if split else geom.nsamp_int),

@@ -347,6 +347,9 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   for (auto &e : c->fence_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
       return fail(set_err(c, B2P_EHIP, "hipEventCreate"));
+  // the timing region's pair too, so opening the first region costs nothing
+  if (hipEventCreate(&c->region_a) != hipSuccess || hipEventCreate(&c->region_b) != hipSuccess)
+    return fail(set_err(c, B2P_EHIP, "hipEventCreate"));
   // two replica sets, then the two 4-B tickets (zeroed together; every
   // finalize leaves its set and ticket zero again)
   const size_t set_words = (size_t)c->nrep * c->nout;

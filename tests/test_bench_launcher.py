@@ -110,3 +110,11 @@ def test_bad_counts_rejected():
     for args in (["--gpus", "0"], ["--steps", "0"]):
         r = _run(args)
         assert r.returncode == 2 and "must be >= 1" in r.stderr
+
+
+def test_baseline_config_names():
+    assert bench.baseline_config("c2", 1, False) == "configs[1]"
+    assert bench.baseline_config("c2", 4, False) == "configs[3]"
+    assert bench.baseline_config("c5", 8, False) == "configs[4]"
+    assert bench.baseline_config("c2", 8, False).startswith("configs[1] per GPU x8")
+    assert "split over 2" in bench.baseline_config("c2", 2, True)
