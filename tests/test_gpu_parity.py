@@ -171,6 +171,33 @@ def test_full_config2_block_vs_c_oracle(gpu):
         assert same_bits(out, co.power(g, host, nthreads=16))
 
 
+def test_full_config3_pinned_host_vs_c_oracle(gpu):
+    """BASELINE configs[2]: 1024 ch x 2 pol int8 (4 GiB per integration) from
+    a registered (pinned) host buffer, H2D overlapped with the kernel through
+    the staging pair, pushed in three ragged frame-whole pieces; then the
+    same context integrates the next block from the device (the fused
+    path), so host and device spans share one context"""
+    g = npo.Geom(nbit=8, nchan_chunk=1024)
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        d = it.alloc(g.block_bytes)
+        it.fill_synthetic(d, SEED, 3, 0)
+        host = it.download(d)
+        it.register_host(host)
+        try:
+            cuts = [0, 777 * g.frame_bytes, g.block_bytes - 5 * g.frame_bytes, g.block_bytes]
+            for a, b in zip(cuts, cuts[1:]):
+                it.push(host[a:b])
+            out = it.finish()
+        finally:
+            it.unregister_host(host)
+        it.fill_synthetic(d, SEED, 3, 1)
+        nxt = it.integrate(d)
+        host2 = it.download(d)
+        d.free()
+    assert same_bits(out, co.power(g, host, nthreads=16))
+    assert same_bits(nxt, co.power(g, host2, nthreads=16))
+
+
 def test_full_bmf_block_vs_c_oracle(gpu):
     # reference-native: 8192 DF x 48 chunks x 7168 B = 2818572288 B
     g = npo.BMF
