@@ -164,12 +164,19 @@ def check_world(a, world: int) -> str | None:
 # --------------------------------------------------------------------------
 # labels
 # --------------------------------------------------------------------------
-def workload_label(config: str, geom_desc: str, world: int, split: bool, host_mode: bool) -> str:
+def workload_label(config: str, geom_desc: str, world: int, split: bool, host_mode: bool,
+                   ndev: int | None = None) -> str:
+    """what ran, on how many GPUs: ndev (the GPUs the ranks map to) below
+    world means ranks sharing GPUs, a gloo rehearsal of the plumbing"""
+    ndev = world if ndev is None else ndev
     where = "pinned host buffer, H2D overlapped" if host_mode else "HBM-resident"
+    over = (f"{world} MI355X" if ndev >= world
+            else f"{world} ranks sharing {ndev} MI355X (rehearsal, not a scaling run)")
     if split:
         return (f"1 sub-band, {geom_desc}, {where}; one integration split by time over "
-                f"{world} MI355X, exact partials reduced to rank 0")
-    return (f"{world} sub-band(s), {geom_desc} each, {where}, 1 per MI355X over {world} MI355X"
+                f"{over}, exact partials reduced to rank 0")
+    return (f"{world} sub-band(s), {geom_desc} each, {where}, "
+            + (f"1 per MI355X over {over}" if ndev >= world else f"over {over}")
             + (", spectra gathered to rank 0" if world > 1 else ""))
 
 
@@ -522,7 +529,8 @@ def main(argv=None) -> int:
             "aggregate_frac_of_world_peak": round(value * 1e6 * (geom.nbit // 8) * 2 / 1e9
                                                   / (HBM_PEAK_GBS * (1 if split else world)), 4),
             "config": {
-                "workload": workload_label(a.config, geom_desc, world, split, host_mode),
+                "workload": workload_label(a.config, geom_desc, world, split, host_mode,
+                                           min(world, torch.cuda.device_count())),
                 "baseline_config": baseline_config(a.config, world, split),
                 "nchan": int(paf_b2p.geometry.nchan(geom)),
                 "npol": int(geom.npol),

@@ -106,6 +106,12 @@ def test_labels_follow_world(world, split):
         assert "gather of spectra to rank 0" in p
 
 
+def test_label_of_ranks_sharing_a_gpu():
+    w = bench.workload_label("c2", "256 ch x 2 pol int8", 8, False, False, ndev=1)
+    assert "8 ranks sharing 1 MI355X (rehearsal" in w and "1 per MI355X" not in w
+    assert "over 8 MI355X" in bench.workload_label("c2", "x", 8, False, False, ndev=8)
+
+
 def test_bad_counts_rejected():
     for args in (["--gpus", "0"], ["--steps", "0"]):
         r = _run(args)
