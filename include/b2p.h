@@ -202,7 +202,10 @@ uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
  * ncclCommInitAll + ncclGather (rccl.h:236,745), enqueued on every member's
  * stream behind its finalize; valid on ctxs[0] after b2p_group_sync().
  * mode 0 = RCCL; mode 1 = peer copies (test rigs where members share a
- * device, which RCCL refuses).  All members need the same nout. */
+ * device, which RCCL refuses).  All members need the same nout.  A member's
+ * spectra / sums buffer must not be rewritten before b2p_group_sync()
+ * (mode 1 copies it on ctxs[0]'s stream).  A member context in the failed
+ * state makes the collective return B2P_EFAILED. */
 typedef struct b2p_group b2p_group_t;
 int b2p_group_open(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode);
 int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);

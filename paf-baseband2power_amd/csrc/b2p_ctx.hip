@@ -651,6 +651,7 @@ void *b2p_internal_stream(b2p_ctx_t *c) { return c ? (void *)c->stream : nullptr
 
 int b2p_internal_flush(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
+  LIVE(c);  // a group collective over a failed member reports it
   CK(c, hipSetDevice(c->device));
   return flush_pending(c);
 }
