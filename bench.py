@@ -303,8 +303,12 @@ def main(argv=None) -> int:
         elem0 = first * paf_b2p.geometry.frame_bytes(geom) // (geom.nbit // 8)
     my_geom = {f: int(getattr(geom, f)) for f, _ in geom._fields_ if f != "reserved"}
     K = a.steps
-    # with one visible GPU every rank maps to it (paf_baseband2power.cu:89-90)
-    it = paf_b2p.Integrator(geom, device=D.device_of(local))
+    # rank r on GPU r; with one visible GPU every rank maps to it
+    # (paf_baseband2power.cu:89-90).  torch's current device follows, so
+    # its tensors (spectra, partials) live where the integrator runs
+    dev = D.device_of(local)
+    torch.cuda.set_device(dev)
+    it = paf_b2p.Integrator(geom, device=dev)
     nout, bb = it.nout, it.block_bytes
     if rccl:
         # one stream for the integrator and torch: the collective after the
