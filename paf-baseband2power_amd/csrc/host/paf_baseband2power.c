@@ -20,10 +20,11 @@
  *
  * DADA library: built by default against libpafdada (include/b2p_dada.h).
  * With -DB2P_PSRDADA it includes PSRDADA's own headers and calls only the
- * PSRDADA subset the reference's hosts use plus
- * ipcbuf_get_nbufs, so it links against the real libpsrdada
- * (INTEGRATION.md); GPU-resident rings and two blocks in flight, both
- * libpafdada extensions, are then off.
+ * PSRDADA subset the reference's hosts use, touching
+ * no DADA struct but dada_hdu_t's data_block / header_block, so it links
+ * against the real libpsrdada; GPU-resident rings, two
+ * blocks in flight and pinning every ring block up front (libpafdada
+ * extensions) are then off, and blocks are pinned when first seen.
  */
 #include <getopt.h>
 #include <inttypes.h>
@@ -51,6 +52,7 @@
 #define MSTR_LEN 512 /* paf_baseband2power.cuh:4 */
 #define TSAMP_BMF_US (27.0 / 32.0) /* README.md:2 */
 #define MAX_SUB 64
+#define MAX_PIN 64 /* ring blocks pinned per input ring */
 #define kWarm 8 /* outputs before the steady-state clock starts (FINISH line) */
 
 typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
@@ -79,6 +81,8 @@ typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
   uint64_t rbufsz;
   int locked;
   int ondev; /* input blocks are in GPU memory (dada_db -g) */
+  char *pinned[MAX_PIN]; /* host ring blocks registered for DMA (dada_cuda_dbregister role) */
+  int npinned;
 } sub_t;
 
 static void usage(void) {
@@ -205,6 +209,20 @@ static int ring_device(dada_hdu_t *h) {
 #endif
 }
 
+/* Register a host ring block for DMA once, the first time it is seen (the
+ * default build registers every block up front, so this finds them all). */
+static void pin_block(sub_t *s, char *blk, multilog_t *log) {
+  if (s->ondev || !blk) return;
+  for (int i = 0; i < s->npinned; i++)
+    if (s->pinned[i] == blk) return;
+  if (s->npinned == MAX_PIN) return; /* unpinned blocks still work, at pageable rate */
+  if (b2p_register_host(s->ctx, blk, s->rbufsz) != B2P_OK) {
+    multilog(log, LOG_INFO, "register block: %s", b2p_last_error(s->ctx));
+    return;
+  }
+  s->pinned[s->npinned++] = blk;
+}
+
 /* next input block, or NULL at the end of the transfer (checked with
  * ipcbuf_eod first, so a reader never waits on a ring whose transfer ended) */
 static char *next_block(dada_hdu_t *h, uint64_t *bytes) {
@@ -290,6 +308,7 @@ static void *worker(void *arg) {
       if (rc == B2P_OK) rc = b2p_sync(s->ctx);
       ipcio_close_block_read(s->in->data_block, bytes);
     } else {
+      pin_block(s, blk, sh->log);
       rc = b2p_push(s->ctx, blk, bytes, 0); /* returns once the block is copied */
       ipcio_close_block_read(s->in->data_block, bytes);
       if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
@@ -411,6 +430,7 @@ static void *worker_split(void *arg) {
     if (w->r == 0) {
       sh->blk_bytes = 0;
       sh->blk = next_block(s0->in, &sh->blk_bytes);
+      pin_block(s0, sh->blk, sh->log);
       sh->have[0] = !sh->blk ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
     }
     pthread_barrier_wait(&sh->bar);
@@ -619,10 +639,12 @@ int main(int argc, char *argv[]) {
       multilog(log, LOG_INFO, "input ring %x is GPU-resident (device %d): no H2D copy",
                (unsigned)s->key, ring_dev);
     }
-    /* pin the input ring's blocks for DMA (dada_cuda_dbregister role) */
+#if DEVICE_RINGS
+    /* pin the input ring's blocks for DMA up front (dada_cuda_dbregister
+     * role), so no first-use registration lands on an integration */
     for (uint64_t i = 0; !s->ondev && i < ipcbuf_get_nbufs(data_buf(s->in)); i++)
-      if (b2p_register_host(s->ctx, data_buf(s->in)->buffer[i], s->rbufsz) != B2P_OK)
-        multilog(log, LOG_INFO, "register block %" PRIu64 ": %s", i, b2p_last_error(s->ctx));
+      pin_block(s, ipcbuf_get_buffer(data_buf(s->in), i), log);
+#endif
   }
   b2p_info_t info;
   b2p_get_info(sub[0].ctx, &info);
@@ -758,9 +780,7 @@ done:
     if (s->ctx) {
       if (s->part_dev) b2p_dev_free(s->ctx, s->part_dev);
       if (r == 0 && sh.root_sum) b2p_dev_free(s->ctx, sh.root_sum);
-      for (uint64_t i = 0; !s->ondev && s->in && s->in->data_block &&
-                           i < ipcbuf_get_nbufs(data_buf(s->in)); i++)
-        b2p_unregister_host(s->ctx, data_buf(s->in)->buffer[i]);
+      for (int i = 0; i < s->npinned; i++) b2p_unregister_host(s->ctx, s->pinned[i]);
       if (r == 0 && sh.spec_host) b2p_unregister_host(s->ctx, sh.spec_host);
       if (s->spec_dev) b2p_dev_free(s->ctx, s->spec_dev);
       if (r == 0 && sh.root_dev) b2p_dev_free(s->ctx, sh.root_dev);

@@ -49,8 +49,8 @@ def read_conf(path: str) -> dict:
     return c
 
 
-def _bin(name: str) -> str:
-    return os.path.join(dada.BIN_DIR, name)
+def _bin(name: str, bin_dir: str | None = None) -> str:
+    return os.path.join(bin_dir or dada.BIN_DIR, name)
 
 
 def _ring_device(gpu: int, r: int) -> int:
@@ -65,7 +65,7 @@ def _ring_device(gpu: int, r: int) -> int:
 def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
-        device_ring: bool = False, split: int = 1) -> list:
+        device_ring: bool = False, split: int = 1, bin_dir: str | None = None) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
     sub-bands and gathers their spectra to its first GPU).
@@ -105,7 +105,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
             out = (outfiles[r] if outfiles else os.path.join(sub_dir, "power.dada"))
             outs.append(out)
             dfile = datafile if isinstance(datafile, str) else datafile[r]
-            b2p_cmd = [_bin("paf_baseband2power"), "-a", f"{kin:x}", "-b", f"{kout:x}",
+            b2p_cmd = [_bin("paf_baseband2power", bin_dir), "-a", f"{kin:x}", "-b", f"{kout:x}",
                        "-c", sub_dir, "-d", str(gpu + r), "-p", str(npol_out)]
             if layout:
                 b2p_cmd += ["-f", layout]
@@ -117,7 +117,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
                                           stderr=subprocess.PIPE))
             procs.append(subprocess.Popen(b2p_cmd, stderr=subprocess.PIPE))
             procs.append(subprocess.Popen(
-                [_bin("paf_diskdb"), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
+                [_bin("paf_diskdb", bin_dir), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
                  "-c", os.path.basename(dfile), "-d", hdr, "-e", str(c["diskdb_sod"])],
                 stderr=subprocess.PIPE))
         t_end = time.time() + timeout

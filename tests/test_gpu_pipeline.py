@@ -100,3 +100,30 @@ def test_int8_header_layout_two_subbands(gpu, tmp_path):
             assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk).view(np.uint32))
         assert abs(dada.header_get(hdr, "TSAMP", "%lf") - 0.84375 * (1 << 16)) < 1e-6
         assert dada.header_get(hdr, "NCHAN", "%d") == 256
+
+
+def test_psrdada_mode_host_pipeline(gpu, tmp_path):
+    """The PSRDADA-mode hosts (bin/psrdada_api: -DB2P_PSRDADA, compiled
+    against the Appendix A declarations, linked against libpafdada) run the
+    three-process chain: header read with ipcbuf_get_next_read /
+    mark_cleared, ring blocks pinned as first seen, end of data from
+    ipcbuf_eod, no libpafdada extension.  Spectra equal the oracle."""
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 16)
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nUTC_START 2018-11-05-00:00:00\n"
+                     "NBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\nTSAMP 0.84375\n")
+    payload = co.fill_synthetic(g, g.block_bytes * 3 + g.frame_bytes * 7, SEED, 6, 0)
+    f = tmp_path / "sb.dada"
+    dada.write_dada_file(str(f), "x 1\n", payload)
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 16, 1, 1024, 256, 0x6e40, 0x6e50, str(hfile))
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, str(f), timeout=600,
+                        bin_dir=os.path.join(dada.BIN_DIR, "psrdada_api"))
+    hdr, sp = spectra(outs[0], 256)
+    assert sp.shape == (3, 256)
+    for i in range(3):
+        blk = payload[i * g.block_bytes:(i + 1) * g.block_bytes]
+        assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk).view(np.uint32))
+    assert dada.header_get(hdr, "NBIT", "%d") == 32
+    log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
+    assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log

@@ -7,9 +7,9 @@ in this image, so this test compiles both hosts with -DB2P_PSRDADA against
 declarations-only stand-ins for PSRDADA's headers (tests/c/psrdada_api,
 restated from SURVEY.md Appendix A) and checks the objects' undefined DADA
 symbols: every one must be in the PSRDADA subset the reference's hosts call
-(Appendix A "writer subset" + "reader subset") or ipcbuf_get_nbufs; none of
-libpafdada's extensions (device rings, read depth, dada_hdu_open_read,
-ascii_header_del, ipcbuf_get_buffer) may remain.
+(Appendix A "writer subset" + "reader subset"); none of libpafdada's
+extensions (device rings, read depth, dada_hdu_open_read, ascii_header_del,
+ipcbuf_get_nbufs / ipcbuf_get_buffer) may remain.
 """
 import os
 import re
@@ -32,7 +32,6 @@ PSRDADA_SUBSET = {
     "multilog_open", "multilog_add", "multilog_close", "multilog",
     "dada_hdu_lock_read", "dada_hdu_unlock_read", "ipcbuf_get_next_read", "ipcbuf_mark_cleared",
     "ipcio_open_block_read", "ipcio_close_block_read", "ipcbuf_eod", "ascii_header_get",
-    "ipcbuf_get_nbufs",  # PSRDADA ipcbuf.h; walks the blocks to pin them (dada_cuda_dbregister role)
 }
 DADA_PREFIX = re.compile(r"^(dada_|ipcbuf_|ipcio_|ascii_header_|multilog|fileread)")
 
@@ -63,3 +62,37 @@ def test_default_build_still_uses_libpafdada_extensions(tmp_path):
                     os.path.join(HOSTS, "paf_baseband2power.c"), "-o", str(obj)], check=True)
     u = undefined(obj)
     assert {"ipcbuf_get_device", "ipcbuf_set_read_depth"} <= u
+
+
+def test_psrdada_mode_diskdb_runs(tmp_path):
+    """The PSRDADA-mode paf_diskdb (bin/psrdada_api: compiled against the
+    Appendix A declarations, linked against libpafdada, whose calls it
+    shares) writes a file into a ring byte for byte, header ring included,
+    with the short last block ending the transfer (diskdb.cu:69-121)"""
+    import numpy as np
+
+    from paf_b2p import dada
+    exe = os.path.join(dada.BIN_DIR, "psrdada_api", "paf_diskdb")
+    assert os.path.exists(exe), "make -C paf-baseband2power_amd all builds it"
+    key = 0x6e00 + (os.getpid() % 64) * 4
+    dada.destroy_ring(key)
+    bufsz = 32 * 1024
+    dada.create_ring(key, 4, bufsz, 1)
+    try:
+        payload = np.random.default_rng(5).integers(0, 256, bufsz * 5 // 2, dtype=np.uint8)
+        src = tmp_path / "obs.dada"
+        dada.write_dada_file(str(src), "SKIPPED 1\n", payload)
+        hdr = tmp_path / "header.txt"
+        hdr.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\n")
+        out = tmp_path / "out.dada"
+        sink = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_dbdisk"), "-k", f"{key:x}", "-o",
+                                 str(out)], stderr=subprocess.PIPE)
+        src_p = subprocess.run([exe, "-a", f"{key:x}", "-b", str(tmp_path), "-c", "obs.dada", "-d",
+                                str(hdr), "-e", "1"], capture_output=True, text=True, timeout=60)
+        assert src_p.returncode == 0, src_p.stderr
+        assert sink.wait(60) == 0, sink.stderr.read()
+        h, data = dada.read_dada_file(str(out))
+        assert h.decode() == hdr.read_text()
+        assert np.array_equal(data, payload)
+    finally:
+        dada.destroy_ring(key)
