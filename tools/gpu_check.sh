@@ -119,9 +119,9 @@ for s in $STEPS; do
     profbmf) run prof_bmf 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bmf" -o run \
             -- python3 bench.py --config bmf --steps 20 --warmup 3 --cpu-seconds 0 ;;
     pmcbmf) run pmc_fetch_bmf 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_bmf" -o run \
-            -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 &&
+            -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_bmf 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_bmf" -o run \
-            -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 ;;
+            -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
