@@ -90,7 +90,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="ranks, one process per GPU")
     ap.add_argument("--steps", type=int, default=50, help="integrations per timed region")
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--min-seconds", type=float, default=0.5,
+    ap.add_argument("--min-seconds", type=float, default=1.0,
                     help="repeat the K-step region until this much timed work has run")
     ap.add_argument("--config", default="c2", choices=["c2", "c5", "bmf", "c3"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
