@@ -124,3 +124,42 @@ def test_baseline_config_names():
     assert bench.baseline_config("c5", 8, False) == "configs[4]"
     assert bench.baseline_config("c2", 8, False).startswith("configs[1] per GPU x8")
     assert "split over 2" in bench.baseline_config("c2", 2, True)
+
+
+def test_chunked_oracle_equals_one_shot():
+    """bench.py's verification feeds the oracle whole-frame chunks of <= 256
+    MiB; the exact uint64 sums make that equal to one pass (BMF frames of
+    344 064 B do not divide 256 MiB, so the chunk is rounded down to frames)"""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import b2p_oracle as npo
+    import oracle_c as co
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=128 * 900)
+    buf = co.fill_synthetic(g, g.block_bytes, 20181105, 0, 3)       # 310 MB: two chunks
+    geom = g.asdict()
+    got = bench.oracle_spectrum(geom, lambda off, n: buf[off:off + n], g.block_bytes, 4)
+    assert np.array_equal(got.view(np.uint32), co.power(g, buf, nthreads=4).view(np.uint32))
+    # and the host-regenerated blocks of the time-split check equal the block itself
+    rd = bench.synthetic_reader(geom, 0, 3, 4)
+    assert np.array_equal(rd(g.frame_bytes * 5, g.frame_bytes * 2),
+                          buf[g.frame_bytes * 5:g.frame_bytes * 7])
+
+
+def test_cpu_share_parsing(monkeypatch, tmp_path):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import cpu_baseline as cb
+    f = tmp_path / "cpu.max"
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        return real_open(f if path == "/sys/fs/cgroup/cpu.max" else path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", fake_open)
+    f.write_text("1600000 100000\n")
+    assert cb.cgroup_cpus() == 16.0
+    assert cb.effective_cpus() == min(16, len(os.sched_getaffinity(0)))
+    f.write_text("max 100000\n")
+    assert cb.cgroup_cpus() is None
+    assert cb.effective_cpus() == len(os.sched_getaffinity(0))
+    env = cb.child_env(16)
+    assert env["OMP_NUM_THREADS"] == "16" and env["OMP_PLACES"] == "cores"
