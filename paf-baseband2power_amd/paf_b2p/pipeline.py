@@ -231,10 +231,15 @@ def main(argv=None) -> int:
                     help="split each integration by time over N GPUs (exact partials reduced)")
     ap.add_argument("--device-ring", action="store_true",
                     help="input ring blocks in GPU memory (dada_db -g): no H2D in the integrator")
+    ap.add_argument("--bin-dir", default=None,
+                    help="where paf_diskdb / paf_baseband2power live (e.g. bin/psrdada: the "
+                         "PSRDADA builds, INTEGRATION.md); paf_dbdisk stays the default one")
     a = ap.parse_args(argv)
+    if a.bin_dir and a.device_ring:
+        ap.error("--device-ring needs libpafdada's hosts (GPU-resident rings are an extension)")
     files = a.dfname if a.subbands > 1 or a.gather else a.dfname[0]
     outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean,
-               gather=a.gather, device_ring=a.device_ring, split=a.split)
+               gather=a.gather, device_ring=a.device_ring, split=a.split, bin_dir=a.bin_dir)
     print("\n".join(outs))
     return 0
 
