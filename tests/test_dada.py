@@ -405,3 +405,57 @@ def test_reader_read_depth_two(ring, short_last):
     t.join(60)
     assert not t.is_alive()
     assert got == blocks and held_max[0] == 2
+
+
+def test_ring_transfers_property(ring):
+    """Random transfers through a small ring with a concurrent reader: each
+    transfer's blocks arrive in order and unchanged, its end is a short,
+    empty or (at unlock_write) appended empty block, and the next transfer
+    follows after unlock_read + lock_read (per-block EOD marks)"""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    transfer = st.tuples(st.integers(0, 5), st.sampled_from(["full", "short", "empty"]),
+                         st.integers(1, 511))
+
+    @settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+    @given(xfers=st.lists(transfer, min_size=1, max_size=3), nbufs=st.integers(2, 4),
+           seed=st.integers(0, 1 << 30))
+    def check(xfers, nbufs, seed):
+        bufsz = 512
+        k = ring(nbufs, bufsz)
+        rng = np.random.default_rng(seed)
+        want = []
+        for nfull, end, short in xfers:
+            blocks = [rng.integers(0, 256, bufsz, dtype=np.uint8).tobytes() for _ in range(nfull)]
+            if end == "short":
+                blocks.append(rng.integers(0, 256, short, dtype=np.uint8).tobytes())
+            want.append(blocks)
+        got = []
+
+        def reader():
+            for t in range(len(xfers)):
+                with dada.Hdu(k, "R") as r:
+                    h = r.read_header()
+                    blocks = []
+                    while (b := r.read_block()) is not None:
+                        blocks.append(b)
+                    got.append((int(h.split()[1]), blocks, r.eod()))
+
+        th = threading.Thread(target=reader)
+        th.start()
+        for t, (blocks, (nfull, end, short)) in enumerate(zip(want, xfers)):
+            with dada.Hdu(k, "W") as w:
+                w.write_header(f"XFER {t}\n")
+                for b in blocks:
+                    w.write_block(b)
+                if end == "empty":
+                    w.write_block(b"")          # an explicit 0-byte EOD block
+        th.join(60)
+        assert not th.is_alive()
+        assert [g[0] for g in got] == list(range(len(xfers)))
+        for (_, blocks, eod), exp in zip(got, want):
+            assert blocks == exp and eod
+        dada.destroy_ring(k)
+
+    check()
