@@ -363,6 +363,8 @@ def main(argv=None) -> int:
             # finalize rides on the next launch)
             it.integrate(blk, dst, True)
 
+    coll = {"op": "gather"}
+
     def collective():
         """the region's exchange: spectra gathered (or partials reduced) to
         rank 0; returns what rank 0 holds"""
@@ -380,7 +382,9 @@ def main(argv=None) -> int:
                 it.sync()
             return None
         if rccl:
-            return D.gather_spectra(out_t)  # RCCL gather of K x nout fp32 to rank 0
+            if coll["op"] == "gather":
+                return D.gather_spectra(out_t)  # RCCL gather of K x nout fp32 to rank 0
+            return D.all_gather_spectra(out_t)
         if dist_on:
             host = it.download(out_buf, nbytes=K * nout * 4).view("float32").reshape(K, nout)
             return D.gather_spectra(torch.from_numpy(host.copy()))
@@ -399,7 +403,14 @@ def main(argv=None) -> int:
         kk += 1
     it.sync()
     if dist_on:  # a communicator's first collective sets up its channels
-        collective()
+        try:
+            collective()
+        except RuntimeError as e:  # a backend without gather: every rank gets the spectra
+            if split:
+                raise
+            print(f"bench.py: rank {rank}: gather failed ({e}); using all_gather", file=sys.stderr)
+            coll["op"] = "all_gather"
+            collective()
     fence()
 
     def region():
@@ -542,7 +553,8 @@ def main(argv=None) -> int:
                 "bytes_per_integration": int(bb * (world if split else 1)),
                 "input": "pinned host buffer, H2D overlapped (PCIe-inclusive)" if host_mode
                          else f"HBM-resident, {NBLOCKS} rotating blocks per GPU",
-                "parallelism": parallelism_label(world, split, dist_on, rccl),
+                "parallelism": parallelism_label(world, split, dist_on, rccl)
+                + ("" if coll["op"] == "gather" else " (all_gather: the backend refused gather)"),
                 "launcher": ("bench.py --gpus spawned torch.distributed.run"
                              if os.environ.get("BENCH_LAUNCHED_RANKS") else
                              ("torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")),

@@ -65,6 +65,15 @@ def gather_spectra(local: torch.Tensor) -> list[torch.Tensor] | None:
     return None
 
 
+def all_gather_spectra(local: torch.Tensor) -> list[torch.Tensor] | None:
+    """gather_spectra through all_gather, for a backend that refuses gather:
+    rank 0 keeps every rank's spectra, the peers drop theirs"""
+    world = dist.get_world_size()
+    bufs = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(bufs, local.contiguous())
+    return bufs if dist.get_rank() == 0 else None
+
+
 def time_share(rank: int, world: int, nframes: int) -> tuple[int, int]:
     """(first frame, frames) of rank's share of an nframes integration: the
     time axis is cut into world equal contiguous shares."""

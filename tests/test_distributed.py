@@ -41,6 +41,10 @@ def _worker(rank, world, port, q):
         spec.append(npo.power(g, buf))
     local = torch.from_numpy(np.stack(spec))
     got = D.gather_spectra(local)
+    got2 = D.all_gather_spectra(local)      # the fallback keeps the same contract
+    assert (got2 is None) == (r != 0)
+    if r == 0:
+        assert all(torch.equal(a, b) for a, b in zip(got, got2))
     el = D.max_over_ranks(0.5 + r)
     if r == 0:
         q.put(("gather", [t.numpy() for t in got], el))
