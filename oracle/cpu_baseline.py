@@ -81,14 +81,14 @@ def host_cpu() -> dict:
             "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus()}
 
 
-def child_env(threads: int) -> dict:
+def child_env(threads: int, places: str = "cores", wait: str = "active") -> dict:
     env = dict(os.environ)
-    env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores",
-               OMP_WAIT_POLICY="active")
+    env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES=places,
+               OMP_WAIT_POLICY=wait)
     return env
 
 
-def run(geom: dict, seconds: float, seed: int) -> dict:
+def run(geom: dict, seconds: float, seed: int, one_thread: bool = True) -> dict:
     sys.path.insert(0, _HERE)
     import numpy as np
 
@@ -114,6 +114,12 @@ def run(geom: dict, seconds: float, seed: int) -> dict:
                 break
         return rates, time.perf_counter() - t_all
 
+    if not one_thread:  # one setting only (bench.py's every-logical-CPU leg)
+        r_n, el_n = timed(threads, seconds)
+        return {"threads": threads, "value": round(statistics.median(r_n), 2), "passes": len(r_n),
+                "passes_range": [round(min(r_n), 2), round(max(r_n), 2)],
+                "binding": f"OMP_PLACES={os.environ.get('OMP_PLACES')} "
+                           f"OMP_WAIT_POLICY={os.environ.get('OMP_WAIT_POLICY')}"}
     r_n, el_n = timed(threads, seconds * 0.7)
     r_1, el_1 = timed(1, seconds * 0.3)
     nodes = numa_nodes()
@@ -135,4 +141,5 @@ def run(geom: dict, seconds: float, seed: int) -> dict:
 
 if __name__ == "__main__":
     geom = json.loads(sys.argv[1])
-    print(json.dumps(run(geom, float(sys.argv[2]), int(sys.argv[3]))), flush=True)
+    one = not (len(sys.argv) > 4 and sys.argv[4] == "only")
+    print(json.dumps(run(geom, float(sys.argv[2]), int(sys.argv[3]), one_thread=one)), flush=True)
