@@ -549,6 +549,7 @@ def main(argv=None) -> int:
             "timed_regions": len(els_max),
             "timed_seconds": round(sum(els_max), 4),
             "ms_per_step_range": [round(min(els_max) / K * 1e3, 4), round(max(els_max) / K * 1e3, 4)],
+            "ms_per_step_mean": round(statistics.fmean(els_max) / K * 1e3, 4),
             "per_rank_ms_per_step": per_rank_ms,
             # whole-job HBM read rate and its share of world x 8 TB/s
             # ("% of 8x roofline" for configs[4])
