@@ -113,6 +113,13 @@ int ipcbuf_get_device(ipcbuf_t *id);
 int ipcbuf_copy_in(ipcbuf_t *id, char *block, const void *src, uint64_t n);
 int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n);
 uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread);
+/* Extension: make every ring wait of this process (a reader waiting for a
+ * block, a writer waiting for a free one) give up -- the call fails, e.g.
+ * ipcio_open_block_read returns NULL -- instead of resuming, once a signal
+ * has interrupted it.  Async-signal-safe: meant for a SIGINT/SIGTERM
+ * handler, so a stage stops between blocks and ends its output transfer
+ * (unlock_write) cleanly instead of dying mid-ring. */
+void dada_interrupt_waits(void);
 
 /* ---- ipcio: block-level streaming over an ipcbuf ---- */
 typedef struct ipcio {

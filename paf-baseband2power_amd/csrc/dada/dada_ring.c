@@ -11,6 +11,7 @@
  * on a full block ends it with an empty block (ipcbuf_enable_eod).
  */
 #include <errno.h>
+#include <signal.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -24,7 +25,13 @@
 #include "b2p_dada.h"
 #include "dada_internal.h"
 
-/* semop with EINTR retry; flags e.g. SEM_UNDO | IPC_NOWAIT */
+/* set by dada_interrupt_waits (a signal handler): interrupted waits fail */
+static volatile sig_atomic_t g_interrupt;
+
+void dada_interrupt_waits(void) { g_interrupt = 1; }
+
+/* semop with EINTR retry (until dada_interrupt_waits); flags e.g.
+ * SEM_UNDO | IPC_NOWAIT */
 static int sem_do(int semid, int num, int op, int flags) {
   struct sembuf sb;
   sb.sem_num = (unsigned short)num;
@@ -32,7 +39,7 @@ static int sem_do(int semid, int num, int op, int flags) {
   sb.sem_flg = (short)flags;
   for (;;) {
     if (semop(semid, &sb, 1) == 0) return 0;
-    if (errno != EINTR) return -1;
+    if (errno != EINTR || (g_interrupt && op < 0)) return -1;
   }
 }
 

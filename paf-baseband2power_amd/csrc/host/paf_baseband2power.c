@@ -29,6 +29,7 @@
 #include <getopt.h>
 #include <inttypes.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -103,6 +104,33 @@ static void usage(void) {
           " -t  Split each integration of the one input ring by time over N GPUs (d + r);\n"
           "     exact partial sums are reduced on GPU d (host ring: N PCIe links in parallel)\n"
           " -h  show help\n");
+}
+
+/* SIGINT / SIGTERM: stop between blocks and end the output transfer
+ * cleanly (unlock_write writes its end of data, so the sink finishes).
+ * Ring waits in progress give up (dada_interrupt_waits); worker threads
+ * blocked in one are woken with SIGUSR2 by the main thread. */
+static volatile sig_atomic_t g_stop;
+
+static void on_stop(int sig) {
+  (void)sig;
+  g_stop = 1;
+#if DEVICE_RINGS
+  dada_interrupt_waits();
+#endif
+}
+
+static void on_wake(int sig) { (void)sig; }
+
+static void install_stop_handlers(void) {
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sigemptyset(&sa.sa_mask);
+  sa.sa_handler = on_stop; /* no SA_RESTART: a blocked semop returns EINTR */
+  sigaction(SIGINT, &sa, NULL);
+  sigaction(SIGTERM, &sa, NULL);
+  sa.sa_handler = on_wake;
+  sigaction(SIGUSR2, &sa, NULL);
 }
 
 static double now_s(void) {
@@ -278,7 +306,7 @@ static void *worker(void *arg) {
   sub_t *s = &sh->sub[w->r];
   for (;;) {
     uint64_t bytes = 0;
-    char *blk = next_block(s->in, &bytes);
+    char *blk = g_stop ? NULL : next_block(s->in, &bytes);
     sh->have[w->r] = !blk ? -1 : (bytes == s->rbufsz ? 1 : 0);
     pthread_barrier_wait(&sh->bar); /* all sub-bands agree on this round */
     int stop = sh->failed, skip = 0;
@@ -372,7 +400,7 @@ static void run_device_pipelined(shared_t *sh) {
   int open_prev = 0; /* block k-1 still held */
   for (;;) {
     uint64_t bytes = 0, bid = 0;
-    char *blk = ipcio_open_block_read(in, &bytes, &bid);
+    char *blk = g_stop ? NULL : ipcio_open_block_read(in, &bytes, &bid);
     const int full = blk && bytes == s->rbufsz;
     if (!full) { /* end of data or a partial block: drain the pipeline */
       if (b2p_sync(s->ctx) != B2P_OK) sh->failed = 1;
@@ -429,7 +457,7 @@ static void *worker_split(void *arg) {
   for (;;) {
     if (w->r == 0) {
       sh->blk_bytes = 0;
-      sh->blk = next_block(s0->in, &sh->blk_bytes);
+      sh->blk = g_stop ? NULL : next_block(s0->in, &sh->blk_bytes);
       pin_block(s0, sh->blk, sh->log);
       sh->have[0] = !sh->blk ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
     }
@@ -544,6 +572,7 @@ int main(int argc, char *argv[]) {
   multilog_t *log = multilog_open("paf_baseband2power", 0);
   multilog_add(log, fp_log);
   multilog(log, LOG_INFO, "START PAF_PROCESS");
+  install_stop_handlers();
 
   /* only one visible GPU => index 0 (paf_baseband2power.cu:86-90) */
   int ndev = 0;
@@ -764,7 +793,19 @@ int main(int argc, char *argv[]) {
       wk[r].r = r;
       pthread_create(&th[r], NULL, split ? worker_split : worker, &wk[r]);
     }
-    for (int r = 0; r < nmem; r++) pthread_join(th[r], NULL);
+    /* join by polling, so a stop request can wake workers that wait on a ring */
+    int joined[MAX_SUB] = {0}, left = nmem;
+    while (left) {
+      for (int r = 0; r < nmem; r++)
+        if (!joined[r] && pthread_tryjoin_np(th[r], NULL) == 0) {
+          joined[r] = 1;
+          left--;
+        }
+      if (g_stop)
+        for (int r = 0; r < nmem; r++)
+          if (!joined[r]) pthread_kill(th[r], SIGUSR2);
+      if (left) usleep(20000);
+    }
     pthread_barrier_destroy(&sh.bar);
   }
 #if DEVICE_RINGS
@@ -792,6 +833,7 @@ done:
   }
   free(sh.spec_host);
   dada_hdu_destroy(out);
+  if (g_stop) multilog(log, LOG_INFO, "stopped by a signal between blocks; output transfer ended");
   multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s, "
            "%.6f s from the first integration to the last output, %.6f s for the last %" PRIu64,
            sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED",

@@ -127,3 +127,57 @@ def test_psrdada_mode_host_pipeline(gpu, tmp_path):
     assert dada.header_get(hdr, "NBIT", "%d") == 32
     log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
     assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log
+
+
+def test_stage_stops_cleanly_on_sigterm(gpu, tmp_path):
+    """SIGTERM while paf_baseband2power waits for its next input block: the
+    wait gives up, the stage ends its output transfer (end of data), the
+    sink finishes with every spectrum so far, and the stage exits 0"""
+    import signal
+    import subprocess
+    import time
+
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 14)
+    kin, kout = 0x6f00 + (os.getpid() % 32) * 4, 0x6f80 + (os.getpid() % 32) * 4
+    for k in (kin, kout):
+        dada.destroy_ring(k)
+    dada.create_ring(kin, 3, g.block_bytes)
+    dada.create_ring(kout, 4, g.nout * 4)
+    out = tmp_path / "power.dada"
+    procs = []
+    try:
+        procs.append(subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_dbdisk"), "-k", f"{kout:x}",
+                                       "-o", str(out)], stderr=subprocess.PIPE, text=True))
+        stage = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_baseband2power"), "-a", f"{kin:x}",
+                                  "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0"],
+                                 stderr=subprocess.PIPE, text=True)
+        procs.append(stage)
+        blocks = [co.fill_synthetic(g, g.block_bytes, SEED, 7, k) for k in range(2)]
+        log = tmp_path / "paf_baseband2power.log"
+        with dada.Hdu(kin, "W") as w:
+            w.write_header("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\n"
+                           "TSAMP 0.84375\n")
+            for b in blocks:
+                w.write_block(b.tobytes())
+            t_end = time.time() + 120
+            while "integration 2:" not in (log.read_text() if log.exists() else ""):
+                assert time.time() < t_end and stage.poll() is None, stage.stderr.read()
+                time.sleep(0.1)
+            time.sleep(0.3)                       # the stage is now waiting for block 3
+            stage.send_signal(signal.SIGTERM)
+            assert stage.wait(60) == 0, stage.stderr.read()
+            assert procs[0].wait(60) == 0, procs[0].stderr.read()
+        _, data = dada.read_dada_file(str(out))
+        sp = data.view(np.float32).reshape(-1, g.nout)
+        assert sp.shape == (2, g.nout)
+        for k in range(2):
+            assert np.array_equal(sp[k].view(np.uint32), co.power(g, blocks[k]).view(np.uint32))
+        text = log.read_text()
+        assert "stopped by a signal" in text and "FINISH PAF_PROCESS: 2 integrations" in text
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
