@@ -38,6 +38,7 @@
 #include <math.h>
 #include <netinet/in.h>
 #include <poll.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -52,6 +53,15 @@
 #define MAXPORT 16
 #define RECV_BATCH 64
 #define TBUF_NDF 256 /* capture.h:35 */
+
+/* SIGINT / SIGTERM: stop receiving, deliver the block being filled and end
+ * the ring's transfer cleanly (the reference's capture stopped on a quit
+ * flag polled without atomics, capture.c:32-39, 443-446) */
+static volatile sig_atomic_t g_stop;
+static void on_stop(int sig) {
+  (void)sig;
+  g_stop = 1;
+}
 
 static double now_s(void) {
   struct timespec t;
@@ -209,6 +219,14 @@ int main(int argc, char **argv) {
   cap_t c;
   memset(&c, 0, sizeof c);
   c.log = multilog_open("paf_capture", 0);
+  {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sigemptyset(&sa.sa_mask);
+    sa.sa_handler = on_stop;
+    sigaction(SIGINT, &sa, NULL);
+    sigaction(SIGTERM, &sa, NULL);
+  }
   multilog_add(c.log, stderr);
   FILE *logf = NULL;
   if (logdir) {
@@ -310,10 +328,15 @@ int main(int argc, char **argv) {
     uint64_t got_all = 0, bad = 0;
     double last_rx = now_s(), t_first = 0;
     const double start_s = idle_s * 5 > 30 ? idle_s * 5 : 30; /* first frame within */
-    int stop = 0, jumped = 0;
+    int stop = 0, jumped = 0, stopped = 0;
     while (!stop) {
       int pr = poll(pfd, (nfds_t)nport, 20);
       if (pr < 0 && errno != EINTR) break;
+      if (g_stop) {
+        multilog(c.log, LOG_INFO, "stopped by a signal: delivering the current block");
+        stopped = 1;
+        break;
+      }
       int any = 0;
       for (int p = 0; p < nport && pr > 0; p++) {
         if (!(pfd[p].revents & POLLIN)) continue;
@@ -425,7 +448,8 @@ int main(int argc, char **argv) {
       }
     }
     free(rx);
-    if (jumped && c.blk && close_block(&c) < 0) goto done; /* deliver what arrived */
+    if ((jumped || stopped) && !record && c.blk && close_block(&c) < 0)
+      goto done; /* deliver what arrived */
     const double el = t_first > 0 ? last_rx - t_first : 0.0;
     multilog(c.log, LOG_INFO, "capture: %" PRIu64 " frames received (%" PRIu64 " not frames), %" PRIu64
              " blocks, %" PRIu64 " frames placed, %" PRIu64 " behind their block, %" PRIu64

@@ -68,3 +68,28 @@ def test_capture_flags_non_frames(tmp_path):
     assert cap.returncode == 0, err
     assert "capture: 1 frames received (2 not frames)" in err
     assert os.path.getsize(out) == 7232
+
+
+def test_capture_stops_cleanly_on_sigterm(tmp_path):
+    """SIGTERM ends the capture at once (no idle wait), with everything
+    received so far recorded and exit status 0"""
+    import signal
+    import socket
+    port = 24000 + (os.getpid() % 500) * 8
+    out, outc = tmp_path / "r.df", tmp_path / "r.chunks"
+    cap = subprocess.Popen([os.path.join(BIN, "paf_capture"), "-o", str(out), "-O", str(outc),
+                            "-P", str(port), "-N", "1", "-m", "freq:1300", "-t", "60"],
+                           stderr=subprocess.PIPE, text=True)
+    time.sleep(0.5)
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    for _ in range(3):
+        s.sendto(bytes(npo.DF_BYTES), ("127.0.0.1", port))
+    s.close()
+    time.sleep(0.5)
+    t0 = time.time()
+    cap.send_signal(signal.SIGTERM)
+    _, err = cap.communicate(timeout=30)
+    assert cap.returncode == 0, err
+    assert time.time() - t0 < 5
+    assert "stopped by a signal" in err and "capture: 3 frames received" in err
+    assert os.path.getsize(out) == 3 * npo.DF_BYTES
