@@ -90,10 +90,12 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1, help="ranks, one process per GPU")
     ap.add_argument("--steps", type=int, default=50, help="integrations per timed region")
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--min-seconds", type=float, default=1.0,
+    ap.add_argument("--min-seconds", type=float, default=5.0,
                     help="repeat the K-step region until this much timed work has run")
     ap.add_argument("--config", default="c2", choices=["c2", "c5", "bmf", "c3"])
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=4.0,
+                    help="CPU-baseline budget (tuned port, 1 thread, oracle), run after the GPU "
+                         "leg; the every-logical-CPU leg adds a quarter of it")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (spectra gathered on the host)")
     ap.add_argument("--force-dist", action="store_true",
@@ -104,6 +106,9 @@ def parse(argv=None):
     ap.add_argument("--no-fuse", action="store_true",
                     help="use b2p_push + b2p_finish_async instead of b2p_integrate")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-timing oracle check")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds one multi-rank phase (rendezvous, first collective, a timed "
+                         "region, verification) may take; past it the rank exits 4 naming it")
     a = ap.parse_args(argv)
     if a.gpus < 1 or a.steps < 1 or a.warmup < 0:
         ap.error("--gpus and --steps must be >= 1, --warmup >= 0")
@@ -216,8 +221,9 @@ def cpu_threads() -> int:
 
 
 def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
-    """The C restatement timed in a child process (its own OpenMP binding),
-    at every CPU this job may use and at 1 thread, on one full block; then,
+    """The tuned CPU port (oracle/b2p_cpu_port.c) timed in a child process
+    (its own OpenMP binding), at every CPU this job may use and at 1 thread,
+    with the scalar oracle beside it, on one full block; then,
     when the host shows more logical CPUs than that, once more at all of
     them (reported beside, as `all_cpus`: under a cgroup quota they only
     time-slice the same CPUs)."""
@@ -238,7 +244,7 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
     ncpu = os.cpu_count() or threads
     if res is not None and ncpu > threads:
         res["all_cpus"] = child(cb.child_env(ncpu, places="threads", wait="passive"),
-                                max(2.0, seconds * 0.3), "only")
+                                max(1.0, seconds * 0.25), "only")
     return res
 
 
@@ -299,8 +305,10 @@ def main(argv=None) -> int:
     geom = cfg["geom"]()
     dist_on = world > 1 or a.force_dist
     rccl = dist_on and a.dist_backend == "nccl"
+    wd = D.Watchdog(rank, a.dist_timeout)
     if dist_on:
-        D.init(a.dist_backend, local)
+        with wd.phase(f"rendezvous ({a.dist_backend} init_process_group, {world} ranks)"):
+            D.init(a.dist_backend, local, a.dist_timeout)
     split = a.split == "time"
     host_mode = a.config == "c3"
     subband = 0 if split else D.subband_of(rank)
@@ -415,6 +423,7 @@ def main(argv=None) -> int:
         kk += 1
     it.sync()
     if dist_on:  # a communicator's first collective sets up its channels
+        wd.arm(f"first {a.dist_backend} collective (communicator set-up)")
         try:
             collective()
         except RuntimeError as e:  # a backend without gather: every rank gets the spectra
@@ -424,9 +433,21 @@ def main(argv=None) -> int:
             coll["op"] = "all_gather"
             collective()
     fence()
+    # who actually ran: the live group read back, and every rank's GPU
+    world_seen = D.observed_world()
+    ident = {"rank": rank, "local_rank": local, "host": socket.gethostname(),
+             "device": int(it.info.device), "pci_bus_id": paf_b2p.pci_bus_id(int(it.info.device)),
+             "name": torch.cuda.get_device_name(int(it.info.device)),
+             "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")
+             or os.environ.get("ROCR_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+    idents = D.gather_identities(ident)
+    ngpu_seen = D.distinct_gpus(idents)
+    wd.disarm()
 
     def region():
         nonlocal kk
+        if dist_on:
+            wd.arm("a timed region (its collective included)")
         fence()
         t0 = time.perf_counter()
         it.set_timing(2)  # one event pair on the integrator's stream around the K launches
@@ -438,6 +459,7 @@ def main(argv=None) -> int:
             it.sync()
         got = collective()
         fence()
+        wd.disarm()
         return time.perf_counter() - t0, got
 
     it.reset_stats()
@@ -466,6 +488,8 @@ def main(argv=None) -> int:
     # ---- verification (outside timing) ------------------------------------
     verified = None
     vinfo = {}
+    if dist_on:
+        wd.arm("verification against the oracle", max(a.dist_timeout, 900.0))
     if not a.no_verify:
         vthreads = max(1, cpu_threads() // world)
         rows_ok = True
@@ -518,6 +542,7 @@ def main(argv=None) -> int:
                            + (", regenerated on the host" if split else ", downloaded from HBM")
                            + f"), bit for bit, {'rank 0' if split else 'every rank'}"),
                      threads=vthreads)
+    wd.disarm()
 
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
@@ -545,7 +570,11 @@ def main(argv=None) -> int:
             "verified": verified,
             "verification": vinfo or None,
             "ranks": world,
-            "rccl_ranks": world if rccl else 0,
+            # read back from the live process group after its first collective
+            "rccl_ranks": world_seen["rccl_ranks"],
+            "dist_backend": world_seen["backend"],
+            "distinct_gpus": ngpu_seen,
+            "rank_devices": [{k: v for k, v in i.items() if v is not None} for i in idents],
             "timed_regions": len(els_max),
             "timed_seconds": round(sum(els_max), 4),
             "ms_per_step_range": [round(min(els_max) / K * 1e3, 4), round(max(els_max) / K * 1e3, 4)],
@@ -557,8 +586,7 @@ def main(argv=None) -> int:
             "aggregate_frac_of_world_peak": round(value * 1e6 * (geom.nbit // 8) * 2 / 1e9
                                                   / (HBM_PEAK_GBS * (1 if split else world)), 4),
             "config": {
-                "workload": workload_label(a.config, geom_desc, world, split, host_mode,
-                                           min(world, torch.cuda.device_count())),
+                "workload": workload_label(a.config, geom_desc, world, split, host_mode, ngpu_seen),
                 "baseline_config": baseline_config(a.config, world, split),
                 "nchan": int(paf_b2p.geometry.nchan(geom)),
                 "npol": int(geom.npol),

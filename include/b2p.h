@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define B2P_ABI_VERSION 1
+#define B2P_ABI_VERSION 2
 
 /* status codes (replace CudaSafeCall's exit(-1), cudautil.cuh:29-41) */
 #define B2P_OK 0
@@ -48,6 +48,10 @@ extern "C" {
                                  set_timing) returns this until b2p_close;
                                  cleanup (dev_free, unregister_host, close) and
                                  b2p_last_error (the first failure) still work */
+#define B2P_ETIMEDOUT (-10)   /* a group's communicator setup or collective did
+                                 not complete within the group's time limit;
+                                 the communicators were aborted and the group
+                                 only accepts b2p_group_close from then on */
 
 /*
  * Layout of one input ring block:
@@ -126,12 +130,41 @@ int b2p_abi_version(void);
 /* ---- devices (paf_baseband2power.cu:86-90) ---- */
 int b2p_device_count(int *count);
 
+/* PCI bus id of a device ("0000:75:00.0"), for logs and multi-GPU run
+ * records: which physical GPU a member or rank actually used. */
+int b2p_device_pci_bus_id(int device, char *buf, int len);
+
+/* ---- launch tuning (tools/tune.py) ----
+ * The release defaults are the measured ones and no
+ * environment variable changes them; a tuning sweep passes its variant
+ * explicitly.  Every field at 0 / -1 (b2p_tuning_init) means "default".
+ * Unsupported values are refused with B2P_EINVAL, not clamped. */
+typedef struct b2p_tuning {
+  uint32_t size;          /* sizeof(b2p_tuning_t)                           */
+  int32_t max_threads;    /* 0, or 64..1024: cap on threads per workgroup   */
+  int32_t threads;        /* 0, or a whole-wave divisor of the frame's 16-B
+                             vectors (frame-split layouts only)             */
+  int32_t wg_per_cu;      /* 0, or 1..32 workgroups per CU                  */
+  int32_t row_groups;     /* 0, or >= 1 workgroups along time               */
+  int32_t replicas;       /* 0, or 1..1024 accumulator replicas             */
+  int32_t unroll;         /* 0, or 4 | 8 | 16 rows in flight per lane       */
+  int32_t nontemporal;    /* -1, or 0 | 1: non-temporal loads               */
+  int32_t interleave;     /* -1, or 0 | 1: interleaved row ownership        */
+  int32_t fuse;           /* -1, or 0 | 1: b2p_integrate finalizes in its
+                             own last workgroup                             */
+  int32_t stage_mib;      /* 0, or 1..16384: host-span staging buffer size  */
+  int32_t assemble_grid;  /* 0, or >= 1: b2p_assemble workgroup cap         */
+} b2p_tuning_t;
+void b2p_tuning_init(b2p_tuning_t *t);
+
 /* ---- context lifecycle ----
  * b2p_open replaces the intended init of baseband2power.cu (empty) and the
  * device selection at paf_baseband2power.cu:87-90: device < 0 is an error;
  * if exactly one device is visible, index 0 is used whatever was asked (the
  * reference's docker fallback). */
 int b2p_open(b2p_ctx_t **ctx, const b2p_geom_t *g, int device);
+/* b2p_open with an explicit launch variant (t may be NULL = defaults) */
+int b2p_open_tuned(b2p_ctx_t **ctx, const b2p_geom_t *g, int device, const b2p_tuning_t *t);
 int b2p_close(b2p_ctx_t *ctx);
 int b2p_get_info(const b2p_ctx_t *ctx, b2p_info_t *info);
 const char *b2p_last_error(const b2p_ctx_t *ctx); /* ctx may be NULL */
@@ -208,6 +241,13 @@ uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
  * state makes the collective return B2P_EFAILED. */
 typedef struct b2p_group b2p_group_t;
 int b2p_group_open(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode);
+/* b2p_group_open with a time limit (ms, > 0) on the RCCL communicator setup
+ * and on every b2p_group_sync: setup runs non-blocking
+ * (ncclCommInitRankConfig with blocking = 0, rccl.h:204) and is polled;
+ * past the limit, or on an asynchronous RCCL error, the communicators are
+ * aborted (ncclCommAbort, rccl.h:271) and the call returns B2P_ETIMEDOUT /
+ * B2P_EHIP instead of hanging.  b2p_group_open uses 60 000 ms. */
+int b2p_group_open_timed(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode, int timeout_ms);
 int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);
 /* Time-split mode (second mode): member r integrated its share
  * of ONE sub-band's samples and emitted exact sums with
@@ -216,6 +256,8 @@ int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);
  * ncclReduce(ncclUint64, ncclSum) in mode 0, peer copies + a sum kernel in
  * mode 1.  Exact, so bit-identical to a single-GPU integration. */
 int b2p_group_reduce(b2p_group_t *grp, uint64_t *const *sums, uint64_t count, uint64_t *root_sum);
+/* Waits for every member's stream, bounded by the group's time limit
+ * (B2P_ETIMEDOUT past it; the group is then unusable). */
 int b2p_group_sync(b2p_group_t *grp);
 const char *b2p_group_last_error(const b2p_group_t *grp); /* grp may be NULL */
 int b2p_group_close(b2p_group_t *grp);

@@ -1,6 +1,8 @@
 """oracle/cpu_baseline.py -- TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).
 
-Times the C restatement (oracle/b2p_oracle.c, OpenMP) on one FULL integration
+Times the tuned CPU port (oracle/b2p_cpu_port.c: AVX-512 VNNI / AVX-512 /
+AVX2 picked at run time, OpenMP over time tiles) -- and, beside it, the
+scalar C restatement that serves as the checker (oracle/b2p_oracle.c) -- on one FULL integration
 block of the bench's workload held in host RAM (no file I/O), so the passes
 stream from DRAM rather than the L3 (the EPYC 9575F host has 512 MiB of L3;
 a 1 GiB block does not fit).  SURVEY.md 8(d) "CPU baseline": the reference has
@@ -88,7 +90,7 @@ def child_env(threads: int, places: str = "cores", wait: str = "active") -> dict
     return env
 
 
-def run(geom: dict, seconds: float, seed: int, one_thread: bool = True) -> dict:
+def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str = "auto") -> dict:
     sys.path.insert(0, _HERE)
     import numpy as np
 
@@ -103,36 +105,53 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True) -> dict:
     co.fill_synthetic(g, g.block_bytes, seed, 0, 0, out=buf)   # first touch by the bound threads
     per_pass = g.block_bytes // g.word_bytes * g.npol          # complex samples in the block
 
-    def timed(nt: int, budget: float, min_passes: int = 3):
-        co.integrate(g, buf[: g.frame_bytes * max(1, (64 << 20) // g.frame_bytes)], nthreads=nt)
+    def port(nt):
+        return co.port_integrate(g, buf, nthreads=nt, isa=isa)
+
+    def oracle(nt):
+        return co.integrate(g, buf, nthreads=nt)
+
+    def timed(fn, nt: int, budget: float, min_passes: int = 3):
+        warm = buf[: g.frame_bytes * max(1, (64 << 20) // g.frame_bytes)]
+        (co.port_integrate(g, warm, nthreads=nt, isa=isa) if fn is port
+         else co.integrate(g, warm, nthreads=nt))
         rates, t_all = [], time.perf_counter()
         while len(rates) < min_passes or time.perf_counter() - t_all < budget:
             t0 = time.perf_counter()
-            co.integrate(g, buf, nthreads=nt)
+            fn(nt)
             rates.append(per_pass / (time.perf_counter() - t0) / 1e6)
             if len(rates) >= 10000:
                 break
         return rates, time.perf_counter() - t_all
 
+    used = co.port_isa(isa)
     if not one_thread:  # one setting only (bench.py's every-logical-CPU leg)
-        r_n, el_n = timed(threads, seconds)
+        r_n, el_n = timed(port, threads, seconds)
         return {"threads": threads, "value": round(statistics.median(r_n), 2), "passes": len(r_n),
-                "passes_range": [round(min(r_n), 2), round(max(r_n), 2)],
+                "passes_range": [round(min(r_n), 2), round(max(r_n), 2)], "isa": used,
                 "binding": f"OMP_PLACES={os.environ.get('OMP_PLACES')} "
                            f"OMP_WAIT_POLICY={os.environ.get('OMP_WAIT_POLICY')}"}
-    r_n, el_n = timed(threads, seconds * 0.7)
-    r_1, el_1 = timed(1, seconds * 0.3)
+    r_n, el_n = timed(port, threads, seconds * 0.55)
+    r_1, el_1 = timed(port, 1, seconds * 0.25)
+    r_o, el_o = timed(oracle, threads, seconds * 0.2)
+    # the port is a baseline, not the checker: its sums must equal the oracle's
+    equal = bool(np.array_equal(port(threads), oracle(threads)))
     nodes = numa_nodes()
     node = next((n for n, c in nodes.items() if first in c), None)
     return {
         "value": round(statistics.median(r_n), 2), "unit": "Msamples/s", "cores": threads,
-        "kind": "port",
-        "sample": (f"{len(r_n)} passes ({el_n:.1f} s) at {threads} threads and {len(r_1)} passes "
-                   f"({el_1:.1f} s) at 1 thread over one full {g.block_bytes >> 20} MiB "
-                   f"{g.nchan}-chan int{g.nbit} integration block in host RAM (no file I/O); "
-                   "value = median pass"),
+        "kind": "port-tuned",
+        "isa": used,
+        "sample": (f"tuned port ({used}, OpenMP time tiles): {len(r_n)} passes ({el_n:.1f} s) at "
+                   f"{threads} threads and {len(r_1)} passes ({el_1:.1f} s) at 1 thread over one "
+                   f"full {g.block_bytes >> 20} MiB {g.nchan}-chan int{g.nbit} integration block "
+                   "in host RAM (no file I/O); value = median pass"),
         "value_1thread": round(statistics.median(r_1), 2),
         "passes_range": [round(min(r_n), 2), round(max(r_n), 2)],
+        "equals_oracle": equal,
+        "oracle_value": round(statistics.median(r_o), 2),
+        "oracle": (f"scalar C restatement (the checker, oracle/b2p_oracle.c): {len(r_o)} passes "
+                   f"({el_o:.1f} s) at {threads} threads, median"),
         "numa": {"node": node, "binding": "OMP_PLACES=cores OMP_PROC_BIND=close, packed from the "
                                           "first allowed CPU; block first-touched by the same threads"},
         "host": host,
@@ -142,4 +161,6 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True) -> dict:
 if __name__ == "__main__":
     geom = json.loads(sys.argv[1])
     one = not (len(sys.argv) > 4 and sys.argv[4] == "only")
-    print(json.dumps(run(geom, float(sys.argv[2]), int(sys.argv[3]), one_thread=one)), flush=True)
+    isa = sys.argv[5] if len(sys.argv) > 5 else "auto"
+    print(json.dumps(run(geom, float(sys.argv[2]), int(sys.argv[3]), one_thread=one, isa=isa)),
+          flush=True)

@@ -130,3 +130,41 @@ def assemble(dfs: np.ndarray, chunk_of_df: np.ndarray, ref_idf: int, ref_sec: in
     L.orc_assemble(_ptr(dfs), ndf, 7232, _ptr(chunk_of_df), ref_idf, ref_sec, _ptr(block),
                    block_ndf, nchunk, _ptr(counts))
     return counts
+
+
+# ---- the tuned CPU port (oracle/b2p_cpu_port.c): bench.py's cpu_baseline --
+_PORT_PATH = os.path.join(_HERE, "lib", "libb2p_cpuport.so")
+ISA = {"auto": 0, "scalar": 1, "avx2": 2, "avx512bw": 3, "avx512vnni": 4}
+_port = None
+
+
+def port_lib():
+    global _port
+    if _port is None:
+        if not os.path.exists(_PORT_PATH):
+            build()
+        L = C.CDLL(_PORT_PATH)
+        L.cpp_integrate.argtypes = [C.POINTER(OrcGeom), C.c_void_p, C.c_size_t, C.c_void_p, C.c_int,
+                                    C.c_int]
+        L.cpp_isa_name.argtypes = [C.c_int]
+        L.cpp_isa_name.restype = C.c_char_p
+        _port = L
+    return _port
+
+
+def port_isa(isa: str = "auto") -> str:
+    """the ISA the port runs for a request ("auto": the best this CPU has)"""
+    return port_lib().cpp_isa_name(ISA[isa]).decode()
+
+
+def port_integrate(g: Geom, buf: np.ndarray, nthreads: int = 1, acc: np.ndarray | None = None,
+                   isa: str = "auto") -> np.ndarray:
+    """exact uint64 sums from the tuned port (equal to integrate())"""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    if acc is None:
+        acc = np.zeros(g.nout, dtype=np.uint64)
+    rc = port_lib().cpp_integrate(C.byref(OrcGeom.of(g)), _ptr(buf), buf.size, _ptr(acc),
+                                  nthreads, ISA[isa])
+    if rc != 0:
+        raise ValueError("cpu port rejected input (ragged or unsupported geometry)")
+    return acc

@@ -88,7 +88,10 @@ struct b2p_ctx {
   // (b2p_push's host-span loop), so the running sums are unknown; only
   // b2p_close is meaningful afterwards (B2P_EFAILED)
   int failed = 0;
-  long inject_push_fail = -1;  // test hook: B2P_INJECT_PUSH_FAIL=<chunk index>
+  b2p_tuning_t tun{};           // launch variant (b2p_open_tuned); defaults otherwise
+#ifdef B2P_TEST_HOOKS
+  long inject_push_fail = -1;  // test build only: b2p_test_inject_push_fail
+#endif
   char err[256] = {0};
 };
 
@@ -145,6 +148,7 @@ const char *b2p_strerror(int code) {
     case B2P_ENOMEM: return "out of memory";
     case B2P_EALIGN: return "buffer not 16-byte aligned";
     case B2P_EFAILED: return "context failed part-way through an earlier call; close it";
+    case B2P_ETIMEDOUT: return "collective did not complete within the group's time limit";
   }
   return "unknown error";
 }
@@ -208,6 +212,7 @@ int b2p_device_count(int *count) {
 // Choose the workgroup shape (DESIGN.md "integrate kernel / launch shape").
 static int plan_launch(b2p_ctx_t *c, int ncu) {
   const b2p_geom_t *g = &c->g;
+  const b2p_tuning_t &t = c->tun;
   const uint32_t wb = (uint32_t)word_bytes(g);
   c->VW = 16 / wb;
   c->IV = g->nsamp_df * g->nchan_chunk / c->VW;
@@ -215,10 +220,7 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   const uint32_t P = g->nchan_chunk / gcd_u(g->nchan_chunk, c->VW);
   c->CP = g->nchunk == 1 ? P : c->FV;
   uint32_t maxT = g->nbit == 8 ? 512 : 448;
-  if (const char *e = getenv("B2P_MAX_THREADS")) {
-    int v = atoi(e);
-    if (v >= 64 && v <= 1024) maxT = (uint32_t)v;
-  }
+  if (t.max_threads) maxT = (uint32_t)t.max_threads;
   const uint32_t L = c->CP / gcd_u(c->CP, 64) * 64;  // lcm(CP, 64)
   uint32_t colB = 0;  // whole-wave divisor of L for a row split into columns
   if (c->CP <= maxT && L > maxT && g->nchunk == 1)
@@ -243,9 +245,11 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
     uint32_t best = 0;
     for (uint32_t b = maxT / 64 * 64; b >= 64; b -= 64)
       if (c->CP % b == 0) { best = b; break; }
-    if (const char *e = getenv("B2P_THREADS")) {  // tuning knob: exact divisor
-      int v = atoi(e);
-      if (v >= 64 && v <= 1024 && c->CP % (uint32_t)v == 0) best = (uint32_t)v;
+    if (t.threads) {  // tuning: an exact whole-wave divisor of the frame
+      if (c->CP % (uint32_t)t.threads)
+        return set_err(c, B2P_EINVAL, "tuning threads %d does not divide the %u-vector frame",
+                       t.threads, c->CP);
+      best = (uint32_t)t.threads;
     }
     if (best) {
       c->B = best;
@@ -270,28 +274,62 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
   // ... counted as ~8 waves: a narrower workgroup (a frame that only
   // divides into 256-thread columns) gets two per CU
   uint32_t per_cu = std::max<uint32_t>(1, 512 / c->Bpad);
-  if (const char *e = getenv("B2P_WG_PER_CU")) {
-    int v = atoi(e);
-    if (v >= 1 && v <= 32) per_cu = (uint32_t)v;
-  }
+  if (t.wg_per_cu) per_cu = (uint32_t)t.wg_per_cu;
   const uint32_t target = (uint32_t)ncu * per_cu;
   c->G = std::max<uint32_t>(1, (target + c->NC / 2) / c->NC);
-  if (const char *e = getenv("B2P_ROW_GROUPS")) {  // test knob: long per-lane runs
-    int v = atoi(e);
-    if (v >= 1) c->G = (uint32_t)v;
-  }
-  c->nrep = 16;
-  if (const char *e = getenv("B2P_NREP")) {
-    int v = atoi(e);
-    if (v >= 1 && v <= 1024) c->nrep = (uint32_t)v;
+  if (t.row_groups) c->G = (uint32_t)t.row_groups;  // e.g. long per-lane runs in tests
+  c->nrep = t.replicas ? (uint32_t)t.replicas : 16;
+  return B2P_OK;
+}
+
+void b2p_tuning_init(b2p_tuning_t *t) {
+  if (!t) return;
+  memset(t, 0, sizeof *t);
+  t->size = sizeof *t;
+  t->nontemporal = t->interleave = t->fuse = -1;
+}
+
+// every value a tuning may carry; anything else is refused, not clamped
+static const char *tuning_problem(const b2p_tuning_t *t) {
+  if (t->size != sizeof *t) return "b2p_tuning_t.size does not match this library";
+  if (t->max_threads && (t->max_threads < 64 || t->max_threads > 1024)) return "max_threads";
+  if (t->threads && (t->threads < 64 || t->threads > 1024 || t->threads % 64)) return "threads";
+  if (t->wg_per_cu && (t->wg_per_cu < 1 || t->wg_per_cu > 32)) return "wg_per_cu";
+  if (t->row_groups < 0) return "row_groups";
+  if (t->replicas && (t->replicas < 1 || t->replicas > 1024)) return "replicas";
+  if (t->unroll && t->unroll != 4 && t->unroll != 8 && t->unroll != 16) return "unroll";
+  if (t->nontemporal < -1 || t->nontemporal > 1) return "nontemporal";
+  if (t->interleave < -1 || t->interleave > 1) return "interleave";
+  if (t->fuse < -1 || t->fuse > 1) return "fuse";
+  if (t->stage_mib && (t->stage_mib < 1 || t->stage_mib > 16384)) return "stage_mib";
+  if (t->assemble_grid < 0) return "assemble_grid";
+  return nullptr;
+}
+
+int b2p_device_pci_bus_id(int device, char *buf, int len) {
+  if (!buf || len < 13 || device < 0) return B2P_EINVAL;
+  hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+  if (e != hipSuccess) {
+    buf[0] = 0;
+    return set_err(nullptr, B2P_ENODEV, "hipDeviceGetPCIBusId(%d): %s", device, hipGetErrorString(e));
   }
   return B2P_OK;
 }
 
 int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
+  return b2p_open_tuned(out, g, device, nullptr);
+}
+
+int b2p_open_tuned(b2p_ctx_t **out, const b2p_geom_t *g, int device, const b2p_tuning_t *tun) {
   if (!out || !g) return set_err(nullptr, B2P_EINVAL, "null argument");
   *out = nullptr;
   if (b2p_geom_check(g) != B2P_OK) return set_err(nullptr, B2P_EINVAL, "unsupported geometry");
+  b2p_tuning_t t;
+  b2p_tuning_init(&t);
+  if (tun) {
+    if (const char *bad = tuning_problem(tun)) return set_err(nullptr, B2P_EINVAL, "tuning: %s", bad);
+    t = *tun;
+  }
   if (device < 0) return set_err(nullptr, B2P_ENODEV, "device index %d < 0", device);
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
@@ -303,6 +341,7 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   b2p_ctx_t *c = new (std::nothrow) b2p_ctx_t();
   if (!c) return set_err(nullptr, B2P_ENOMEM, "context allocation");
   c->g = *g;
+  c->tun = t;
   c->device = device;
   c->mode = g->nbit == 8 ? kI8 : (g->big_endian ? kI16BE : kI16LE);
   c->nchan = g->nchunk * g->nchan_chunk;
@@ -314,17 +353,10 @@ int b2p_open(b2p_ctx_t **out, const b2p_geom_t *g, int device) {
   // of loads in flight per CU -- 4 rows per lane; int8 512 threads with
   // contiguous row slices, int16 (BMF) 448 threads with interleaved rows --
   // one workgroup per CU, non-temporal loads
-  c->kc.unroll = 4;
-  c->kc.nt = true;
-  if (const char *e = getenv("B2P_UNROLL")) {
-    int v = atoi(e);
-    if (v == 4 || v == 8 || v == 16) c->kc.unroll = v;
-  }
-  if (const char *e = getenv("B2P_NT")) c->kc.nt = atoi(e) != 0;
-  c->interleave = g->nbit == 16 ? 1 : 0;
-  if (const char *e = getenv("B2P_INTERLEAVE")) c->interleave = atoi(e) != 0;
-  if (const char *e = getenv("B2P_FUSE")) c->fuse = atoi(e) != 0;
-  if (const char *e = getenv("B2P_INJECT_PUSH_FAIL")) c->inject_push_fail = atol(e);
+  c->kc.unroll = t.unroll ? t.unroll : 4;
+  c->kc.nt = t.nontemporal != 0;
+  c->interleave = t.interleave >= 0 ? (uint32_t)t.interleave : (g->nbit == 16 ? 1u : 0u);
+  c->fuse = t.fuse > 0;
   c->block_bytes = b2p_block_bytes(g);
   int rc;
   int ncu = 256;
@@ -570,11 +602,7 @@ static int flush_pending(b2p_ctx_t *c) {
 
 static int ensure_staging(b2p_ctx_t *c) {
   if (c->d_stage[0]) return B2P_OK;
-  uint64_t want = 256ull << 20;
-  if (const char *e = getenv("B2P_STAGE_MIB")) {
-    long v = atol(e);
-    if (v >= 1 && v <= 16384) want = (uint64_t)v << 20;
-  }
+  const uint64_t want = (uint64_t)(c->tun.stage_mib ? c->tun.stage_mib : 256) << 20;
   uint64_t sb = want / c->frame_bytes * c->frame_bytes;
   if (sb == 0) sb = c->frame_bytes;
   c->stage_bytes = sb;
@@ -598,8 +626,10 @@ static int push_host(b2p_ctx_t *c, const uint8_t *h, uint64_t nbytes) {
   for (uint64_t off = 0; off < nbytes; off += c->stage_bytes, ++k) {
     const uint64_t n = std::min<uint64_t>(c->stage_bytes, nbytes - off);
     const int i = (int)(c->stage_next++ & 1);
+#ifdef B2P_TEST_HOOKS
     if (k == c->inject_push_fail)
-      return set_err(c, B2P_EHIP, "injected failure at staging chunk %ld (B2P_INJECT_PUSH_FAIL)", k);
+      return set_err(c, B2P_EHIP, "injected failure at staging chunk %ld (test build)", k);
+#endif
     CK(c, hipStreamWaitEvent(c->copy_stream, c->ev_consumed[i], 0));
     CK(c, hipMemcpyAsync(c->d_stage[i], h + off, n, hipMemcpyHostToDevice, c->copy_stream));
     CK(c, hipEventRecord(c->ev_copied[i], c->copy_stream));
@@ -858,7 +888,7 @@ int b2p_assemble(b2p_ctx_t *c, const void *dfs, uint64_t ndf, uint32_t df_bytes,
   a.block_ndf = block_ndf;
   a.nchunk = nchunk;
   a.counts = counts;
-  CK(c, launch_assemble(a, c->stream));
+  CK(c, launch_assemble(a, (uint32_t)c->tun.assemble_grid, c->stream));
   return B2P_OK;
 }
 
@@ -895,5 +925,16 @@ int b2p_memcpy(b2p_ctx_t *c, void *dst, const void *src, size_t bytes, int kind)
   CK(c, hipMemcpy(dst, src, bytes, k));
   return B2P_OK;
 }
+
+#ifdef B2P_TEST_HOOKS
+// Test build only (lib/hooks/libpafb2p.so, -DB2P_TEST_HOOKS): the next
+// host-span push fails at staging chunk `chunk` after the earlier chunks were
+// enqueued, as a HIP error would.  The release library has no such entry.
+int b2p_test_inject_push_fail(b2p_ctx_t *c, long chunk) {
+  if (!c) return B2P_EINVAL;
+  c->inject_push_fail = chunk;
+  return B2P_OK;
+}
+#endif
 
 }  // extern "C"

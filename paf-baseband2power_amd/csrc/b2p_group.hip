@@ -15,6 +15,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <vector>
 
@@ -32,6 +34,8 @@ struct b2p_group {
   unsigned long long *scratch = nullptr;  // mode 1 reduce: rows gathered on the root
   uint64_t scratch_count = 0;
   uint32_t nout = 0;
+  int timeout_ms = 60000;
+  int dead = 0;  // communicators aborted (time limit or RCCL error): close only
   char err[256] = {0};
 };
 
@@ -41,17 +45,108 @@ int gerr(b2p_group_t *g, int code, const char *what, const char *detail) {
   snprintf(g ? g->err : g_gerr, 256, "%s: %s", what, detail ? detail : "");
   return code;
 }
+double now_s() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+// Abort every communicator: after a time limit or an asynchronous RCCL
+// error nothing else may be issued on them (rccl.h:266-271).
+void abort_comms(b2p_group_t *g) {
+  for (auto &c : g->comm)
+    if (c) {
+      ncclCommAbort(c);
+      c = nullptr;
+    }
+  g->dead = 1;
+}
+
+// Poll the non-blocking communicators until none is ncclInProgress, an
+// asynchronous error shows, or the deadline passes (then abort).
+int settle_comms(b2p_group_t *g, double deadline, const char *what) {
+  for (;;) {
+    bool pending = false;
+    for (int r = 0; r < (int)g->comm.size(); ++r) {
+      ncclResult_t st = ncclSuccess;
+      ncclResult_t q = ncclCommGetAsyncError(g->comm[r], &st);
+      if (q != ncclSuccess) st = q;
+      if (st == ncclInProgress) {
+        pending = true;
+      } else if (st != ncclSuccess) {
+        char d[160];
+        snprintf(d, sizeof d, "member %d (device %d): %s", r, g->dev[r], ncclGetErrorString(st));
+        abort_comms(g);
+        return gerr(g, B2P_EHIP, what, d);
+      }
+    }
+    if (!pending) return B2P_OK;
+    if (now_s() > deadline) {
+      char d[96];
+      snprintf(d, sizeof d, "not complete after %d ms; communicators aborted", g->timeout_ms);
+      abort_comms(g);
+      return gerr(g, B2P_ETIMEDOUT, what, d);
+    }
+    usleep(200);
+  }
+}
+
+// The collective's work on every member stream, with the group's deadline.
+int wait_streams(b2p_group_t *g, const char *what) {
+  const double deadline = now_s() + 1e-3 * g->timeout_ms;
+  for (;;) {
+    bool busy = false;
+    for (int r = 0; r < g->n; ++r) {
+      (void)hipSetDevice(g->dev[r]);
+      hipError_t e = hipStreamQuery(g->stream[r]);
+      if (e == hipErrorNotReady) {
+        busy = true;
+      } else if (e != hipSuccess) {
+        if (!g->comm.empty()) abort_comms(g);
+        g->dead = 1;
+        return gerr(g, B2P_EHIP, what, hipGetErrorString(e));
+      }
+    }
+    if (!g->comm.empty()) {  // an RCCL failure shows here before the stream idles
+      ncclResult_t st = ncclSuccess;
+      for (int r = 0; r < (int)g->comm.size() && st == ncclSuccess; ++r) {
+        ncclResult_t q = ncclCommGetAsyncError(g->comm[r], &st);
+        if (q != ncclSuccess) st = q;
+        if (st == ncclInProgress) st = ncclSuccess;
+      }
+      if (st != ncclSuccess) {
+        abort_comms(g);
+        return gerr(g, B2P_EHIP, what, ncclGetErrorString(st));
+      }
+    }
+    if (!busy) return B2P_OK;
+    if (now_s() > deadline) {
+      char d[96];
+      snprintf(d, sizeof d, "not complete after %d ms; communicators aborted", g->timeout_ms);
+      if (!g->comm.empty()) abort_comms(g);
+      g->dead = 1;
+      return gerr(g, B2P_ETIMEDOUT, what, d);
+    }
+    usleep(50);
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 int b2p_group_open(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int mode) {
-  if (!out || !ctxs || n < 1 || (mode != 0 && mode != 1)) return B2P_EINVAL;
+  return b2p_group_open_timed(out, ctxs, n, mode, 60000);
+}
+
+int b2p_group_open_timed(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int mode, int timeout_ms) {
+  if (!out || !ctxs || n < 1 || (mode != 0 && mode != 1) || timeout_ms <= 0) return B2P_EINVAL;
   *out = nullptr;
   b2p_group_t *g = new (std::nothrow) b2p_group_t();
   if (!g) return B2P_ENOMEM;
   g->n = n;
   g->mode = mode;
+  g->timeout_ms = timeout_ms;
   for (int r = 0; r < n; ++r) {
     b2p_info_t info;
     if (!ctxs[r] || b2p_get_info(ctxs[r], &info) != B2P_OK) {
@@ -68,10 +163,40 @@ int b2p_group_open(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int mode) {
     g->stream.push_back((hipStream_t)b2p_internal_stream(ctxs[r]));
   }
   if (mode == 0) {
-    g->comm.resize(n);
-    ncclResult_t nr = ncclCommInitAll(g->comm.data(), n, g->dev.data());
+    // ncclCommInitAll's work (rccl.h:236), made non-blocking so that a
+    // set-up that never completes ends at the time limit instead of hanging
+    // the process: one unique id, every rank initialised inside one group
+    // call, then polled
+    const double deadline = now_s() + 1e-3 * timeout_ms;
+    ncclUniqueId id;
+    ncclResult_t nr = ncclGetUniqueId(&id);
     if (nr != ncclSuccess) {
-      int rc = gerr(nullptr, B2P_EHIP, "ncclCommInitAll", ncclGetErrorString(nr));
+      int rc = gerr(nullptr, B2P_EHIP, "ncclGetUniqueId", ncclGetErrorString(nr));
+      delete g;
+      return rc;
+    }
+    g->comm.assign(n, nullptr);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    nr = ncclGroupStart();
+    for (int r = 0; r < n && (nr == ncclSuccess || nr == ncclInProgress); ++r) {
+      (void)hipSetDevice(g->dev[r]);
+      nr = ncclCommInitRankConfig(&g->comm[r], n, id, r, &cfg);
+    }
+    ncclResult_t ne = ncclGroupEnd();
+    if (nr == ncclSuccess || nr == ncclInProgress) nr = ne;
+    int rc = B2P_OK;
+    if (nr != ncclSuccess && nr != ncclInProgress) {
+      char d[160];
+      snprintf(d, sizeof d, "%s (%d members)", ncclGetErrorString(nr), n);
+      rc = gerr(g, B2P_EHIP, "ncclCommInitRankConfig", d);
+      abort_comms(g);
+    } else {
+      rc = settle_comms(g, deadline, "RCCL communicator set-up");
+    }
+    if (rc != B2P_OK) {
+      snprintf(g_gerr, sizeof g_gerr, "%s", g->err);
+      g->comm.clear();
       delete g;
       return rc;
     }
@@ -91,6 +216,7 @@ int b2p_group_open(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int mode) {
 
 int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
   if (!g || !spectra || !root_out) return B2P_EINVAL;
+  if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_gather", "group aborted earlier; close it");
   // every member's deferred finalize must be enqueued before the gather
   for (int r = 0; r < g->n; ++r) {
     int rc = b2p_internal_flush(g->ctx[r]);
@@ -105,9 +231,9 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
                       g->stream[r]);
     }
     ncclResult_t ne = ncclGroupEnd();
-    if (nr != ncclSuccess || ne != ncclSuccess)
+    if ((nr != ncclSuccess && nr != ncclInProgress) || (ne != ncclSuccess && ne != ncclInProgress))
       return gerr(g, B2P_EHIP, "ncclGather", ncclGetErrorString(nr != ncclSuccess ? nr : ne));
-    return B2P_OK;
+    return settle_comms(g, now_s() + 1e-3 * g->timeout_ms, "ncclGather enqueue");
   }
   for (int r = 0; r < g->n; ++r) {
     (void)hipSetDevice(g->dev[r]);
@@ -126,6 +252,7 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
 
 int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint64_t *root_sum) {
   if (!g || !sums || !root_sum || !count) return B2P_EINVAL;
+  if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_reduce", "group aborted earlier; close it");
   for (int r = 0; r < g->n; ++r) {
     int rc = b2p_internal_flush(g->ctx[r]);
     if (rc != B2P_OK) return gerr(g, rc, "flush", b2p_last_error(g->ctx[r]));
@@ -138,9 +265,9 @@ int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint
                       g->stream[r]);
     }
     ncclResult_t ne = ncclGroupEnd();
-    if (nr != ncclSuccess || ne != ncclSuccess)
+    if ((nr != ncclSuccess && nr != ncclInProgress) || (ne != ncclSuccess && ne != ncclInProgress))
       return gerr(g, B2P_EHIP, "ncclReduce", ncclGetErrorString(nr != ncclSuccess ? nr : ne));
-    return B2P_OK;
+    return settle_comms(g, now_s() + 1e-3 * g->timeout_ms, "ncclReduce enqueue");
   }
   // mode 1: rows copied to the root, summed there
   (void)hipSetDevice(g->dev[0]);
@@ -176,19 +303,30 @@ int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint
 
 int b2p_group_sync(b2p_group_t *g) {
   if (!g) return B2P_EINVAL;
+  if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_sync", "group aborted earlier; close it");
+  // enqueue every member's deferred finalize, then wait -- polled against
+  // the group's deadline rather than hipStreamSynchronize, so a collective
+  // that never completes is reported instead of hanging the caller
   for (int r = 0; r < g->n; ++r) {
-    int rc = b2p_sync(g->ctx[r]);
-    if (rc != B2P_OK) return rc;
+    int rc = b2p_internal_flush(g->ctx[r]);
+    if (rc != B2P_OK) return gerr(g, rc, "flush", b2p_last_error(g->ctx[r]));
   }
-  return B2P_OK;
+  return wait_streams(g, "b2p_group_sync");
 }
 
 const char *b2p_group_last_error(const b2p_group_t *g) { return g ? g->err : g_gerr; }
 
 int b2p_group_close(b2p_group_t *g) {
   if (!g) return B2P_EINVAL;
-  for (auto c : g->comm)
-    if (c) ncclCommDestroy(c);
+  // non-blocking communicators: finalize (polled, bounded), then destroy;
+  // past the limit they are aborted instead
+  if (!g->dead && !g->comm.empty()) {
+    for (auto c : g->comm)
+      if (c) ncclCommFinalize(c);
+    if (settle_comms(g, now_s() + 1e-3 * g->timeout_ms, "ncclCommFinalize") == B2P_OK)
+      for (auto c : g->comm)
+        if (c) ncclCommDestroy(c);
+  }
   if (g->scratch) {
     (void)hipSetDevice(g->dev[0]);
     (void)hipFree(g->scratch);

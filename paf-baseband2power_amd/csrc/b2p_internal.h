@@ -95,7 +95,7 @@ struct AssembleArgs {
   uint32_t nchunk;
   unsigned long long *counts;   // nchunk placed, then before / after / bad chunk
 };
-hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s);
+hipError_t launch_assemble(const AssembleArgs &a, uint32_t grid_cap, hipStream_t s);
 hipError_t launch_convert(const ConvertArgs &a, hipStream_t s);
 hipError_t launch_warm(hipStream_t s);
 hipError_t launch_sum_rows(const SumRowsArgs &a, hipStream_t s);

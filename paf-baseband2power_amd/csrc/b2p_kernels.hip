@@ -444,31 +444,20 @@ __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
     if (cnt[j]) atomicAdd(&a.counts[j], cnt[j]);
 }
 
-// B2P_ASM_VARIANT: 0 nt load+store, payload loads issued before the header
-// is decoded (default); 1 the same with 2 frames per iteration; 2 plain
-// loads/stores; 3 nt loads / plain stores; 4 header first, then payload (the
-// round-1 kernel); 5 header first, 2 frames.  B2P_ASM_GRID: workgroups of 4 waves
-hipError_t launch_assemble(const AssembleArgs &a, hipStream_t s) {
+// Nontemporal loads and stores, payload loads issued before the header is
+// decoded, one frame per wave per iteration, 8192 workgroups of 4 waves: the
+// winner of the round-1 sweep over load/store policy, frames per iteration,
+// header-first ordering and grid (profiles/r01_assemble_sweep.txt).
+// grid_cap (b2p_tuning_t.assemble_grid) overrides the workgroup cap.
+hipError_t launch_assemble(const AssembleArgs &a, uint32_t grid_cap, hipStream_t s) {
   if (a.nchunk > 256) return hipErrorInvalidValue;
-  static const int variant = getenv("B2P_ASM_VARIANT") ? atoi(getenv("B2P_ASM_VARIANT")) : 0;
-  static const long grid_env = getenv("B2P_ASM_GRID") ? atol(getenv("B2P_ASM_GRID")) : 0;
-  const int k = (variant == 1 || variant == 5) ? 2 : 1;
-  uint64_t blocks = (a.ndf + 4 * k - 1) / (4 * k);  // 4 waves per workgroup
-  const uint64_t cap = grid_env > 0 ? (uint64_t)grid_env : 8192;  // swept: profiles/r01_assemble_sweep.txt
+  uint64_t blocks = (a.ndf + 3) / 4;  // 4 waves per workgroup
+  const uint64_t cap = grid_cap ? grid_cap : 8192;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  AssembleArgs arg = a;
-  void *args[] = {&arg};
-  const void *f;
-  switch (variant) {
-    case 1: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 2, true>); break;
-    case 2: f = reinterpret_cast<const void *>(b2p_assemble_kernel<false, false, 1, true>); break;
-    case 3: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, false, 1, true>); break;
-    case 4: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 1, false>); break;
-    case 5: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 2, false>); break;
-    default: f = reinterpret_cast<const void *>(b2p_assemble_kernel<true, true, 1, true>);
-  }
-  return hipLaunchKernel(f, dim3((uint32_t)blocks), dim3(256), args, 0, s);
+  hipLaunchKernelGGL((b2p_assemble_kernel<true, true, 1, true>), dim3((uint32_t)blocks), dim3(256),
+                     0, s, a);
+  return hipGetLastError();
 }
 
 // ---- launchers --------------------------------------------------------------

@@ -65,6 +65,8 @@ typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
   int mean;
   int nsub;
   int nsplit; /* > 1: one ring's integration split by time over nsplit GPUs */
+  int gather;  /* -G: 0 auto (RCCL unless members share a GPU), 1 RCCL, 2 copies */
+  int coll_timeout_s; /* -T: RCCL set-up / collective time limit */
 } conf_t;
 
 typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
@@ -103,6 +105,9 @@ static void usage(void) {
           " -n  Number of sub-bands (rings key_in + 0x10*r, GPUs d + r), gathered to GPU d\n"
           " -t  Split each integration of the one input ring by time over N GPUs (d + r);\n"
           "     exact partial sums are reduced on GPU d (host ring: N PCIe links in parallel)\n"
+          " -G  Transport for -n / -t: rccl | copy (default: RCCL unless members share a GPU)\n"
+          " -T  Time limit in s for the RCCL set-up and each collective (default 60); past it\n"
+          "     the communicators are aborted and the stage exits with an error\n"
           " -h  show help\n");
 }
 
@@ -491,6 +496,7 @@ static void *worker_split(void *arg) {
         uint64_t *parts[MAX_SUB];
         for (int r = 0; r < sh->nsub; r++) parts[r] = sh->sub[r].part_dev;
         rc = b2p_group_reduce(sh->grp, parts, sh->nout, sh->root_sum);
+        if (rc == B2P_OK) rc = b2p_group_sync(sh->grp); /* bounded by -T */
         if (rc == B2P_OK)
           rc = b2p_finalize_sums(s0->ctx, sh->root_sum, 1, sh->nsamp_full, s0->spec_dev);
         if (rc == B2P_OK) rc = b2p_memcpy(s0->ctx, sh->spec_host, s0->spec_dev, sh->obytes, 2);
@@ -516,6 +522,17 @@ static void *worker_split(void *arg) {
   return NULL;
 }
 
+/* RCCL refuses two members on one GPU, so members sharing one use peer
+ * copies unless -G rccl insists (which then fails at set-up, reported) */
+static int group_mode(const conf_t *conf, int dup_dev, multilog_t *log) {
+  if (conf->gather == 1) {
+    if (dup_dev) multilog(log, LOG_WARNING, "-G rccl with members sharing a GPU: RCCL will refuse it");
+    return 0;
+  }
+  if (conf->gather == 2) return 1;
+  return dup_dev ? 1 : 0;
+}
+
 int main(int argc, char *argv[]) {
   int arg;
   conf_t conf;
@@ -523,10 +540,11 @@ int main(int argc, char *argv[]) {
   conf.npol_out = 1;
   conf.nsub = 1;
   conf.nsplit = 1;
+  conf.coll_timeout_s = 60;
   strcpy(conf.dir, ".");
   int have_in = 0, have_out = 0;
 
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:mh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:G:T:mh")) != -1) {
     switch (arg) {
       case 'h':
         usage();
@@ -552,11 +570,21 @@ int main(int argc, char *argv[]) {
       case 'n': conf.nsub = atoi(optarg); break;
       case 't': conf.nsplit = atoi(optarg); break;
       case 'm': conf.mean = 1; break;
+      case 'G':
+        if (!strcmp(optarg, "rccl")) conf.gather = 1;
+        else if (!strcmp(optarg, "copy")) conf.gather = 2;
+        else {
+          fprintf(stderr, "-G takes rccl or copy, not %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        break;
+      case 'T': conf.coll_timeout_s = atoi(optarg); break;
       default: usage(); return EXIT_FAILURE;
     }
   }
   if (!have_in || !have_out || conf.nsub < 1 || conf.nsub > MAX_SUB || conf.nsplit < 1 ||
-      conf.nsplit > MAX_SUB || (conf.nsub > 1 && conf.nsplit > 1)) {
+      conf.nsplit > MAX_SUB || (conf.nsub > 1 && conf.nsplit > 1) || conf.coll_timeout_s < 1 ||
+      conf.coll_timeout_s > 86400) {
     usage();
     return EXIT_FAILURE;
   }
@@ -678,6 +706,13 @@ int main(int argc, char *argv[]) {
   b2p_info_t info;
   b2p_get_info(sub[0].ctx, &info);
   sh.nout = info.nout;
+  for (int r = 0; r < nmem && nmem > 1; r++) { /* which physical GPU each member drives */
+    b2p_info_t mi;
+    char bus[32] = "?";
+    b2p_get_info(sub[r].ctx, &mi);
+    b2p_device_pci_bus_id((int)mi.device, bus, (int)sizeof bus);
+    multilog(log, LOG_INFO, "member %d: GPU %u (PCI %s)", r, mi.device, bus);
+  }
   sh.obytes = (uint64_t)conf.nsub * info.nout * sizeof(float);
   if (split)
     multilog(log, LOG_INFO, "time split: each integration of ring %x over %d GPUs, %" PRIu64
@@ -749,11 +784,12 @@ int main(int argc, char *argv[]) {
       goto done;
     b2p_ctx_t *ctxs[MAX_SUB];
     for (int r = 0; r < nmem; r++) ctxs[r] = sub[r].ctx;
-    const char *gm = getenv("B2P_GATHER");
-    int mode = dup_dev || (gm && !strcmp(gm, "copy")) ? 1 : 0;
-    int rc = b2p_group_open(&sh.grp, ctxs, nmem, mode);
+    const int mode = group_mode(&conf, dup_dev, log);
+    int rc = b2p_group_open_timed(&sh.grp, ctxs, nmem, mode, conf.coll_timeout_s * 1000);
     if (rc != B2P_OK) {
-      multilog(log, LOG_ERR, "b2p_group_open: %s", b2p_group_last_error(NULL));
+      multilog(log, LOG_ERR, "b2p_group_open: %s: %s", b2p_strerror(rc), b2p_group_last_error(NULL));
+      fprintf(stderr, "paf_baseband2power: b2p_group_open: %s: %s\n", b2p_strerror(rc),
+              b2p_group_last_error(NULL));
       goto done;
     }
     multilog(log, LOG_INFO, "reduce of %d time shares to GPU %d via %s", nmem, sub[0].device,
@@ -765,12 +801,12 @@ int main(int argc, char *argv[]) {
     if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, sh.obytes) != B2P_OK) goto done;
     b2p_ctx_t *ctxs[MAX_SUB];
     for (int r = 0; r < conf.nsub; r++) ctxs[r] = sub[r].ctx;
-    /* RCCL needs distinct devices; members sharing one GPU use peer copies */
-    const char *gm = getenv("B2P_GATHER");
-    int mode = dup_dev || (gm && !strcmp(gm, "copy")) ? 1 : 0;
-    int rc = b2p_group_open(&sh.grp, ctxs, conf.nsub, mode);
+    const int mode = group_mode(&conf, dup_dev, log);
+    int rc = b2p_group_open_timed(&sh.grp, ctxs, conf.nsub, mode, conf.coll_timeout_s * 1000);
     if (rc != B2P_OK) {
-      multilog(log, LOG_ERR, "b2p_group_open: %s", b2p_group_last_error(NULL));
+      multilog(log, LOG_ERR, "b2p_group_open: %s: %s", b2p_strerror(rc), b2p_group_last_error(NULL));
+      fprintf(stderr, "paf_baseband2power: b2p_group_open: %s: %s\n", b2p_strerror(rc),
+              b2p_group_last_error(NULL));
       goto done;
     }
     multilog(log, LOG_INFO, "gather of %d sub-bands to GPU %d via %s", conf.nsub, sub[0].device,

@@ -32,6 +32,8 @@ B2P_EHIP = -6
 B2P_ENOMEM = -7
 B2P_EALIGN = -8
 B2P_EFAILED = -9
+B2P_ETIMEDOUT = -10
+ABI_VERSION = 2
 
 
 class B2PError(RuntimeError):
@@ -63,6 +65,25 @@ class Stats(C.Structure):
                 ("finalize_ms", C.c_double), ("finalizes", C.c_uint64)]
 
 
+class Tuning(C.Structure):
+    """b2p_tuning_t (include/b2p.h): an explicit launch variant for tuning
+    sweeps; 0 / -1 fields keep the measured defaults."""
+    _fields_ = [("size", C.c_uint32), ("max_threads", C.c_int32), ("threads", C.c_int32),
+                ("wg_per_cu", C.c_int32), ("row_groups", C.c_int32), ("replicas", C.c_int32),
+                ("unroll", C.c_int32), ("nontemporal", C.c_int32), ("interleave", C.c_int32),
+                ("fuse", C.c_int32), ("stage_mib", C.c_int32), ("assemble_grid", C.c_int32)]
+
+    @classmethod
+    def make(cls, **kw) -> "Tuning":
+        t = cls()
+        lib().b2p_tuning_init(C.byref(t))
+        for k, v in kw.items():
+            if k not in dict(cls._fields_) or k == "size":
+                raise KeyError(f"no tuning field {k!r}")
+            setattr(t, k, int(v))
+        return t
+
+
 # name -> (restype, argtypes); must match include/b2p.h exactly
 _P = C.c_void_p
 PROTOTYPES = {
@@ -75,6 +96,9 @@ PROTOTYPES = {
     "b2p_block_bytes": (C.c_uint64, [C.POINTER(Geom)]),
     "b2p_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "b2p_open": (C.c_int, [C.POINTER(_P), C.POINTER(Geom), C.c_int]),
+    "b2p_open_tuned": (C.c_int, [C.POINTER(_P), C.POINTER(Geom), C.c_int, C.POINTER(Tuning)]),
+    "b2p_tuning_init": (None, [C.POINTER(Tuning)]),
+    "b2p_device_pci_bus_id": (C.c_int, [C.c_int, C.c_char_p, C.c_int]),
     "b2p_close": (C.c_int, [_P]),
     "b2p_get_info": (C.c_int, [_P, C.POINTER(Info)]),
     "b2p_set_stream": (C.c_int, [_P, _P]),
@@ -103,11 +127,15 @@ PROTOTYPES = {
     "b2p_finalize_sums": (C.c_int, [_P, _P, C.c_uint64, C.c_uint64, _P]),
     "b2p_group_reduce": (C.c_int, [_P, _P, C.c_uint64, _P]),
     "b2p_group_open": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int]),
+    "b2p_group_open_timed": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int, C.c_int]),
     "b2p_group_gather": (C.c_int, [_P, C.POINTER(_P), _P]),
     "b2p_group_sync": (C.c_int, [_P]),
     "b2p_group_last_error": (C.c_char_p, [_P]),
     "b2p_group_close": (C.c_int, [_P]),
 }
+
+# the test build's extra entry (lib/hooks/libpafb2p.so, -DB2P_TEST_HOOKS)
+HOOK_PROTOTYPES = {"b2p_test_inject_push_fail": (C.c_int, [_P, C.c_long])}
 
 _lib = None
 
@@ -124,7 +152,12 @@ def lib() -> C.CDLL:
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.b2p_abi_version() != 1:
+        for name, (res, args) in HOOK_PROTOTYPES.items():
+            f = getattr(L, name, None)
+            if f is not None:
+                f.restype = res
+                f.argtypes = args
+        if L.b2p_abi_version() != ABI_VERSION:
             raise ImportError("libpafb2p ABI version mismatch")
         _lib = L
     return _lib

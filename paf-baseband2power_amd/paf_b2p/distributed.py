@@ -16,10 +16,64 @@ each is issued once per batch of integrations, not per block.
 """
 from __future__ import annotations
 
+import datetime
 import os
+import sys
+import threading
 
 import torch
 import torch.distributed as dist
+
+# How long one multi-rank phase may take before the rank gives up: the
+# rendezvous, a communicator's first collective (RCCL sets up its channels
+# there), one timed region.  Seconds; bench.py --dist-timeout overrides.
+DEFAULT_TIMEOUT_S = 300.0
+WATCHDOG_EXIT = 4
+
+
+class Watchdog:
+    """Bounds each multi-rank phase.  A rank stuck in a rendezvous or inside
+    an RCCL call cannot be unwound from Python, so when a phase outlives its
+    limit the rank names the phase on stderr and leaves with exit code 4
+    (os._exit; torch.distributed.run then stops the other ranks).  This
+    turns "the first 8-rank RCCL run hangs until the driver's limit" into a
+    bounded, labelled failure."""
+
+    def __init__(self, rank: int, limit_s: float, exit_code: int = WATCHDOG_EXIT, out=None):
+        self.rank, self.limit_s, self.exit_code = rank, float(limit_s), exit_code
+        self.out = out or sys.stderr
+        self._timer = None
+        self.phase_name = None
+
+    def _expire(self, name: str, limit: float) -> None:
+        print(f"bench.py: rank {self.rank}: {name} did not finish within {limit:g} s "
+              f"(stuck rendezvous or collective); exiting {self.exit_code}", file=self.out, flush=True)
+        os._exit(self.exit_code)
+
+    def arm(self, name: str, limit_s: float | None = None) -> None:
+        self.disarm()
+        limit = self.limit_s if limit_s is None else float(limit_s)
+        self.phase_name = name
+        self._timer = threading.Timer(limit, self._expire, args=(name, limit))
+        self._timer.daemon = True
+        self._timer.start()
+
+    def disarm(self) -> None:
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+        self.phase_name = None
+
+    def phase(self, name: str, limit_s: float | None = None):
+        wd = self
+
+        class _P:
+            def __enter__(self_):
+                wd.arm(name, limit_s)
+
+            def __exit__(self_, *exc):
+                wd.disarm()
+        return _P()
 
 
 def env_ranks() -> tuple[int, int, int]:
@@ -41,14 +95,44 @@ def device_of(local_rank: int) -> int:
     return local_rank % n if n > 0 else 0
 
 
-def init(backend: str, local_rank: int) -> None:
+def init(backend: str, local_rank: int, timeout_s: float = DEFAULT_TIMEOUT_S) -> None:
+    """init_process_group with an explicit timeout: it bounds the TCP-store
+    rendezvous and, for "nccl" (RCCL), every collective (torch's watchdog
+    aborts the communicator past it).  The eager RCCL set-up that device_id
+    starts is bounded by the caller's Watchdog."""
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    td = datetime.timedelta(seconds=timeout_s)
     if backend == "nccl":
         dev = device_of(local_rank)
         torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev), timeout=td)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=td)
+
+
+def observed_world() -> dict:
+    """what the live process group is, read back after its first collective
+    (not what was asked for): backend, size, and RCCL ranks"""
+    if not dist.is_initialized():
+        return {"backend": None, "world_size": 1, "rccl_ranks": 0}
+    be = str(dist.get_backend())
+    n = dist.get_world_size()
+    return {"backend": be, "world_size": n, "rccl_ranks": n if be == "nccl" else 0}
+
+
+def gather_identities(ident: dict) -> list[dict]:
+    """every rank's identity record (rank, host, device, PCI bus id ...), in
+    rank order, on every rank"""
+    if not dist.is_initialized():
+        return [ident]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, ident)
+    return out
+
+
+def distinct_gpus(idents: list[dict]) -> int:
+    """physical GPUs behind the ranks: distinct (host, PCI bus id) pairs"""
+    return len({(i.get("host"), i.get("pci_bus_id")) for i in idents})
 
 
 def gather_spectra(local: torch.Tensor) -> list[torch.Tensor] | None:

@@ -32,12 +32,18 @@ class DeviceBuffer:
 
 
 class Integrator:
-    def __init__(self, geom=None, device: int = 0, **geom_kw):
+    def __init__(self, geom=None, device: int = 0, tuning: dict | None = None, **geom_kw):
+        """tuning: b2p_tuning_t fields (tools/tune.py); None = the measured
+        defaults (b2p_open)"""
         g = geom if isinstance(geom, L.Geom) else make_geom(**(geom or {}), **geom_kw)
         self.geom = g
         self._ctx = C.c_void_p()
         lib = L.lib()
-        L.check(lib.b2p_open(C.byref(self._ctx), C.byref(g), device), None)
+        if tuning:
+            t = L.Tuning.make(**tuning)
+            L.check(lib.b2p_open_tuned(C.byref(self._ctx), C.byref(g), device, C.byref(t)), None)
+        else:
+            L.check(lib.b2p_open(C.byref(self._ctx), C.byref(g), device), None)
         info = L.Info()
         L.check(lib.b2p_get_info(self._ctx, C.byref(info)), self._ctx)
         self.info = info
@@ -220,16 +226,23 @@ def device_count() -> int:
     return n.value if rc == L.B2P_OK else 0
 
 
+def pci_bus_id(device: int) -> str:
+    """b2p_device_pci_bus_id: the physical GPU behind a device index"""
+    buf = C.create_string_buffer(32)
+    L.check(L.lib().b2p_device_pci_bus_id(device, buf, 32))
+    return buf.value.decode()
+
+
 class Group:
     """b2p_group: gather the spectra of N Integrators (one per GPU /
     sub-band) to the first one's device -- RCCL (mode 0) or peer copies
     (mode 1, members sharing a device)."""
 
-    def __init__(self, members: list[Integrator], mode: int = 0):
+    def __init__(self, members: list[Integrator], mode: int = 0, timeout_ms: int = 60000):
         self.members = members
         arr = (C.c_void_p * len(members))(*[m._ctx.value for m in members])
         self._g = C.c_void_p()
-        rc = L.lib().b2p_group_open(C.byref(self._g), arr, len(members), mode)
+        rc = L.lib().b2p_group_open_timed(C.byref(self._g), arr, len(members), mode, timeout_ms)
         if rc != L.B2P_OK:
             raise L.B2PError(rc, L.lib().b2p_group_last_error(None).decode(errors="replace"))
 
@@ -238,7 +251,12 @@ class Group:
         rc = L.lib().b2p_group_gather(self._g, arr, C.c_void_p(root_out_ptr))
         if rc != L.B2P_OK:
             raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
-        L.check(L.lib().b2p_group_sync(self._g))
+        self.sync()
+
+    def sync(self) -> None:
+        rc = L.lib().b2p_group_sync(self._g)
+        if rc != L.B2P_OK:
+            raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
 
     def reduce(self, sums_ptrs: list[int], count: int, root_sum_ptr: int) -> None:
         """b2p_group_reduce: exact uint64 sum of every member's partial sums
@@ -247,7 +265,7 @@ class Group:
         rc = L.lib().b2p_group_reduce(self._g, arr, count, C.c_void_p(root_sum_ptr))
         if rc != L.B2P_OK:
             raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
-        L.check(L.lib().b2p_group_sync(self._g))
+        self.sync()
 
     def close(self) -> None:
         if self._g:

@@ -65,7 +65,8 @@ def _ring_device(gpu: int, r: int) -> int:
 def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
-        device_ring: bool = False, split: int = 1, bin_dir: str | None = None) -> list:
+        device_ring: bool = False, split: int = 1, bin_dir: str | None = None,
+        stage_args: list | None = None) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
     sub-bands and gathers their spectra to its first GPU).
@@ -73,10 +74,11 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
     (dada_db -g): paf_diskdb copies into HBM and
     paf_baseband2power integrates the block in place.  split=N cuts every
     integration of a (single) chain by time over N GPUs (paf_baseband2power
-    -t N, SURVEY.md 8e second mode)."""
+    -t N, SURVEY.md 8e second mode).  stage_args: extra paf_baseband2power
+    options (e.g. ["-G", "rccl", "-T", "30"])."""
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
-                             timeout, hfname, device_ring)
+                             timeout, hfname, device_ring, stage_args)
     c = read_conf(conf_path)
     hdr = hfname or c["diskdb_hfname"]
     if not os.path.isabs(hdr):
@@ -113,6 +115,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
                 b2p_cmd.append("-m")
             if split > 1:
                 b2p_cmd += ["-t", str(split)]
+            b2p_cmd += list(stage_args or [])
             procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
                                           stderr=subprocess.PIPE))
             procs.append(subprocess.Popen(b2p_cmd, stderr=subprocess.PIPE))
@@ -174,7 +177,7 @@ def _wait_all(procs, timeout):
 
 
 def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, mean, timeout,
-                  hfname, device_ring=False):
+                  hfname, device_ring=False, stage_args=None):
     c = read_conf(conf_path)
     hdr = _resolve_header(c, conf_path, hfname)
     os.makedirs(directory, exist_ok=True)
@@ -199,6 +202,7 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
             cmd += ["-f", layout]
         if mean:
             cmd.append("-m")
+        cmd += list(stage_args or [])
         procs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE))
         for r in range(nsub):
             dfile = datafiles[r]

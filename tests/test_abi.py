@@ -53,9 +53,9 @@ def test_struct_layout_matches_header(tmp_path):
 #include <stddef.h>
 #include "b2p.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(b2p_geom_t), offsetof(b2p_geom_t, nsamp_int),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(b2p_geom_t), offsetof(b2p_geom_t, nsamp_int),
          offsetof(b2p_geom_t, mean), sizeof(b2p_info_t), sizeof(b2p_stats_t),
-         offsetof(b2p_stats_t, kernel_ms));
+         offsetof(b2p_stats_t, kernel_ms), sizeof(b2p_tuning_t), offsetof(b2p_tuning_t, assemble_grid));
   return 0;
 }''')
     exe = tmp_path / "probe"
@@ -64,7 +64,8 @@ int main(void) {
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
                                           check=True).stdout.split()]
     want = [C.sizeof(L.Geom), L.Geom.nsamp_int.offset, L.Geom.mean.offset, C.sizeof(L.Info),
-            C.sizeof(L.Stats), L.Stats.kernel_ms.offset]
+            C.sizeof(L.Stats), L.Stats.kernel_ms.offset, C.sizeof(L.Tuning),
+            L.Tuning.assemble_grid.offset]
     assert got == want
 
 
@@ -120,3 +121,51 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         paf_b2p.Integrator(paf_b2p.bmf_geom())
     with pytest.raises(ImportError):
         L.lib()
+
+
+def test_release_library_has_no_test_hook():
+    """The shipped libpafb2p.so carries no fault-injection entry and reads no
+    environment knobs (launch variants go through b2p_open_tuned); the test
+    build (lib/hooks/, -DB2P_TEST_HOOKS) is the only one with the hook."""
+    lib = C.CDLL(L.LIB_PATH)
+    assert not hasattr(lib, "b2p_test_inject_push_fail")
+    blob = open(L.LIB_PATH, "rb").read()
+    for word in (b"B2P_INJECT", b"B2P_ASM_VARIANT", b"B2P_UNROLL", b"B2P_FUSE", b"B2P_STAGE"):
+        assert word not in blob, word
+    und = subprocess.run(["nm", "-D", "--undefined-only", L.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert not re.search(r"\bgetenv\b", und)
+    hooks = os.path.join(os.path.dirname(L.LIB_PATH), "hooks", "libpafb2p.so")
+    assert hasattr(C.CDLL(hooks), "b2p_test_inject_push_fail")
+
+
+def test_tuning_defaults_and_refusals():
+    """b2p_tuning_init marks every field "default"; out-of-range values are
+    refused with B2P_EINVAL before any device is touched (no clamping)"""
+    t = L.Tuning.make()
+    assert t.size == C.sizeof(L.Tuning)
+    assert (t.nontemporal, t.interleave, t.fuse) == (-1, -1, -1)
+    assert (t.max_threads, t.unroll, t.replicas, t.stage_mib) == (0, 0, 0, 0)
+    g = L.Geom()
+    L.lib().b2p_geom_bmf(C.byref(g))
+    for bad in ({"unroll": 5}, {"max_threads": 32}, {"threads": 100}, {"wg_per_cu": 33},
+                {"replicas": 2000}, {"nontemporal": 2}, {"fuse": -2}, {"stage_mib": 20000},
+                {"row_groups": -1}):
+        ctx = C.c_void_p()
+        tt = L.Tuning.make(**bad)
+        assert L.lib().b2p_open_tuned(C.byref(ctx), C.byref(g), 0, C.byref(tt)) == L.B2P_EINVAL, bad
+        assert b"tuning" in L.lib().b2p_last_error(None)
+    tt = L.Tuning.make()
+    tt.size = 4
+    ctx = C.c_void_p()
+    assert L.lib().b2p_open_tuned(C.byref(ctx), C.byref(g), 0, C.byref(tt)) == L.B2P_EINVAL
+    with pytest.raises(KeyError):
+        L.Tuning.make(bogus=1)
+
+
+def test_group_refuses_bad_timeout_and_pci_args():
+    grp = C.c_void_p()
+    arr = (C.c_void_p * 1)(None)
+    assert L.lib().b2p_group_open_timed(C.byref(grp), arr, 1, 0, 0) == L.B2P_EINVAL
+    assert L.lib().b2p_device_pci_bus_id(0, None, 32) == L.B2P_EINVAL
+    assert L.lib().b2p_strerror(L.B2P_ETIMEDOUT).decode().startswith("collective did not complete")

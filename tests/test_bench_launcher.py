@@ -163,3 +163,37 @@ def test_cpu_share_parsing(monkeypatch, tmp_path):
     assert cb.effective_cpus() == len(os.sched_getaffinity(0))
     env = cb.child_env(16)
     assert env["OMP_NUM_THREADS"] == "16" and env["OMP_PLACES"] == "cores"
+
+
+def test_watchdog_names_the_stuck_phase_and_exits_4(tmp_path):
+    """a phase that outlives its limit ends the rank with exit 4 and a line
+    naming the phase (a rank stuck inside RCCL cannot be unwound)"""
+    code = ("import time, sys; sys.path.insert(0, %r)\n"
+            "from paf_b2p.distributed import Watchdog\n"
+            "w = Watchdog(3, 0.5)\n"
+            "with w.phase('quick phase'):\n    time.sleep(0.1)\n"
+            "w.arm('first nccl collective (communicator set-up)')\n"
+            "time.sleep(30)\n" % os.path.join(REPO, "paf-baseband2power_amd"))
+    t0 = __import__("time").time()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 4
+    assert __import__("time").time() - t0 < 20
+    assert "rank 3: first nccl collective (communicator set-up) did not finish within 0.5 s" in r.stderr
+
+
+def test_missing_rank_rendezvous_is_bounded():
+    """a launched rank whose peer never arrives gives up within
+    --dist-timeout (non-zero exit) instead of waiting for the driver's limit"""
+    import socket
+    import time
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    t0 = time.time()
+    r = _run(["--gpus", "2", "--steps", "2", "--dist-backend", "gloo", "--dist-timeout", "6"],
+             {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+              "MASTER_PORT": str(port)})
+    assert r.returncode != 0
+    assert time.time() - t0 < 120
+    assert r.stdout.strip() == ""

@@ -33,8 +33,14 @@ def test_bench_prints_one_contract_line(gpu):
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert rf["traffic"] is None or rf["traffic"] > 0
     cb = d["cpu_baseline"]
-    assert cb["unit"] == d["unit"] and cb["kind"] in ("port", "reference") and cb["cores"] >= 1
+    assert cb["unit"] == d["unit"] and cb["kind"] == "port-tuned" and cb["cores"] >= 1
     assert d["value"] > 0 and cb["value"] > 0 and cb["value_1thread"] > 0
+    assert cb["equals_oracle"] is True and cb["oracle_value"] > 0
+    assert cb["isa"] in ("avx512vnni", "avx512bw", "avx2", "scalar")
+    # the ranks that ran, read back from the process (no group at N = 1)
+    assert d["rccl_ranks"] == 0 and d["distinct_gpus"] == 1
+    rd = d["rank_devices"]
+    assert len(rd) == 1 and rd[0]["rank"] == 0 and rd[0]["pci_bus_id"].count(":") == 2
     assert d["verified"] is True and d["ranks"] == 1 and d["timed_regions"] >= 1
     lo, hi = d["ms_per_step_range"]
     assert lo <= d["ms_per_step"] <= hi
@@ -57,3 +63,30 @@ def test_bench_gpus2_gloo_spawns_two_ranks(gpu):
     assert "2 ranks sharing 1 MI355X" in w or "over 2 MI355X" in w   # 1 or >= 2 GPUs visible
     assert d["config"]["launcher"].startswith("bench.py --gpus")
     assert len(d["per_rank_ms_per_step"]) == 2 and d["cpu_baseline"] is None
+    assert d["dist_backend"] == "gloo" and [x["rank"] for x in d["rank_devices"]] == [0, 1]
+
+
+def test_configs3_four_rank_rehearsal_full_size(gpu):
+    """configs[3] as the driver's 4-GPU run would do it, rehearsed with gloo:
+    4 ranks, each integrating full 1 GiB 256-ch int8 blocks of its own
+    sub-band (4 distinct blocks per rank, 16 GiB in all), the K spectra of
+    every rank gathered to rank 0, every spectrum checked against the C
+    oracle.  The ranks share this box's GPU, so the rate means nothing; the
+    plumbing (launcher, world check, watchdog, identities, gather,
+    verification) is what runs."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "4", "--steps", "4",
+                        "--warmup", "1", "--dist-backend", "gloo", "--min-seconds", "0",
+                        "--dist-timeout", "120"],
+                       capture_output=True, text=True, timeout=600, cwd=REPO,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["ranks"] == 4 and d["verified"] is True
+    assert d["config"]["bytes_per_integration"] == 1 << 30 and d["config"]["nchan"] == 256
+    assert "configs[3]" in d["config"]["baseline_config"]
+    assert d["verification"]["gather"].startswith("rank 0 holds")
+    assert "4 distinct block" in d["verification"]["what"]
+    assert [x["rank"] for x in d["rank_devices"]] == [0, 1, 2, 3]
+    assert d["distinct_gpus"] >= 1 and d["dist_backend"] == "gloo" and d["rccl_ranks"] == 0

@@ -76,6 +76,36 @@ def test_multi_subband_c_host_gathered(gpu, tmp_path):
     assert "gather of 3 sub-bands" in log
 
 
+def test_c_host_reports_rccl_setup_failure(gpu, tmp_path):
+    """-n 2 on the one-GPU box with -G rccl: RCCL refuses two members on one
+    device.  The stage must log the b2p_group_open failure and exit non-zero
+    within its -T limit -- never hang (the first real multi-rank RCCL run is
+    the driver's, so its failure has to be loud and bounded)."""
+    import time
+    from test_gpu_pipeline import write_conf
+    if paf_b2p.device_count() != 1:
+        pytest.skip("needs members that share one GPU")
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 12)
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\n"
+                     "TSAMP 0.84375\n")
+    files = []
+    for r in range(2):
+        f = tmp_path / f"sb{r}.dada"
+        dada.write_dada_file(str(f), "x 1\n", co.fill_synthetic(g, g.block_bytes, SEED, r, 0))
+        files.append(str(f))
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 12, 1, 1024, 256, 0x7c10, 0x7d10, str(hfile))
+    t0 = time.time()
+    with pytest.raises(RuntimeError) as e:
+        pipeline.run(str(conf), str(tmp_path / "out"), 0, files, nsub=2, gather=True, timeout=120,
+                     stage_args=["-G", "rccl", "-T", "20"])
+    assert time.time() - t0 < 100
+    assert "paf_baseband2power: rc=1" in str(e.value)
+    log = open(str(tmp_path / "out" / "paf_baseband2power.log")).read()
+    assert "b2p_group_open" in log and "member 1: GPU 0 (PCI" in log
+
+
 # ---- time-split mode (SURVEY.md 8e, second mode) -----------------------------
 
 @pytest.mark.parametrize("npol_out,mean", [(1, 0), (2, 1)])

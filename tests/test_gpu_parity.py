@@ -7,6 +7,8 @@ oracle on the downloaded block and through size-independent properties
 (chunking/order invariance, determinism, back-to-back integrations).
 """
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -14,7 +16,7 @@ import pytest
 import b2p_oracle as npo
 import oracle_c as co
 import paf_b2p
-from conftest import golden_geom, load_golden
+from conftest import REPO, golden_geom, load_golden
 from paf_b2p import _lib as L
 
 pytestmark = pytest.mark.gpu
@@ -27,36 +29,25 @@ def to_b2p(g: npo.Geom) -> L.Geom:
 
 
 def gpu_power(g: npo.Geom, buf: np.ndarray, splits=None, host=False, register=False,
-              env=None) -> np.ndarray:
-    old = {}
-    for k, v in (env or {}).items():
-        old[k] = os.environ.get(k)
-        os.environ[k] = str(v)
-    try:
-        with paf_b2p.Integrator(to_b2p(g), device=0) as it:
-            bounds = [0] + list(splits or []) + [buf.size]
-            if host:
-                hb = np.ascontiguousarray(buf)
-                if register and hb.nbytes:
-                    it.register_host(hb)
-                for a, b in zip(bounds[:-1], bounds[1:]):
-                    it.push(hb[a:b])
-                if register and hb.nbytes:
-                    it.unregister_host(hb)
-            else:
-                d = it.upload(buf)
-                for a, b in zip(bounds[:-1], bounds[1:]):
-                    it.push((d, a, b - a))
-                out = it.finish(allow_partial=True)
-                d.free()
-                return out
-            return it.finish(allow_partial=True)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+              tuning=None) -> np.ndarray:
+    with paf_b2p.Integrator(to_b2p(g), device=0, tuning=tuning) as it:
+        bounds = [0] + list(splits or []) + [buf.size]
+        if host:
+            hb = np.ascontiguousarray(buf)
+            if register and hb.nbytes:
+                it.register_host(hb)
+            for a, b in zip(bounds[:-1], bounds[1:]):
+                it.push(hb[a:b])
+            if register and hb.nbytes:
+                it.unregister_host(hb)
+        else:
+            d = it.upload(buf)
+            for a, b in zip(bounds[:-1], bounds[1:]):
+                it.push((d, a, b - a))
+            out = it.finish(allow_partial=True)
+            d.free()
+            return out
+        return it.finish(allow_partial=True)
 
 
 def same_bits(a, b):
@@ -142,9 +133,9 @@ def test_extreme_int8_long_lane_runs(gpu):
     # 65536 rows: exercises the 32768-row widening and uint32 wrap (2^32/lane)
     g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 20, npol_out=2)
     buf = np.full(g.block_bytes, 0x80, dtype=np.uint8)
-    out = gpu_power(g, buf, env={"B2P_ROW_GROUPS": 1})
+    out = gpu_power(g, buf, tuning={"row_groups": 1})
     assert np.all(out == np.float32((1 << 20) * 2 * 16384))
-    out1 = gpu_power(npo.Geom(**{**g.asdict(), "npol_out": 1}), buf, env={"B2P_ROW_GROUPS": 2})
+    out1 = gpu_power(npo.Geom(**{**g.asdict(), "npol_out": 1}), buf, tuning={"row_groups": 2})
     assert np.all(out1 == np.float32((1 << 20) * 4 * 16384))
 
 
@@ -314,19 +305,15 @@ def test_integrate_fused_equals_push_finish(gpu, name, npol_out, mean):
     g = npo.Geom(**{**GEOMS[name].asdict(), "npol_out": npol_out, "mean": mean})
     bufs = [npo.fill_synthetic(g, g.block_bytes, SEED, 2, k) for k in range(3)]
     for inter in (0, 1):
-        os.environ["B2P_INTERLEAVE"] = str(inter)
-        try:
-            with paf_b2p.Integrator(to_b2p(g)) as it:
-                for b in bufs:
-                    d = it.upload(b)
-                    fused = it.integrate(d)
-                    it.push(d)
-                    pf = it.finish()
-                    d.free()
-                    assert same_bits(fused, pf)
-                    assert same_bits(fused, npo.power(g, b))
-        finally:
-            os.environ.pop("B2P_INTERLEAVE", None)
+        with paf_b2p.Integrator(to_b2p(g), tuning={"interleave": inter}) as it:
+            for b in bufs:
+                d = it.upload(b)
+                fused = it.integrate(d)
+                it.push(d)
+                pf = it.finish()
+                d.free()
+                assert same_bits(fused, pf)
+                assert same_bits(fused, npo.power(g, b))
 
 
 def test_integrate_host_span_and_errors(gpu):
@@ -379,7 +366,7 @@ def test_timing_modes(gpu):
             it.integrate(d, None)
         it.set_timing(0)
         s2 = it.stats()
-        assert s2["launches"] == 4 and s2["finalizes"] in (0, 4)  # fused or not (B2P_FUSE)
+        assert s2["launches"] == 4 and s2["finalizes"] in (0, 4)  # fused or not (tuning.fuse)
         assert s2["kernel_ms"] / 4 > 0.5 * per
         d.free()
 
@@ -402,73 +389,55 @@ def test_integrate_device_span_is_one_launch(gpu):
 def test_back_to_back_async_integrations(gpu, fuse):
     # 7 integrations enqueued without a host sync: the two replica sets
     # alternate and every finalize overlaps the next integrate (or runs in
-    # the last workgroup with B2P_FUSE=1); each spectrum must be exact
+    # the last workgroup with tuning fuse=1); each spectrum must be exact
     g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 16)
-    os.environ["B2P_FUSE"] = str(fuse)
-    try:
-        with paf_b2p.Integrator(to_b2p(g)) as it:
-            blocks = []
-            for k in range(3):
-                d = it.alloc(g.block_bytes)
-                it.fill_synthetic(d, SEED, 9, k)
-                blocks.append(d)
-            out = it.alloc(7 * g.nout * 4)
-            for k in range(7):
-                it.integrate(blocks[k % 3], out.ptr + k * g.nout * 4, True)
-            it.sync()
-            got = it.download(out).view(np.float32).reshape(7, g.nout).copy()
-            # the push / finish_async form, also unsynchronised
-            for k in range(7):
-                it.push(blocks[k % 3])
-                it.finish_async(out.ptr + k * g.nout * 4, True)
-            it.sync()
-            got2 = it.download(out).view(np.float32).reshape(7, g.nout)
-            assert same_bits(got, got2)
-            hosts = [it.download(b) for b in blocks]
-            for b in blocks:
-                b.free()
-            out.free()
-    finally:
-        os.environ.pop("B2P_FUSE", None)
+    with paf_b2p.Integrator(to_b2p(g), tuning={"fuse": fuse}) as it:
+        blocks = []
+        for k in range(3):
+            d = it.alloc(g.block_bytes)
+            it.fill_synthetic(d, SEED, 9, k)
+            blocks.append(d)
+        out = it.alloc(7 * g.nout * 4)
+        for k in range(7):
+            it.integrate(blocks[k % 3], out.ptr + k * g.nout * 4, True)
+        it.sync()
+        got = it.download(out).view(np.float32).reshape(7, g.nout).copy()
+        # the push / finish_async form, also unsynchronised
+        for k in range(7):
+            it.push(blocks[k % 3])
+            it.finish_async(out.ptr + k * g.nout * 4, True)
+        it.sync()
+        got2 = it.download(out).view(np.float32).reshape(7, g.nout)
+        assert same_bits(got, got2)
+        hosts = [it.download(b) for b in blocks]
+        for b in blocks:
+            b.free()
+        out.free()
     for k in range(7):
         assert same_bits(got[k], co.power(g, hosts[k % 3])), k
 
 
-def test_push_failure_part_way_marks_context_failed(gpu, monkeypatch):
+def test_push_failure_part_way_marks_context_failed(gpu):
     """A host-span push that fails after its first staging chunk was summed
     leaves the integration unknown: the call reports the failure and every
     later call on the context returns B2P_EFAILED until b2p_close (the
     reference would have exit(-1)ed, cudautil.cuh:29-41).  The failure is
-    injected at staging chunk 2 of a 4-chunk span."""
-    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=4096)      # 4 MiB per integration
-    buf = co.fill_synthetic(g, g.block_bytes, SEED, 0, 0)
-    monkeypatch.setenv("B2P_STAGE_MIB", "1")
-    monkeypatch.setenv("B2P_INJECT_PUSH_FAIL", "2")
-    it = paf_b2p.Integrator(to_b2p(g))
-    with pytest.raises(paf_b2p.B2PError) as e:
-        it.push(buf)
-    assert e.value.code == L.B2P_EHIP and "injected" in str(e.value)
-    for call in (lambda: it.push(buf), lambda: it.finish(allow_partial=True), it.sync,
-                 lambda: it.set_timing(2), it.fence):
-        with pytest.raises(paf_b2p.B2PError) as e:
-            call()
-        assert e.value.code == L.B2P_EFAILED
-    assert "injected" in L.lib().b2p_last_error(it._ctx).decode()   # the first failure's text
-    it.close()
-    monkeypatch.delenv("B2P_INJECT_PUSH_FAIL")
-    with paf_b2p.Integrator(to_b2p(g)) as it2:                     # a fresh context is fine
-        it2.push(buf)
-        assert same_bits(it2.finish(), co.power(g, buf))
+    injected at staging chunk 2 of a 4-chunk span by the TEST build of the
+    library (lib/hooks/libpafb2p.so, -DB2P_TEST_HOOKS), loaded in a child
+    process; the release library has no injection entry at all."""
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tests", "hooks_push_fail.py")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "push-fail hook: ok" in r.stdout
 
 
-def test_fused_host_output_after_finish_async_host(gpu, monkeypatch):
-    """B2P_FUSE=1: a fused integrate whose spectrum goes to the host follows
+def test_fused_host_output_after_finish_async_host(gpu):
+    """tuning fuse=1: a fused integrate whose spectrum goes to the host follows
     a finish_async to the host; the carried finalize of the first and the
     fused finalize of the second must not share the staging output"""
-    monkeypatch.setenv("B2P_FUSE", "1")
     g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=8192)
     bufs = [co.fill_synthetic(g, g.block_bytes, SEED, 5, k) for k in range(3)]
-    with paf_b2p.Integrator(to_b2p(g)) as it:
+    with paf_b2p.Integrator(to_b2p(g), tuning={"fuse": 1}) as it:
         ds = [it.upload(b) for b in bufs]
         outs = [np.zeros(g.nout, np.float32) for _ in range(3)]
         it.push(ds[0])

@@ -54,10 +54,11 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--order", choices=("both", "tm", "shuffled"), default="both")
+    ap.add_argument("--grid", type=int, default=0, help="workgroup cap (b2p_tuning_t.assemble_grid)")
     a = ap.parse_args()
     nchunk = 48
     geom = paf_b2p.bmf_geom(nsamp_int=a.ndf * 128)
-    it = paf_b2p.Integrator(geom)
+    it = paf_b2p.Integrator(geom, tuning={"assemble_grid": a.grid} if a.grid else None)
     bb = it.block_bytes
     n = a.ndf * nchunk
     d_blk = it.alloc(bb)
@@ -123,8 +124,7 @@ def main():
             # channels x pols x time, as bench.py counts samples
             "stream_to_spectrum_Msamples_s": round(a.ndf * 128 * it.nout * 2 / both_s / 1e6, 1),
             "host_stream_build_s": round(prep, 1),
-            "variant": os.environ.get("B2P_ASM_VARIANT", "0"),
-            "grid": os.environ.get("B2P_ASM_GRID", "default"),
+            "grid": a.grid or "default",
         }), flush=True)
         d_dfs.free()
         d_chk.free()

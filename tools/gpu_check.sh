@@ -64,10 +64,10 @@ for s in $STEPS; do
     asm) run bench_assemble 600 python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
     profasm) run prof_asm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
-    asmsweep) for v in 0 1 4 5; do for g in 4096 8192 16384; do
-                run asm_v${v}_g${g} 300 env B2P_ASM_VARIANT=$v B2P_ASM_GRID=$g python3 tools/bench_assemble.py \
+    asmsweep) for g in 4096 8192 16384; do
+                run asm_g${g} 300 python3 tools/bench_assemble.py --grid $g \
                   --steps 10 --warmup 2 --order tm || exit $?
-              done; done ;;
+              done ;;
     ring) run bench_ring 600 python3 tools/bench_ring.py --blocks 200 &&
           run bench_ring_sync 600 env B2P_NO_PIPELINE=1 python3 tools/bench_ring.py --blocks 200 &&
           run bench_ring_host 600 python3 tools/bench_ring.py --blocks 20 --host ;;
@@ -84,11 +84,11 @@ for s in $STEPS; do
              run free_rep 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
              run keep_rep_b 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 --keep ;;
     knobs) i=0
-           for kv in "B2P_UNROLL=8" "B2P_UNROLL=16" "B2P_MAX_THREADS=448" "B2P_MAX_THREADS=256" \
-                     "B2P_INTERLEAVE=1" "B2P_INTERLEAVE=0" "B2P_WG_PER_CU=2" "B2P_NT=0"; do
+           for kv in '{"unroll":8}' '{"unroll":16}' '{"max_threads":448}' '{"max_threads":256}' \
+                     '{"interleave":1}' '{"interleave":0}' '{"wg_per_cu":2}' '{"nontemporal":0}'; do
              i=$((i+1))
-             run knob_$i 300 env $kv python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 2 &&
-             run knob16_$i 300 env $kv python3 tools/perf_matrix.py --steps 20 --only "int16 LE 256ch" --npol-out 1 || exit $?
+             run knob_$i 300 python3 tools/perf_matrix.py --tuning "$kv" --steps 20 --only "int8 256ch" --npol-out 2 &&
+             run knob16_$i 300 python3 tools/perf_matrix.py --tuning "$kv" --steps 20 --only "int16 LE 256ch" --npol-out 1 || exit $?
            done ;;
     spikes) run overlap_dist 300 paf-baseband2power_amd/bin/overlap_probe 200 dist &&
             run prof_spikes 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_spikes" -o run \

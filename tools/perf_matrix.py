@@ -37,8 +37,8 @@ CASES = [
 KEEP = []  # --keep: buffers are never freed (diagnostic: no hipFree between runs)
 
 
-def run(name, geom, steps, keep=False):
-    it = paf_b2p.Integrator(geom)
+def run(name, geom, steps, keep=False, tuning=None):
+    it = paf_b2p.Integrator(geom, tuning=tuning)
     bb = it.block_bytes
     blocks = []
     for b in range(2):
@@ -79,8 +79,9 @@ def main():
                     help="idle seconds before each run: the previous run freed GiBs, and launches "
                          "in the next seconds run 2-8 %% slower (profiles/r01_free_effect.txt)")
     ap.add_argument("--keep", action="store_true", help="never free a run's buffers")
+    ap.add_argument("--tuning", default="", help='b2p_tuning_t fields as JSON, e.g. \'{"unroll": 8}\'')
     a = ap.parse_args()
-    knobs = {k: v for k, v in os.environ.items() if k.startswith("B2P_")}
+    knobs = json.loads(a.tuning) if a.tuning else None
     for name, mk in CASES:
         if a.only and a.only not in name:
             continue
@@ -88,9 +89,9 @@ def main():
             for rep in range(a.repeat):
                 if a.sleep > 0:
                     time.sleep(a.sleep)
-                r = run(name, mk(npol_out=npo), a.steps, a.keep)
+                r = run(name, mk(npol_out=npo), a.steps, a.keep, knobs)
                 if knobs:
-                    r["env"] = knobs
+                    r["tuning"] = knobs
                 if a.repeat > 1:
                     r["rep"] = rep
                 print(json.dumps(r), flush=True)

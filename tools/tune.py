@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Launch-shape sweep for the integrate kernel, interleaved in ONE process
 (cdna_hip_programming.md §5.4 rule 24): every variant is opened as its own
-context (the knobs are read at b2p_open) and timed with dispatch-packet
+context (an explicit b2p_tuning_t through b2p_open_tuned) and timed with dispatch-packet
 events over the same rotating HBM blocks, round after round.
 
     python3 tools/tune.py --config c2 --rounds 3 > gpurun_out/tune_c2.json
@@ -21,37 +21,27 @@ sys.path.insert(0, os.path.join(REPO, "paf-baseband2power_amd"))
 import paf_b2p  # noqa: E402
 from paf_b2p.geometry import CONFIGS  # noqa: E402
 
-KNOBS = ("B2P_MAX_THREADS", "B2P_UNROLL", "B2P_NT", "B2P_WG_PER_CU", "B2P_INTERLEAVE", "FUSE",
-         "B2P_THREADS")
-
-
 def frame_variants(threads):
     """multi-column frames (BMF): exact workgroup sizes"""
     for t, u, il in itertools.product(threads, [4, 8, 16], [0, 1]):
-        yield {"B2P_MAX_THREADS": 1024, "B2P_THREADS": t, "B2P_UNROLL": u, "B2P_NT": 1,
-               "B2P_WG_PER_CU": None, "B2P_INTERLEAVE": il, "FUSE": 0}
+        yield {"max_threads": 1024, "threads": t, "unroll": u, "nontemporal": 1,
+               "wg_per_cu": 0, "interleave": il, "fuse": 0}
 
 
 def variants(quick: bool):
     threads = [256, 512, 1024]
     unroll = [4, 8, 16]
-    per_cu = [None, 1, 2, 4]
+    per_cu = [0, 1, 2, 4]  # 0: the planner's default
     for t, u, p, il, fu in itertools.product(threads, unroll, per_cu, [0, 1], [0, 1]):
-        if quick and (p not in (None, 1) or u == 16):
+        if quick and (p not in (0, 1) or u == 16):
             continue
-        yield {"B2P_MAX_THREADS": t, "B2P_UNROLL": u, "B2P_NT": 1, "B2P_WG_PER_CU": p,
-               "B2P_INTERLEAVE": il, "FUSE": fu}
+        yield {"max_threads": t, "unroll": u, "nontemporal": 1, "wg_per_cu": p,
+               "interleave": il, "fuse": fu}
 
 
 def open_variant(geom, v):
-    for k in KNOBS:
-        os.environ.pop(k, None)
-        if v.get(k) is not None and k.startswith("B2P_"):
-            os.environ[k] = str(v[k])
-    it = paf_b2p.Integrator(geom)
-    for k in KNOBS:
-        os.environ.pop(k, None)
-    return it
+    """one context per variant, its b2p_tuning_t passed explicitly"""
+    return paf_b2p.Integrator(geom, tuning=v)
 
 
 def main():
@@ -60,7 +50,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--launches", type=int, default=12)
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--threads", default="", help="comma list of exact B2P_THREADS (BMF)")
+    ap.add_argument("--threads", default="", help="comma list of exact workgroup sizes (b2p_tuning_t.threads, BMF)")
     a = ap.parse_args()
     geom = CONFIGS[a.config]["geom"]()
     base = paf_b2p.Integrator(geom)
@@ -83,7 +73,7 @@ def main():
             dout = it.alloc(it.nout * 4)
 
             def one(k):
-                if v["FUSE"]:
+                if v["fuse"]:
                     it.integrate(blocks[k % 4], dout.ptr, True)
                 else:
                     it.push(blocks[k % 4])
