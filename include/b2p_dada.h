@@ -136,7 +136,7 @@ char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id);
 int ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes);
 /* NULL at end of data (writer signalled EOD and every block was read) */
 char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id);
-int ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes);
+ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes); /* PSRDADA's type */
 
 /* ---- dada_hdu: data ring at key + header ring at key+1 ---- */
 typedef struct dada_hdu {
@@ -181,7 +181,7 @@ int ascii_header_set(char *header, const char *keyword, const char *format, ...)
 int ascii_header_del(char *header, const char *keyword);
 
 /* read up to bufsz bytes of a file into buffer, NUL-terminated (futils) */
-int64_t fileread(const char *filename, char *buffer, unsigned bufsz);
+int fileread(const char *filename, char *buffer, unsigned bufsz); /* bytes read, -1 on error */
 
 #ifdef __cplusplus
 }

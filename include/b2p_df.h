@@ -33,6 +33,8 @@ extern "C" {
 #define B2P_DF_PERIOD_SEC 27         /* PRD_SEC,  capture.h:31 */
 #define B2P_DF_TSAMP_SEC 1.08E-4     /* TDF_SEC,  capture.h:30 */
 #define B2P_DF_NCHK_BMF 6            /* NCHK_BMF, capture.h:21 */
+#define B2P_DF_SECDAY 86400.0        /* SECDAY,   capture.h:43 */
+#define B2P_DF_TIMESTR "%Y-%m-%d-%H:%M:%S" /* DADA_TIMESTR, capture.h:15 */
 
 /* same members as hdr_t (hdr.h:6-14) */
 typedef struct b2p_df_hdr {
@@ -59,6 +61,24 @@ void b2p_df_ref_advance(b2p_df_hdr_t *ref, uint64_t ndf);
  * address, as stored in sockaddr_in.sin_addr.s_addr (network byte order):
  * (octet3 - 1) * NCHK_BMF + ceil(octet4 / 2) - 1 */
 int b2p_df_chunk_from_ip(uint32_t s_addr);
+
+/* ---- start time of a capture (acquire_start_time, capture.c:791-843) ----
+ * The epoch file maps a header epoch to a day number: lines "EPOCH DAYS
+ * [anything]", '#' lines skipped (capture.c:808-815).  Returns 0 and sets
+ * *days, -1 if the file cannot be opened (capture.c:798-805), -2 if no line
+ * names `epoch` (the reference then silently used the last line read; here
+ * that is an error). */
+int b2p_df_epoch_days(const char *epoch_file, int epoch, double *days);
+/* UTC_START and PICOSECONDS of the frame `start`, the same double
+ * arithmetic as capture.c:819-825:
+ *   sec_prd     = idf * TDF_SEC
+ *   t           = (time_t)(SECDAY * days + sec + floor(sec_prd))
+ *   utc_start   = strftime(DADA_TIMESTR, gmtime(t))
+ *   picoseconds = 1e6 * round(1e6 * (sec_prd - floor(sec_prd)))
+ * utc_start needs >= 20 bytes.  Returns 0, or -1 if the time does not
+ * convert. */
+int b2p_df_start_time(const b2p_df_hdr_t *start, double days, char *utc_start, size_t len,
+                      uint64_t *picoseconds);
 
 #ifdef __cplusplus
 }

@@ -461,7 +461,7 @@ char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id
   return p;
 }
 
-int ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes) {
+ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes) {
   (void)bytes;
   if (!ipc) return -1;
   ipc->curbuf = NULL;
@@ -626,12 +626,12 @@ int dada_db_destroy(key_t key) {
   return a == 0 && b == 0 ? 0 : -1;
 }
 
-int64_t fileread(const char *filename, char *buffer, unsigned bufsz) {
+int fileread(const char *filename, char *buffer, unsigned bufsz) {
   if (!filename || !buffer || !bufsz) return -1;
   FILE *fp = fopen(filename, "r");
   if (!fp) return -1;
   memset(buffer, 0, bufsz);
   size_t n = fread(buffer, 1, bufsz - 1, fp);
   fclose(fp);
-  return (int64_t)n;
+  return (int)n;
 }

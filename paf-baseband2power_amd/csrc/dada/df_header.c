@@ -2,11 +2,14 @@
  * df_header.c -- BMF data-frame header arithmetic (include/b2p_df.h).
  * Restates hdr.c:10-28 (decode), capture.c:562-584 (frame index, chunk from
  * IP) and sync.c:119-125 (reference advance); the encoder is new (the
- * reference only receives frames).  Decode is pinned by tests against the
+ * reference only receives frames); capture.c:791-843 (start time of a
+ * capture: UTC_START, PICOSECONDS).  Decode is pinned by tests against the
  * reference's own hdr.c (tests/golden/hdr_pin.npz).
  */
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include "b2p_df.h"
 
@@ -63,4 +66,34 @@ void b2p_df_ref_advance(b2p_df_hdr_t *ref, uint64_t ndf) {
 int b2p_df_chunk_from_ip(uint32_t s_addr) {
   const unsigned char *ip = (const unsigned char *)&s_addr;
   return (int)(ip[2] - 1) * B2P_DF_NCHK_BMF + (int)ceil((double)(ip[3] / 2.0)) - 1;
+}
+
+int b2p_df_epoch_days(const char *epoch_file, int epoch, double *days) {
+  FILE *fp = epoch_file ? fopen(epoch_file, "r") : NULL;
+  if (!fp) return -1; /* capture.c:798-805 */
+  char line[512];
+  int found = 0;
+  while (!found && fgets(line, sizeof line, fp)) {
+    if (line[0] == '#') continue; /* capture.c:810 */
+    int e;
+    double d;
+    if (sscanf(line, "%d %lf", &e, &d) == 2 && e == epoch) { /* capture.c:811-813 */
+      *days = d;
+      found = 1;
+    }
+  }
+  fclose(fp);
+  return found ? 0 : -2;
+}
+
+int b2p_df_start_time(const b2p_df_hdr_t *start, double days, char *utc_start, size_t len,
+                      uint64_t *picoseconds) {
+  if (!start || !utc_start || len < 20 || !picoseconds) return -1;
+  const double sec_prd = (double)start->idf * B2P_DF_TSAMP_SEC;                     /* :819 */
+  const time_t t = (time_t)(B2P_DF_SECDAY * days + (double)start->sec + floor(sec_prd)); /* :820 */
+  struct tm tm;
+  if (!gmtime_r(&t, &tm) || strftime(utc_start, len, B2P_DF_TIMESTR, &tm) == 0) return -1; /* :821 */
+  const double micro = 1.0E6 * (sec_prd - floor(sec_prd));                        /* :824 */
+  *picoseconds = (uint64_t)(1E6 * round(micro));                                  /* :825 */
+  return 0;
 }

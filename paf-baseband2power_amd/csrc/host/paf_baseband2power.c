@@ -141,7 +141,7 @@ static void install_stop_handlers(void) {
 static double now_s(void) {
   struct timespec t;
   clock_gettime(CLOCK_MONOTONIC, &t);
-  return t.tv_sec + t.tv_nsec * 1e-9;
+  return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
 }
 
 /* layout from -f, else from the input header, else BMF-native */
@@ -229,7 +229,7 @@ static int read_header(dada_hdu_t *h, char **hdr, uint64_t *size) {
   if (!*hdr) return -1;
   memcpy(*hdr, p, n < hsz ? n : hsz);
   *size = hsz;
-  return ipcbuf_mark_cleared(h->header_block);
+  return ipcbuf_mark_cleared(h->header_block) < 0 ? -1 : 0;
 }
 
 /* ring location of an input ring's blocks: -1 host, else the HIP device */
@@ -371,8 +371,9 @@ static void *worker(void *arg) {
         } else {
           const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s per sub-band, "
-                   "%.1f Msamples/s in all", sh->nblocks, dt * 1e3, bytes / dt / 1e9,
-                   (double)sh->nsub * (sh->nout / s->g.npol_out) * s->g.npol * s->g.nsamp_int / dt / 1e6);
+                   "%.1f Msamples/s in all", sh->nblocks, dt * 1e3, (double)bytes / dt / 1e9,
+                   (double)sh->nsub * (double)(sh->nout / s->g.npol_out) * s->g.npol *
+                       (double)s->g.nsamp_int / dt / 1e6);
         }
       }
     }
@@ -512,7 +513,7 @@ static void *worker_split(void *arg) {
         } else {
           const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s over %d GPUs",
-                   sh->nblocks, dt * 1e3, sh->blk_bytes / dt / 1e9, sh->nsub);
+                   sh->nblocks, dt * 1e3, (double)sh->blk_bytes / dt / 1e9, sh->nsub);
         }
       }
     }
@@ -753,9 +754,9 @@ int main(int argc, char *argv[]) {
     ascii_header_set(ohdr, "NBIT", "%d", 32);
     ascii_header_set(ohdr, "NDIM", "%d", 1);
     ascii_header_set(ohdr, "NPOL", "%u", sub[0].g.npol_out);
-    ascii_header_set(ohdr, "NCHAN", "%u", conf.nsub * info.nchan);
+    ascii_header_set(ohdr, "NCHAN", "%u", (uint32_t)conf.nsub * info.nchan);
     ascii_header_set(ohdr, "TSAMP", "%.6f", tsamp_out);
-    ascii_header_set(ohdr, "BYTES_PER_SECOND", "%.6f", sh.obytes / (tsamp_out * 1e-6));
+    ascii_header_set(ohdr, "BYTES_PER_SECOND", "%.6f", (double)sh.obytes / (tsamp_out * 1e-6));
     ascii_header_set(ohdr, "NSAMP_INT", "%" PRIu64, nsamp_out);
     ascii_header_set(ohdr, "POWER_MODE", "%s", sub[0].g.mean ? "MEAN" : "SUM");
     if (conf.nsub > 1) ascii_header_set(ohdr, "NSUBBAND", "%d", conf.nsub);

@@ -16,9 +16,9 @@
  * b2p_assemble into the current block of a dada_db -g ring.  When the block
  * switches, the spill is sorted again against the new reference.
  *
- *   paf_capture -a key -f header_file [-c rbuf_ndf] [-j seconds | -n blocks]
- *               [-I ip] [-P 17100] [-N 6] [-m ip | -m freq:F0]
- *               [-x ref_idf -s ref_sec] [-t idle_s] [-k dir] [-Z]
+ *   paf_capture -a key -f header_file [-g epoch_file] [-i freq] [-c rbuf_ndf]
+ *               [-j seconds | -n blocks] [-I ip] [-P 17100] [-N 6]
+ *               [-m ip | -m freq:F0] [-x ref_idf -s ref_sec] [-t idle_s] [-k dir] [-Z]
  *   paf_capture -o frames.df -O chunks.u8 ...      (no GPU: record what arrives)
  *
  * Chunk of a frame: -m ip (default) derives it from the sender address as
@@ -27,6 +27,13 @@
  * the first frame received unless -x/-s give it.  A block is closed once a
  * frame arrives TBUF_NDF (256, capture.h:35) frames past its end, or when
  * the stream goes idle.
+ *
+ * Header: written when the first data frame arrives, as the reference does
+ * (capture.c:300-312): the template (-f), then UTC_START and PICOSECONDS of
+ * the first block's reference frame from the epoch file (-g; restated
+ * acquire_start_time, capture.c:791-843, b2p_df_start_time) and FREQ from
+ * -i (register_header, capture.c:727-789).  An epoch file that cannot be
+ * read, or does not list the frames' epoch, stops the capture.
  */
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
@@ -89,7 +96,54 @@ typedef struct cap_t {
   int have_ref;
   int64_t max_rel;  /* furthest frame seen, relative to ref */
   multilog_t *log;
+  /* ring header, written at the first data frame (capture.c:300-312) */
+  const char *hfile, *efile;
+  double freq;
+  int have_freq, hdr_done;
 } cap_t;
+
+/* template + UTC_START / PICOSECONDS of the start frame + FREQ
+ * (register_header, capture.c:727-789; acquire_start_time, :791-843) */
+static int write_header(cap_t *c, const b2p_df_hdr_t *start) {
+  char utc[64] = "";
+  uint64_t ps = 0;
+  if (c->efile) {
+    double days = 0;
+    const int e = b2p_df_epoch_days(c->efile, start->epoch, &days);
+    if (e == -1) {
+      multilog(c->log, LOG_ERR, "cannot open epoch file %s (capture.c:798-805)", c->efile);
+      return -1;
+    }
+    if (e == -2) {
+      multilog(c->log, LOG_ERR, "epoch %d is not in epoch file %s", start->epoch, c->efile);
+      return -1;
+    }
+    if (b2p_df_start_time(start, days, utc, sizeof utc, &ps) != 0) {
+      multilog(c->log, LOG_ERR, "start time of idf %" PRIu64 " sec %" PRIu64 " does not convert",
+               start->idf, start->sec);
+      return -1;
+    }
+    multilog(c->log, LOG_INFO, "SEC_START %" PRIu64 ", IDF_START %" PRIu64 ", epoch %d: UTC_START %s, "
+             "PICOSECONDS %" PRIu64, start->sec, start->idf, start->epoch, utc, ps);
+  } else {
+    multilog(c->log, LOG_WARNING, "no epoch file (-g): UTC_START and PICOSECONDS stay as in %s",
+             c->hfile);
+  }
+  char *hb = ipcbuf_get_next_write(c->hdu->header_block);
+  if (!hb || fileread(c->hfile, hb, DADA_DEFAULT_HEADER_SIZE) < 0) {
+    multilog(c->log, LOG_ERR, "cannot pass header %s", c->hfile);
+    return -1;
+  }
+  if ((c->efile && (ascii_header_set(hb, "UTC_START", "%s", utc) < 0 ||
+                    ascii_header_set(hb, "PICOSECONDS", "%" PRIu64, ps) < 0)) ||
+      (c->have_freq && ascii_header_set(hb, "FREQ", "%.1lf", c->freq) < 0)) {
+    multilog(c->log, LOG_ERR, "cannot set UTC_START / PICOSECONDS / FREQ in the header");
+    return -1;
+  }
+  if (ipcbuf_mark_filled(c->hdu->header_block, DADA_DEFAULT_HEADER_SIZE) < 0) return -1;
+  c->hdr_done = 1;
+  return 0;
+}
 
 /* upload the batch and scatter it into the current block */
 static int flush_batch(cap_t *c) {
@@ -170,17 +224,24 @@ int main(int argc, char **argv) {
   key_t key = 0;
   int have_key = 0, port0 = 17100, nport = 6, arg, nozero = 0;
   const char *hfile = NULL, *ip = "0.0.0.0", *mapping = "ip", *ofile = NULL, *ocfile = NULL,
-             *logdir = NULL;
+             *logdir = NULL, *efile = NULL;
   uint64_t rbuf_ndf = 8192, nblocks = 0, ref_idf = 0, ref_sec = 0;
-  int have_ref = 0;
+  int have_ref = 0, have_freq = 0;
   double length = 0, idle_s = 2.0, freq = 0;
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:i:j:k:I:P:N:m:x:s:n:t:o:O:Zh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:g:i:j:k:I:P:N:m:x:s:n:t:o:O:Zh")) != -1) {
     switch (arg) {
       case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
       case 'b': case 'd': break; /* sod / record-header flags: accepted (paf_capture.c:75-85) */
       case 'c': rbuf_ndf = strtoull(optarg, NULL, 10); break;
       case 'f': hfile = optarg; break;
-      case 'i': freq = atof(optarg); break;
+      case 'g': efile = optarg; break;
+      case 'i':
+        if (sscanf(optarg, "%lf", &freq) != 1) {
+          fprintf(stderr, "paf_capture: -i takes the centre frequency in MHz, not %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        have_freq = 1;
+        break;
       case 'j': length = atof(optarg); break;
       case 'k': logdir = optarg; break;
       case 'I': ip = optarg; break;
@@ -196,8 +257,9 @@ int main(int argc, char **argv) {
       case 'Z': nozero = 1; break;
       default:
         fprintf(stdout,
-                "paf_capture -a key -f header [-c rbuf_ndf] [-j seconds | -n blocks] [-I ip] [-P port0]\n"
-                "            [-N nports] [-m ip|freq:F0] [-x ref_idf -s ref_sec] [-t idle_s] [-k dir] [-Z]\n"
+                "paf_capture -a key -f header [-g epoch_file] [-i freq] [-c rbuf_ndf] [-j seconds | -n blocks]\n"
+                "            [-I ip] [-P port0] [-N nports] [-m ip|freq:F0] [-x ref_idf -s ref_sec]\n"
+                "            [-t idle_s] [-k dir] [-Z]\n"
                 "paf_capture -o frames.df -O chunks.u8 [-I ip] [-P port0] [-N nports] [-m ...] [-t idle_s]\n");
         return EXIT_FAILURE;
     }
@@ -214,10 +276,32 @@ int main(int argc, char **argv) {
     fprintf(stderr, "paf_capture: -m ip or -m freq:F0\n");
     return EXIT_FAILURE;
   }
-  (void)freq;
+  if (!record) {
+    /* the header goes out with the first data frame, whose start time it
+     * carries (capture.c:300-312); the template and the epoch file are
+     * checked now, so a bad one fails before any ring or frame is touched */
+    FILE *th = fopen(hfile, "r");
+    if (!th) {
+      fprintf(stderr, "paf_capture: cannot open header template %s\n", hfile);
+      return EXIT_FAILURE;
+    }
+    fclose(th);
+    if (efile) {
+      FILE *te = fopen(efile, "r");
+      if (!te) {
+        fprintf(stderr, "paf_capture: cannot open epoch file %s (capture.c:798-805)\n", efile);
+        return EXIT_FAILURE;
+      }
+      fclose(te);
+    }
+  }
 
   cap_t c;
   memset(&c, 0, sizeof c);
+  c.hfile = hfile;
+  c.efile = efile;
+  c.freq = freq;
+  c.have_freq = have_freq;
   c.log = multilog_open("paf_capture", 0);
   {
     struct sigaction sa;
@@ -296,12 +380,6 @@ int main(int argc, char **argv) {
       goto done;
     if (b2p_dev_alloc(c.ctx, (void **)&c.d_cnt, (c.nchunk + 3) * sizeof(unsigned long long)) != B2P_OK)
       goto done;
-    char *hb = ipcbuf_get_next_write(c.hdu->header_block);
-    if (!hb || fileread(hfile, hb, DADA_DEFAULT_HEADER_SIZE) < 0 ||
-        ipcbuf_mark_filled(c.hdu->header_block, DADA_DEFAULT_HEADER_SIZE) < 0) {
-      multilog(c.log, LOG_ERR, "cannot pass header %s", hfile);
-      goto done;
-    }
   }
   /* host batch: one block's worth of frames at most (GPU mode), pinned */
   c.cap_frames = record ? 4096 : rbuf_ndf * (uint64_t)c.nchunk;
@@ -313,11 +391,10 @@ int main(int argc, char **argv) {
   c.sc = c.spill_cap ? malloc(c.spill_cap) : NULL;
   if (!c.hf || !c.hc || (c.spill_cap && (!c.sf || !c.sc))) goto done;
   if (c.ctx) b2p_register_host(c.ctx, c.hf, c.cap_frames * B2P_DF_BYTES);
-  if (have_ref) {
+  if (have_ref) { /* the first block opens with the first frame, after the header */
     c.ref.idf = ref_idf;
     c.ref.sec = ref_sec;
     c.have_ref = 1;
-    if (!record && open_block(&c) < 0) goto done;
   }
 
   {
@@ -374,11 +451,15 @@ int main(int argc, char **argv) {
               continue;
             }
             if (t_first == 0) t_first = now_s();
-            if (!c.have_ref) { /* the first frame fixes the reference (align_df role) */
-              c.ref = h;
-              c.have_ref = 1;
-              multilog(c.log, LOG_INFO, "reference: idf %" PRIu64 ", sec %" PRIu64, h.idf, h.sec);
-              if (open_block(&c) < 0) goto done;
+            if (!c.hdr_done) { /* the first frame: reference, start time, header, block 0 */
+              if (!c.have_ref) { /* the first frame fixes the reference (align_df role) */
+                c.ref = h;
+                c.have_ref = 1;
+              }
+              c.ref.epoch = h.epoch; /* -x/-s give idf and sec; the epoch is the stream's */
+              multilog(c.log, LOG_INFO, "reference: idf %" PRIu64 ", sec %" PRIu64 ", epoch %d", c.ref.idf,
+                       c.ref.sec, c.ref.epoch);
+              if (write_header(&c, &c.ref) < 0 || open_block(&c) < 0) goto done;
             }
             const int64_t rel = b2p_df_index(&h, &c.ref);
             /* far ahead of the current block: the reference quits the
@@ -460,6 +541,10 @@ int main(int argc, char **argv) {
   status = EXIT_SUCCESS;
 
 done:
+  if (locked && !c.hdr_done) { /* no frame ever came: readers still get a header, then EOD */
+    c.efile = NULL;
+    write_header(&c, &c.ref);
+  }
   if (locked) dada_hdu_unlock_write(c.hdu);
   if (c.hdu) dada_hdu_destroy(c.hdu);
   if (c.ctx) {

@@ -141,9 +141,9 @@ static int do_diskdb(conf_t *conf) {
   }
   free(stage);
   clock_gettime(CLOCK_MONOTONIC, &t1);
-  double el = (t1.tv_sec - t0.tv_sec) + (t1.tv_nsec - t0.tv_nsec) * 1e-9;
+  double el = (double)(t1.tv_sec - t0.tv_sec) + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-9;
   multilog(conf->log, LOG_INFO, "diskdb: %" PRIu64 " B in %" PRIu64 " blocks, %.3f s (%.2f GB/s)",
-           total, nblk, el, el > 0 ? total / el / 1e9 : 0.0);
+           total, nblk, el, el > 0 ? (double)total / el / 1e9 : 0.0);
   return EXIT_SUCCESS;
 }
 

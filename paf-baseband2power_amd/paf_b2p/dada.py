@@ -47,6 +47,7 @@ def dlib():
         L.ipcio_open_block_read.restype = P
         L.ipcio_open_block_read.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.ipcio_close_block_read.argtypes = [P, C.c_uint64]
+        L.ipcio_close_block_read.restype = C.c_ssize_t
         L.ipcbuf_get_next_write.restype = P
         L.ipcbuf_get_next_write.argtypes = [P]
         L.ipcbuf_mark_filled.argtypes = [P, C.c_uint64]
@@ -299,6 +300,11 @@ def _df_lib():
         L.b2p_df_ref_advance.restype = None
         L.b2p_df_chunk_from_ip.argtypes = [C.c_uint32]
         L.b2p_df_chunk_from_ip.restype = C.c_int
+        L.b2p_df_epoch_days.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double)]
+        L.b2p_df_epoch_days.restype = C.c_int
+        L.b2p_df_start_time.argtypes = [C.POINTER(DfHdr), C.c_double, C.c_char_p, C.c_size_t,
+                                        C.POINTER(C.c_uint64)]
+        L.b2p_df_start_time.restype = C.c_int
         L._df_ready = True
     return L
 
@@ -332,3 +338,27 @@ def df_chunk_from_ip(a: int, b: int, c: int, d: int) -> int:
     """chunk of the sender a.b.c.d (sin_addr.s_addr as stored, network order)"""
     s_addr = a | (b << 8) | (c << 16) | (d << 24)  # bytes in memory: a, b, c, d
     return int(_df_lib().b2p_df_chunk_from_ip(s_addr))
+
+
+def df_epoch_days(epoch_file: str, epoch: int) -> float:
+    """b2p_df_epoch_days: the day number the epoch file gives `epoch`
+    (capture.c:808-815); OSError if the file is missing, KeyError if the
+    epoch is not listed"""
+    d = C.c_double()
+    rc = _df_lib().b2p_df_epoch_days(epoch_file.encode(), epoch, C.byref(d))
+    if rc == -1:
+        raise OSError(f"cannot open epoch file {epoch_file}")
+    if rc == -2:
+        raise KeyError(f"epoch {epoch} not in {epoch_file}")
+    return d.value
+
+
+def df_start_time(idf: int, sec: int, days: float) -> tuple[str, int]:
+    """(UTC_START, PICOSECONDS) of a capture starting at frame (idf, sec)
+    (b2p_df_start_time, acquire_start_time capture.c:819-825)"""
+    h = DfHdr(1, idf, sec, 0, 0, 0.0)
+    buf = C.create_string_buffer(64)
+    ps = C.c_uint64()
+    if _df_lib().b2p_df_start_time(C.byref(h), days, buf, 64, C.byref(ps)) != 0:
+        raise ValueError("start time does not convert")
+    return buf.value.decode(), int(ps.value)

@@ -2,5 +2,5 @@
 #ifndef __FUTILS_H
 #define __FUTILS_H
 #include <stdint.h>
-int64_t fileread(const char *filename, char *buffer, unsigned bufsz);
+int fileread(const char *filename, char *buffer, unsigned bufsz);
 #endif

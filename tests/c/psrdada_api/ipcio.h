@@ -2,6 +2,7 @@
  * (152 B): the ipcbuf_t comes first, so (ipcbuf_t *)ipcio is valid. */
 #ifndef __DADA_IPCIO_H
 #define __DADA_IPCIO_H
+#include <sys/types.h>
 #include "ipcbuf.h"
 typedef struct {
   ipcbuf_t buf;
@@ -17,5 +18,5 @@ typedef struct {
 char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id);
 int ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes);
 char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id);
-int ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes);
+ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes);
 #endif

@@ -14,7 +14,7 @@ from paf_b2p import dada
 BIN = dada.BIN_DIR
 
 
-def make_stream(tmp_path, nchunk=4, nblk=3, block_ndf=32, window=48, seed=3):
+def make_stream(tmp_path, nchunk=4, nblk=3, block_ndf=32, window=48, seed=3, epoch=0):
     g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
                  nsamp_int=block_ndf * 128)
     payload = npo.fill_synthetic(g, g.block_bytes * nblk, 7, 0, 0)
@@ -23,7 +23,7 @@ def make_stream(tmp_path, nchunk=4, nblk=3, block_ndf=32, window=48, seed=3):
     df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
     subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(nchunk),
                     "-c", str(ck), "-x", "249990", "-s", "54", "-f", "1300", "-r", str(seed),
-                    "-w", str(window)], check=True, capture_output=True)
+                    "-w", str(window), "-e", str(epoch)], check=True, capture_output=True)
     return g, payload, df, ck
 
 
@@ -93,3 +93,22 @@ def test_capture_stops_cleanly_on_sigterm(tmp_path):
     assert time.time() - t0 < 5
     assert "stopped by a signal" in err and "capture: 3 frames received" in err
     assert os.path.getsize(out) == 3 * npo.DF_BYTES
+
+
+def test_capture_refuses_missing_epoch_file(tmp_path):
+    """-g names an epoch file that does not exist: the capture stops at once
+    (capture.c:798-805), before touching a ring or waiting for frames"""
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text("HDR_SIZE 4096\n")
+    r = subprocess.run([os.path.join(BIN, "paf_capture"), "-a", "7e00", "-f", str(hdr), "-g",
+                        str(tmp_path / "missing_epoch.txt"), "-i", "1340.5"],
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and "cannot open epoch file" in r.stderr
+
+
+def test_capture_refuses_bad_freq(tmp_path):
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text("HDR_SIZE 4096\n")
+    r = subprocess.run([os.path.join(BIN, "paf_capture"), "-a", "7e00", "-f", str(hdr), "-i", "abc"],
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and "-i takes" in r.stderr

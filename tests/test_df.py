@@ -168,3 +168,51 @@ def test_single_field_decoders_match_reference_hdr_c():
         h = dada.df_decode(raw.tobytes())
         p = raw.ctypes.data
         assert (L.hdr_idf(p), L.hdr_sec(p), L.hdr_freq(p)) == (h.idf, h.sec, h.freq)
+
+
+# ---- start time of a capture (acquire_start_time, capture.c:791-843) -------------
+EPOCHS = "# epoch  days-from-1970  date\n36 17532.0 2018-01-01\n37 17713.0 2018-07-01\n38 17897.0 2019-01-01\n"
+
+
+def py_start_time(idf, sec, days):
+    """independent restatement of capture.c:819-825 in Python floats (the
+    same IEEE doubles); C round() is half away from zero"""
+    import math
+    import time as _t
+    sec_prd = idf * 1.08e-4
+    t = int(86400.0 * days + float(sec) + math.floor(sec_prd))
+    utc = _t.strftime("%Y-%m-%d-%H:%M:%S", _t.gmtime(t))
+    micro = 1.0e6 * (sec_prd - math.floor(sec_prd))
+    return utc, int(1e6 * math.floor(micro + 0.5))
+
+
+@pytest.mark.parametrize("idf,sec,days,utc,ps", [
+    (0, 1000, 17713.0, "2018-07-01-00:16:40", 0),
+    (12345, 0, 17713.0, "2018-07-01-00:00:01", 333260000000),        # 1.33326 s into the period
+    (249999, 27, 17713.5, "2018-07-01-12:00:53", 999892000000),      # last frame of a period
+    (0, 0, 0.0, "1970-01-01-00:00:00", 0),
+    (1, 0, 17532.0, "2018-01-01-00:00:00", 108000000),               # one frame = 108 us
+])
+def test_start_time_known_answers(idf, sec, days, utc, ps):
+    assert dada.df_start_time(idf, sec, days) == (utc, ps)
+    assert py_start_time(idf, sec, days) == (utc, ps)
+
+
+def test_start_time_matches_restatement():
+    rng = np.random.default_rng(5)
+    for _ in range(2000):
+        idf = int(rng.integers(0, 250000))
+        sec = int(rng.integers(0, 1 << 30))
+        days = float(rng.integers(0, 40000)) + float(rng.choice([0.0, 0.25, 0.5]))
+        assert dada.df_start_time(idf, sec, days) == py_start_time(idf, sec, days), (idf, sec, days)
+
+
+def test_epoch_file_lookup(tmp_path):
+    f = tmp_path / "epoch.txt"
+    f.write_text(EPOCHS)
+    assert dada.df_epoch_days(str(f), 37) == 17713.0
+    assert dada.df_epoch_days(str(f), 36) == 17532.0
+    with pytest.raises(KeyError):              # the reference silently used the last line read
+        dada.df_epoch_days(str(f), 12)
+    with pytest.raises(OSError):               # capture.c:798-805
+        dada.df_epoch_days(str(tmp_path / "nope.txt"), 37)

@@ -41,11 +41,44 @@ def undefined(obj):
     return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
 
 
+# Return types Appendix A does not pin (INTEGRATION.md "PSRDADA API assumed"):
+# the alternative header set swaps each between int and a wider signed type.
+ALTERNATIVES = {
+    "ipcio.h": [("ssize_t ipcio_close_block_read(", "int ipcio_close_block_read("),
+                ("int ipcio_close_block_write(", "ssize_t ipcio_close_block_write(")],
+    "futils.h": [("int fileread(", "int64_t fileread(")],
+    "ipcbuf.h": [("int ipcbuf_mark_filled(", "ssize_t ipcbuf_mark_filled("),
+                 ("int ipcbuf_mark_cleared(", "ssize_t ipcbuf_mark_cleared("),
+                 ("int ipcbuf_eod(", "long ipcbuf_eod(")],
+    "dada_hdu.h": [("int dada_hdu_lock_read(", "long dada_hdu_lock_read("),
+                   ("int dada_hdu_unlock_write(", "long dada_hdu_unlock_write(")],
+}
+
+
+def api_dir(variant, tmp_path):
+    if variant == "published":
+        return API
+    d = tmp_path / "alt_api"
+    d.mkdir()
+    for name in os.listdir(API):
+        src = open(os.path.join(API, name)).read()
+        for a, b in ALTERNATIVES.get(name, []):
+            assert a in src, (name, a)
+            src = src.replace(a, b)
+        (d / name).write_text(src)
+    return str(d)
+
+
+@pytest.mark.parametrize("variant", ["published", "alternative"])
 @pytest.mark.parametrize("host", ["paf_baseband2power", "paf_diskdb"])
-def test_host_compiles_against_psrdada_subset(host, tmp_path):
+def test_host_compiles_against_psrdada_subset(host, variant, tmp_path):
+    """-Wconversion -Werror against the stand-ins and against the same API
+    with every uncertain return type swapped: the hosts depend on no
+    return type beyond "negative means failure"."""
     obj = tmp_path / f"{host}.o"
-    r = subprocess.run(["gcc", "-c", "-O2", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
-                        "-DB2P_PSRDADA", "-I", API, "-I", os.path.join(REPO, "include"),
+    r = subprocess.run(["gcc", "-c", "-O2", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra",
+                        "-Wconversion", "-Werror", "-DB2P_PSRDADA", "-I", api_dir(variant, tmp_path),
+                        "-I", os.path.join(REPO, "include"),
                         os.path.join(HOSTS, f"{host}.c"), "-o", str(obj)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
