@@ -544,6 +544,22 @@ def main(argv=None) -> int:
                      threads=vthreads)
     wd.disarm()
 
+    # cross-check, outside every timed region: the integrate kernel alone,
+    # timed by start/stop events on each launch's own dispatch packet (no
+    # inter-launch gap, no finalize) -- the quantity rocprofv3 --kernel-trace
+    # reports as the kernel's duration
+    calib_us = None
+    if not split and not host_mode and not a.no_fuse:
+        it.reset_stats()
+        it.set_timing(1)
+        for k in range(16):
+            it.integrate(blocks[k % len(blocks)], out_ptr, True)
+        it.set_timing(0)
+        it.sync()
+        cs = it.stats()
+        if cs["launches"]:
+            calib_us = cs["kernel_ms"] / cs["launches"] * 1e3
+
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
     achieved = bytes_per_launch / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
@@ -614,6 +630,11 @@ def main(argv=None) -> int:
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "avg_launch_us": round(kern_avg_s * 1e6, 2),
+                # per-launch dispatch-packet events over 16 launches after the
+                # timed regions: kernel duration only, as rocprofv3 counts it
+                "kernel_only_us": round(calib_us, 2) if calib_us else None,
+                "frac_kernel_only": (round(bytes_per_launch / (calib_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                                     if calib_us else None),
                 "launches_timed": int(st["launches"]),
                 "timing": "HIP events on the integrator stream bracketing each timed region's "
                           "launches (region / launches: gaps and finalizes included, an upper bound)",

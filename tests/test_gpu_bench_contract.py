@@ -31,6 +31,9 @@ def test_bench_prints_one_contract_line(gpu):
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # the kernel alone (per-launch packet events) is never slower than the
+    # region average it sits inside
+    assert rf["kernel_only_us"] > 0 and rf["frac_kernel_only"] >= rf["frac"] * 0.97
     assert rf["traffic"] is None or rf["traffic"] > 0
     cb = d["cpu_baseline"]
     assert cb["unit"] == d["unit"] and cb["kind"] == "port-tuned" and cb["cores"] >= 1
