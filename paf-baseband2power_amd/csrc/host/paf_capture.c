@@ -45,7 +45,9 @@
 #include <math.h>
 #include <netinet/in.h>
 #include <poll.h>
+#include <pthread.h>
 #include <signal.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -60,6 +62,7 @@
 #define MAXPORT 16
 #define RECV_BATCH 64
 #define TBUF_NDF 256 /* capture.h:35 */
+#define RX_SLOTS 32  /* batches in flight per receive thread */
 
 /* SIGINT / SIGTERM: stop receiving, deliver the block being filled and end
  * the ring's transfer cleanly (the reference's capture stopped on a quit
@@ -145,6 +148,90 @@ static int write_header(cap_t *c, const b2p_df_hdr_t *start) {
   return 0;
 }
 
+/* ---- receive threads ---------------------------------------------------
+ * One per port by default (the reference's capture threads, capture.c:
+ * 405-560): each drains its ports with recvmmsg into a ring of batch slots
+ * (single producer, single consumer) and never touches the ring block; the
+ * main thread takes the batches in order, sorts every frame by time and
+ * files it (so block switching stays on one thread, the role of sync.c's
+ * loop).  A full slot ring makes the thread wait: frames queue in the
+ * socket's 256 MiB receive buffer meanwhile. */
+typedef struct rx_slot {
+  int n;                         /* frames in the batch                    */
+  uint32_t len[RECV_BATCH];      /* datagram length (0: truncated)         */
+  uint32_t addr[RECV_BATCH];     /* sender, sin_addr.s_addr                */
+  int port[RECV_BATCH];          /* port index the frame arrived on        */
+  unsigned char *buf;            /* RECV_BATCH x 7232 B                    */
+} rx_slot_t;
+
+typedef struct rxq {
+  pthread_t th;
+  int started, joined, nport;
+  int port[MAXPORT], sock[MAXPORT];
+  rx_slot_t slot[RX_SLOTS];
+  _Atomic uint64_t head, tail; /* head: slots filled; tail: slots consumed */
+  atomic_int *stop;
+} rxq_t;
+
+typedef struct port_stat {
+  uint64_t frames;
+  uint64_t chunks[4]; /* chunk bytes seen on the port (bitmask) */
+} port_stat_t;
+
+static atomic_int rx_stop;
+
+static void *rx_main(void *arg) {
+  rxq_t *q = (rxq_t *)arg;
+  struct pollfd pfd[MAXPORT];
+  for (int i = 0; i < q->nport; i++) pfd[i] = (struct pollfd){q->sock[i], POLLIN, 0};
+  while (!atomic_load(q->stop)) {
+    const uint64_t head = atomic_load_explicit(&q->head, memory_order_relaxed);
+    if (head - atomic_load_explicit(&q->tail, memory_order_acquire) >= RX_SLOTS) {
+      usleep(20); /* the sorter is behind: the socket buffers hold the stream */
+      continue;
+    }
+    if (poll(pfd, (nfds_t)q->nport, 20) <= 0) continue;
+    for (int i = 0; i < q->nport; i++) {
+      if (!(pfd[i].revents & POLLIN)) continue;
+      const uint64_t h = atomic_load_explicit(&q->head, memory_order_relaxed);
+      if (h - atomic_load_explicit(&q->tail, memory_order_acquire) >= RX_SLOTS) break;
+      rx_slot_t *sl = &q->slot[h % RX_SLOTS];
+      struct mmsghdr msg[RECV_BATCH];
+      struct iovec iov[RECV_BATCH];
+      struct sockaddr_in from[RECV_BATCH];
+      for (unsigned k = 0; k < RECV_BATCH; k++) {
+        iov[k].iov_base = sl->buf + (size_t)k * B2P_DF_BYTES;
+        iov[k].iov_len = B2P_DF_BYTES;
+        memset(&msg[k], 0, sizeof msg[k]);
+        msg[k].msg_hdr.msg_iov = &iov[k];
+        msg[k].msg_hdr.msg_iovlen = 1;
+        msg[k].msg_hdr.msg_name = &from[k];
+        msg[k].msg_hdr.msg_namelen = sizeof from[k];
+      }
+      const int r = recvmmsg(q->sock[i], msg, RECV_BATCH, MSG_DONTWAIT, NULL);
+      if (r <= 0) continue;
+      for (int k = 0; k < r; k++) {
+        sl->len[k] = (msg[k].msg_hdr.msg_flags & MSG_TRUNC) ? 0 : msg[k].msg_len;
+        sl->addr[k] = (uint32_t)from[k].sin_addr.s_addr;
+        sl->port[k] = q->port[i];
+      }
+      sl->n = r;
+      atomic_store_explicit(&q->head, h + 1, memory_order_release);
+    }
+  }
+  return NULL;
+}
+
+/* stop every receive thread and join it (idempotent) */
+static void stop_rx(rxq_t *q, int n) {
+  atomic_store(&rx_stop, 1);
+  for (int t = 0; t < n; t++)
+    if (q[t].started && !q[t].joined) {
+      pthread_join(q[t].th, NULL);
+      q[t].joined = 1;
+    }
+}
+
 /* upload the batch and scatter it into the current block */
 static int flush_batch(cap_t *c) {
   if (!c->hn) return 0;
@@ -226,9 +313,9 @@ int main(int argc, char **argv) {
   const char *hfile = NULL, *ip = "0.0.0.0", *mapping = "ip", *ofile = NULL, *ocfile = NULL,
              *logdir = NULL, *efile = NULL;
   uint64_t rbuf_ndf = 8192, nblocks = 0, ref_idf = 0, ref_sec = 0;
-  int have_ref = 0, have_freq = 0;
+  int have_ref = 0, have_freq = 0, nrx_req = 0;
   double length = 0, idle_s = 2.0, freq = 0;
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:g:i:j:k:I:P:N:m:x:s:n:t:o:O:Zh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:g:i:j:k:I:P:N:R:m:x:s:n:t:o:O:Zh")) != -1) {
     switch (arg) {
       case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
       case 'b': case 'd': break; /* sod / record-header flags: accepted (paf_capture.c:75-85) */
@@ -247,6 +334,7 @@ int main(int argc, char **argv) {
       case 'I': ip = optarg; break;
       case 'P': port0 = atoi(optarg); break;
       case 'N': nport = atoi(optarg); break;
+      case 'R': nrx_req = atoi(optarg); break;
       case 'm': mapping = optarg; break;
       case 'x': ref_idf = strtoull(optarg, NULL, 10); have_ref = 1; break;
       case 's': ref_sec = strtoull(optarg, NULL, 10); have_ref = 1; break;
@@ -258,14 +346,15 @@ int main(int argc, char **argv) {
       default:
         fprintf(stdout,
                 "paf_capture -a key -f header [-g epoch_file] [-i freq] [-c rbuf_ndf] [-j seconds | -n blocks]\n"
-                "            [-I ip] [-P port0] [-N nports] [-m ip|freq:F0] [-x ref_idf -s ref_sec]\n"
+                "            [-I ip] [-P port0] [-N nports] [-R rx_threads] [-m ip|freq:F0] [-x ref_idf -s ref_sec]\n"
                 "            [-t idle_s] [-k dir] [-Z]\n"
                 "paf_capture -o frames.df -O chunks.u8 [-I ip] [-P port0] [-N nports] [-m ...] [-t idle_s]\n");
         return EXIT_FAILURE;
     }
   }
   const int record = ofile != NULL;
-  if ((!record && (!have_key || !hfile)) || (record && !ocfile) || nport < 1 || nport > MAXPORT) {
+  if ((!record && (!have_key || !hfile)) || (record && !ocfile) || nport < 1 || nport > MAXPORT ||
+      nrx_req < 0) {
     fprintf(stderr, "paf_capture: -a and -f (or -o and -O) are required, 1 <= -N <= %d\n", MAXPORT);
     return EXIT_FAILURE;
   }
@@ -322,6 +411,8 @@ int main(int argc, char **argv) {
   int socks[MAXPORT];
   for (int p = 0; p < nport; p++) socks[p] = -1;
   FILE *fo = NULL, *fco = NULL;
+  port_stat_t pstat[MAXPORT];
+  memset(pstat, 0, sizeof pstat);
 
   /* sockets: one per port (capture.c:146-176), large receive buffers */
   for (int p = 0; p < nport; p++) {
@@ -398,56 +489,61 @@ int main(int argc, char **argv) {
   }
 
   {
-    unsigned char *rx = malloc((size_t)RECV_BATCH * B2P_DF_BYTES);
-    if (!rx) goto done;
-    struct pollfd pfd[MAXPORT];
-    for (int p = 0; p < nport; p++) pfd[p] = (struct pollfd){socks[p], POLLIN, 0};
+    /* receive threads: port p is drained by thread p % nrx (the reference
+     * runs one capture thread per port, capture.c:405-560); each hands
+     * batches of raw frames to this thread, which sorts them by time */
+    int nrx = nrx_req > 0 ? nrx_req : nport, rx_failed = 0, rx_ok = 0;
+    if (nrx > nport) nrx = nport;
+    rxq_t *rxq = calloc((size_t)nrx, sizeof *rxq);
+    if (!rxq) goto done;
+    int rx_started = 0;
+    for (int t = 0; t < nrx; t++) {
+      rxq[t].stop = &rx_stop;
+      for (int p = t; p < nport; p += nrx) {
+        rxq[t].port[rxq[t].nport] = p;
+        rxq[t].sock[rxq[t].nport++] = socks[p];
+      }
+      for (int k = 0; k < RX_SLOTS && rxq[t].nport; k++)
+        if (!(rxq[t].slot[k].buf = malloc((size_t)RECV_BATCH * B2P_DF_BYTES))) goto rx_end;
+      if (pthread_create(&rxq[t].th, NULL, rx_main, &rxq[t]) != 0) goto rx_end;
+      rxq[t].started = 1;
+      rx_started++;
+    }
+    multilog(c.log, LOG_INFO, "%d receive thread(s) over %d port(s)", rx_started, nport);
+    {
     uint64_t got_all = 0, bad = 0;
     double last_rx = now_s(), t_first = 0;
     const double start_s = idle_s * 5 > 30 ? idle_s * 5 : 30; /* first frame within */
     int stop = 0, jumped = 0, stopped = 0;
     while (!stop) {
-      int pr = poll(pfd, (nfds_t)nport, 20);
-      if (pr < 0 && errno != EINTR) break;
       if (g_stop) {
         multilog(c.log, LOG_INFO, "stopped by a signal: delivering the current block");
         stopped = 1;
         break;
       }
       int any = 0;
-      for (int p = 0; p < nport && pr > 0; p++) {
-        if (!(pfd[p].revents & POLLIN)) continue;
-        for (;;) { /* drain this port in recvmmsg batches */
-          struct mmsghdr msg[RECV_BATCH];
-          struct iovec iov[RECV_BATCH];
-          struct sockaddr_in from[RECV_BATCH];
-          for (unsigned i = 0; i < RECV_BATCH; i++) {
-            iov[i].iov_base = rx + (size_t)i * B2P_DF_BYTES;
-            iov[i].iov_len = B2P_DF_BYTES;
-            memset(&msg[i], 0, sizeof msg[i]);
-            msg[i].msg_hdr.msg_iov = &iov[i];
-            msg[i].msg_hdr.msg_iovlen = 1;
-            msg[i].msg_hdr.msg_name = &from[i];
-            msg[i].msg_hdr.msg_namelen = sizeof from[i];
-          }
-          if (stop) break;
-          int r = recvmmsg(socks[p], msg, RECV_BATCH, MSG_DONTWAIT, NULL);
-          if (r <= 0) break;
+      for (int t = 0; t < nrx && !stop; t++) {
+        rxq_t *q = &rxq[t];
+        uint64_t tail = atomic_load_explicit(&q->tail, memory_order_relaxed);
+        while (!stop && tail < atomic_load_explicit(&q->head, memory_order_acquire)) {
+          rx_slot_t *sl = &q->slot[tail % RX_SLOTS];
           any = 1;
-          for (int i = 0; i < r; i++) {
-            if (msg[i].msg_len != B2P_DF_BYTES || (msg[i].msg_hdr.msg_flags & MSG_TRUNC)) { /* not a data frame */
+          for (int i = 0; i < sl->n; i++) {
+            if (sl->len[i] != B2P_DF_BYTES) { /* not a data frame (short, long or truncated) */
               bad++;
               continue;
             }
-            const unsigned char *df = rx + (size_t)i * B2P_DF_BYTES;
+            const unsigned char *df = sl->buf + (size_t)i * B2P_DF_BYTES;
             b2p_df_hdr_t h;
             b2p_df_decode(df, &h);
-            int chunk = by_freq ? (int)lround(h.freq - freq0)
-                                : b2p_df_chunk_from_ip((uint32_t)from[i].sin_addr.s_addr);
+            int chunk = by_freq ? (int)lround(h.freq - freq0) : b2p_df_chunk_from_ip(sl->addr[i]);
             const unsigned char ck = (unsigned char)(chunk < 0 || chunk > 255 ? 255 : chunk);
             got_all++;
+            port_stat_t *ps = &pstat[sl->port[i]];
+            ps->frames++;
+            ps->chunks[ck >> 6] |= 1ull << (ck & 63);
             if (record) {
-              if (fwrite(df, B2P_DF_BYTES, 1, fo) != 1 || fwrite(&ck, 1, 1, fco) != 1) goto done;
+              if (fwrite(df, B2P_DF_BYTES, 1, fo) != 1 || fwrite(&ck, 1, 1, fco) != 1) goto rx_fail;
               continue;
             }
             if (t_first == 0) t_first = now_s();
@@ -459,7 +555,7 @@ int main(int argc, char **argv) {
               c.ref.epoch = h.epoch; /* -x/-s give idf and sec; the epoch is the stream's */
               multilog(c.log, LOG_INFO, "reference: idf %" PRIu64 ", sec %" PRIu64 ", epoch %d", c.ref.idf,
                        c.ref.sec, c.ref.epoch);
-              if (write_header(&c, &c.ref) < 0 || open_block(&c) < 0) goto done;
+              if (write_header(&c, &c.ref) < 0 || open_block(&c) < 0) goto rx_fail;
             }
             const int64_t rel = b2p_df_index(&h, &c.ref);
             /* far ahead of the current block: the reference quits the
@@ -483,23 +579,26 @@ int main(int argc, char **argv) {
             }
             c.far_run = 0;
             if (rel > c.max_rel) c.max_rel = rel;
-            if (file_frame(&c, df, ck, rel) < 0) goto done;
+            if (file_frame(&c, df, ck, rel) < 0) goto rx_fail;
             /* forced switch as soon as a frame runs TBUF_NDF past the block
              * (capture.c:510-524), before the spill can overflow */
             while (c.blk && c.max_rel >= (int64_t)(c.block_ndf + TBUF_NDF)) {
-              if (close_block(&c) < 0) goto done;
+              if (close_block(&c) < 0) goto rx_fail;
               if (c.nblk_done >= c.nblk_max) {
                 stop = 1;
                 break;
               }
-              if (open_block(&c) < 0) goto done;
+              if (open_block(&c) < 0) goto rx_fail;
             }
             if (stop) break;
           }
+          atomic_store_explicit(&q->tail, ++tail, memory_order_release);
         }
       }
+      if (stop) break;
       const double t = now_s();
       if (any) last_rx = t;
+      else usleep(100);
       if (record) {
         if (got_all && t - last_rx > idle_s) stop = 1;
         continue;
@@ -507,36 +606,62 @@ int main(int argc, char **argv) {
       if (!got_all) { /* nothing yet: wait for the stream to start */
         if (t - last_rx > start_s) {
           multilog(c.log, LOG_ERR, "no data frame in %.1f s", start_s);
-          goto done;
+          goto rx_fail;
         }
         continue;
       }
       const int idle = t - last_rx > idle_s;
       if (c.hn == c.cap_frames || (c.hn && !any)) /* a full batch, or the sockets ran dry */
-        if (flush_batch(&c) < 0) goto done;
+        if (flush_batch(&c) < 0) goto rx_fail;
       /* the block is over once frames run TBUF_NDF past its end (the
        * reference's forced switch, capture.c:510-524) or the stream stops */
       while (c.blk && (c.max_rel >= (int64_t)(c.block_ndf + TBUF_NDF) || idle)) {
-        if (close_block(&c) < 0) goto done;
+        if (close_block(&c) < 0) goto rx_fail;
         if (c.nblk_done >= c.nblk_max || (idle && !c.sn)) {
           stop = 1;
           break;
         }
-        if (open_block(&c) < 0) goto done;
+        if (open_block(&c) < 0) goto rx_fail;
         if (idle) { /* drain what the spill still holds, then stop */
-          if (flush_batch(&c) < 0) goto done;
+          if (flush_batch(&c) < 0) goto rx_fail;
         }
       }
     }
-    free(rx);
+    if (0) {
+    rx_fail:
+      rx_failed = 1;
+    }
+    stop_rx(rxq, nrx);
+    if (rx_failed) goto rx_end;
     if ((jumped || stopped) && !record && c.blk && close_block(&c) < 0)
-      goto done; /* deliver what arrived */
+      goto rx_end; /* deliver what arrived */
     const double el = t_first > 0 ? last_rx - t_first : 0.0;
     multilog(c.log, LOG_INFO, "capture: %" PRIu64 " frames received (%" PRIu64 " not frames), %" PRIu64
              " blocks, %" PRIu64 " frames placed, %" PRIu64 " behind their block, %" PRIu64
              " past the spill, %" PRIu64 " far ahead, %.3f s from the first frame to the last", got_all,
              bad, c.nblk_done, c.placed_all, c.dropped_late, c.dropped_spill, c.dropped_far, record ? 0.0 : el);
-    if (jumped) goto done; /* EXIT_FAILURE: the stream left the capture window */
+    /* per-port table (capture.c:700-725): frames expected = chunks seen on
+     * the port x frames per chunk over the blocks delivered */
+    multilog(c.log, LOG_INFO, "port\tchunks\tframes\texpected\tloss");
+    for (int p = 0; p < nport; p++) {
+      int nck = 0;
+      for (int w = 0; w < 4; w++) nck += __builtin_popcountll(pstat[p].chunks[w]);
+      const uint64_t expect = record ? 0 : (uint64_t)nck * c.nblk_done * c.block_ndf;
+      if (expect)
+        multilog(c.log, LOG_INFO, "%d\t%d\t%" PRIu64 "\t%" PRIu64 "\t%.1E", port0 + p, nck, pstat[p].frames,
+                 expect, (double)((int64_t)expect - (int64_t)pstat[p].frames) / (double)expect);
+      else
+        multilog(c.log, LOG_INFO, "%d\t%d\t%" PRIu64 "\t-\t-", port0 + p, nck, pstat[p].frames);
+    }
+    if (jumped) goto rx_end; /* EXIT_FAILURE: the stream left the capture window */
+    rx_ok = 1;
+    }
+  rx_end:
+    stop_rx(rxq, nrx);
+    for (int t = 0; t < nrx; t++)
+      for (int k = 0; k < RX_SLOTS; k++) free(rxq[t].slot[k].buf);
+    free(rxq);
+    if (!rx_ok) goto done;
   }
   status = EXIT_SUCCESS;
 

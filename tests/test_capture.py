@@ -3,10 +3,12 @@ replays a paf_dfgen frame stream to several ports, paf_capture -o records
 what arrives (no GPU).  Every frame arrives once, unchanged, with the chunk
 the -m freq mapping gives."""
 import os
+import re
 import subprocess
 import time
 
 import numpy as np
+import pytest
 
 import b2p_oracle as npo
 from paf_b2p import dada
@@ -27,12 +29,17 @@ def make_stream(tmp_path, nchunk=4, nblk=3, block_ndf=32, window=48, seed=3, epo
     return g, payload, df, ck
 
 
-def test_capture_records_every_frame(tmp_path):
+@pytest.mark.parametrize("rx_threads", [0, 1, 2])
+def test_capture_records_every_frame(tmp_path, rx_threads):
+    """every frame arrives once and unchanged, with one receive thread per
+    port (default, as the reference's capture threads), one thread for all
+    ports, or two threads sharing three ports"""
     g, _, df, ck = make_stream(tmp_path)
-    port = 21000 + (os.getpid() % 500) * 8
+    port = 21000 + (os.getpid() % 500) * 8 + rx_threads * 3
     out, outc = tmp_path / "r.df", tmp_path / "r.chunks"
     cap = subprocess.Popen([os.path.join(BIN, "paf_capture"), "-o", str(out), "-O", str(outc),
-                            "-P", str(port), "-N", "3", "-m", "freq:1300", "-t", "1"],
+                            "-P", str(port), "-N", "3", "-m", "freq:1300", "-t", "1",
+                            "-R", str(rx_threads)],
                            stderr=subprocess.PIPE, text=True)
     time.sleep(0.5)
     snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck),
@@ -49,6 +56,15 @@ def test_capture_records_every_frame(tmp_path):
     key = lambda a, c: sorted(zip((r.tobytes() for r in a), c.tolist()))  # noqa: E731
     assert key(got, got_ck) == key(sent, sent_ck)
     assert f"capture: {sent.shape[0]} frames received (0 not frames)" in err
+    assert f"{rx_threads or 3} receive thread(s) over 3 port(s)" in err
+    # per-port table (capture.c:700-725): every port's frames are counted
+    rows = [ln for ln in err.splitlines() if "\t" in ln]
+    counts = {}
+    for ln in err.splitlines():
+        m = re.search(r"(\d+)\t(\d+)\t(\d+)\t-\t-$", ln)
+        if m:
+            counts[int(m.group(1))] = int(m.group(3))
+    assert sorted(counts) == [port, port + 1, port + 2] and sum(counts.values()) == sent.shape[0], rows
 
 
 def test_capture_flags_non_frames(tmp_path):

@@ -7,6 +7,11 @@ capture's own timing are printed (one JSON line per rate).  One BMF NIC
 carries 48 chunks x 7232 B every 108 us = 3.2 GB/s (capture.h:20,27,30).
 
   python tools/bench_capture.py [--ndf 1024] [--blocks 4] [--rates 800,1600,3200]
+                                [--rx-threads 1,6] [--send-threads 1]
+
+--rx-threads: paf_capture -R (receive threads; 0 = one per port, the
+reference's layout); --send-threads: paf_dfsend -T (one sender thread
+saturates near 5 GB/s on loopback).
 """
 from __future__ import annotations
 
@@ -31,6 +36,8 @@ def main():
     ap.add_argument("--ndf", type=int, default=1024)
     ap.add_argument("--blocks", type=int, default=4)
     ap.add_argument("--rates", default="800,1600,3200")
+    ap.add_argument("--rx-threads", default="0")
+    ap.add_argument("--send-threads", type=int, default=1)
     a = ap.parse_args()
     nchunk = 48
     d = tempfile.mkdtemp(prefix="bench_capture_")
@@ -49,7 +56,8 @@ def main():
     hdr = os.path.join(d, "hdr.txt")
     with open(hdr, "w") as f:
         f.write("HDR_SIZE 4096\nNBIT 16\n")
-    for i, rate in enumerate(int(r) for r in a.rates.split(",")):
+    runs = [(int(r), int(x)) for x in a.rx_threads.split(",") for r in a.rates.split(",")]
+    for i, (rate, rx) in enumerate(runs):
         kin, kout = 0x7e40 + 4 * i, 0x7e80 + 4 * i
         for k in (kin, kout):
             dada.destroy_ring(k)
@@ -65,11 +73,13 @@ def main():
                                       stderr=subprocess.PIPE, text=True),
                      subprocess.Popen([os.path.join(BIN, "paf_capture"), "-a", f"{kin:x}", "-f", hdr,
                                        "-c", str(a.ndf), "-n", str(a.blocks), "-P", str(port), "-N", "6",
-                                       "-m", "freq:1300", "-x", "0", "-s", "27", "-t", "1"],
+                                       "-m", "freq:1300", "-x", "0", "-s", "27", "-t", "1",
+                                       "-R", str(rx)],
                                       stderr=subprocess.PIPE, text=True)]
             time.sleep(3)
             snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", df, "-k", ck, "-P", str(port),
-                                  "-N", "6", "-r", str(rate)], capture_output=True, text=True)
+                                  "-N", "6", "-r", str(rate), "-T", str(a.send_threads)],
+                                 capture_output=True, text=True)
             errs = [p.communicate(timeout=300)[1] for p in procs[::-1]]
             cap = errs[0]
             m = re.search(r"capture: (\d+) frames received.*?(\d+) frames placed.*?([0-9.]+) s from the first frame",
@@ -79,13 +89,15 @@ def main():
             got, placed, el = (int(m.group(1)), int(m.group(2)), float(m.group(3))) if m else (0, 0, 0)
             print(json.dumps({"path": "UDP loopback -> paf_capture (GPU assembly) -> device ring -> "
                                       "paf_baseband2power", "rate_target_MBps": rate,
+                              "rx_threads": rx or 6, "send_threads": a.send_threads,
                               "sent_MBps": float(s.group(3)) if s else None, "frames_sent": sent,
                               "frames_received": got, "frames_placed": placed,
                               "loss_pct": round(100.0 * (sent - got) / sent, 3) if sent else None,
                               "capture_s": el,
                               "captured_GBps": round(got * 7232 / el / 1e9, 2) if el else None,
                               "rc": [p.returncode for p in procs],
-                              "capture_summary": cap.strip().splitlines()[-1][22:] if cap.strip() else ""}),
+                              "capture_summary": next((ln[22:] for ln in cap.splitlines()
+                                                       if "capture: " in ln), "")}),
                   flush=True)
         finally:
             for p in procs:

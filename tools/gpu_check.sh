@@ -5,7 +5,7 @@
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
-#          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf
+#          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf capturemt
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -97,6 +97,8 @@ for s in $STEPS; do
     patterns) run read_patterns 300 paf-baseband2power_amd/bin/read_pattern_probe 40 ;;
     diskdb) run bench_diskdb 600 python3 tools/bench_diskdb.py --nint 8 --threads 16 ;;
     capture) run bench_capture 600 python3 tools/bench_capture.py ;;
+    capturemt) run bench_capture_mt 900 python3 tools/bench_capture.py --rates 3200,4800,6400,8000 \
+                 --rx-threads 1,0 --send-threads 3 ;;
     probe) run hbm_probe 300 paf-baseband2power_amd/bin/hbm_probe 1024 ;;
     skew) run skew_probe 300 paf-baseband2power_amd/bin/skew_probe ;;
     overlap) run overlap_probe 300 paf-baseband2power_amd/bin/overlap_probe 40 ;;
