@@ -522,10 +522,13 @@ int main(int argc, char **argv) {
         break;
       }
       int any = 0;
+      /* one batch per thread per round: the ports advance together in time,
+       * so no port's frames fall behind a block another port has already
+       * closed (a full slot ring is 256 frame times of one port) */
       for (int t = 0; t < nrx && !stop; t++) {
         rxq_t *q = &rxq[t];
         uint64_t tail = atomic_load_explicit(&q->tail, memory_order_relaxed);
-        while (!stop && tail < atomic_load_explicit(&q->head, memory_order_acquire)) {
+        if (!stop && tail < atomic_load_explicit(&q->head, memory_order_acquire)) {
           rx_slot_t *sl = &q->slot[tail % RX_SLOTS];
           any = 1;
           for (int i = 0; i < sl->n; i++) {
