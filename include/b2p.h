@@ -223,6 +223,17 @@ int b2p_sync(b2p_ctx_t *ctx);
  * push/finish pair. */
 int b2p_integrate(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device, float *out,
                   int out_is_device);
+/* Several whole integrations in ONE kernel launch: bufs[b] (device, 16-B
+ * aligned, block_bytes each; b < nblk <= B2P_MAX_BLOCKS) is integration b,
+ * its spectrum out + b * nout (device, or host memory valid after
+ * b2p_sync()).  For a consumer that finds several ring blocks queued: the
+ * launch's fixed cost (dispatch ramp and tail, ~2 us) is paid once, not
+ * nblk times, which matters for short integrations (a 256 MiB block reads in
+ * ~40 us).  Same output bits as nblk b2p_integrate calls; the finalize is
+ * deferred as for b2p_finish_async.  Requires no pending push. */
+#define B2P_MAX_BLOCKS 8
+int b2p_integrate_n(b2p_ctx_t *ctx, const void *const *bufs, uint32_t nblk, float *out,
+                    int out_is_device);
 /* Number of samples pushed into the current integration. */
 uint64_t b2p_samples_pending(const b2p_ctx_t *ctx);
 

@@ -25,6 +25,8 @@ constexpr uint32_t kTimingRing = 4096;  // event pairs kept before a drain
 
 thread_local char g_err[256];  // errors before a context exists
 
+static_assert(B2P_MAX_BLOCKS == kMaxBlk, "b2p.h and the kernels agree on blocks per launch");
+
 struct EvPair {
   hipEvent_t a, b;
   uint64_t bytes;
@@ -57,11 +59,17 @@ struct b2p_ctx {
   int cur = 0;                   // replica set of the running integration
   struct {
     int valid;
-    int set;
+    unsigned long long *rep;     // its first replica set
+    uint32_t nblk;               // integrations (consecutive sets / outputs)
     float *dev_out;              // where the kernel writes the spectrum
     float *host_out;             // non-null: D2H copy after it
     int raw;                     // 1: exact uint64 sums instead of fp32
-  } pend = {0, 0, nullptr, nullptr, 0};
+  } pend = {0, nullptr, 1, nullptr, nullptr, 0};
+  // b2p_integrate_n: two banks of kMaxBlk replica sets (launch k sums into
+  // bank k&1 while it finalizes the other), allocated on first use
+  unsigned long long *d_mrep = nullptr;
+  float *d_mout = nullptr;  // host-output staging, kMaxBlk spectra
+  int mbank = 0;
   uint32_t interleave = 0;
   int fuse = 0;  // b2p_integrate: finalize in the last workgroup (1) or a
                  // separate launch (0, measured faster: DESIGN.md)
@@ -450,6 +458,8 @@ int b2p_close(b2p_ctx_t *c) {
   }
   if (c->d_rep) (void)hipFree(c->d_rep);
   if (c->d_out) (void)hipFree(c->d_out);
+  if (c->d_mrep) (void)hipFree(c->d_mrep);
+  if (c->d_mout) (void)hipFree(c->d_mout);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   for (auto e : c->fence_ev)
     if (e) (void)hipEventDestroy(e);
@@ -512,12 +522,13 @@ static hipEvent_t pool_event(b2p_ctx_t *c) {
 }
 
 static size_t pend_bytes(const b2p_ctx_t *c) {
-  return (size_t)c->nout * (c->pend.raw ? sizeof(unsigned long long) : sizeof(float));
+  return (size_t)c->pend.nblk * c->nout * (c->pend.raw ? sizeof(unsigned long long) : sizeof(float));
 }
 
 // Enqueue one integrate launch over a device span (frame-aligned).  With
 // fused_out set, the launch also emits the integration (last workgroup).
-static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out) {
+static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out,
+                        const void *const *blocks = nullptr, uint32_t nblk = 1) {
   IntegrateArgs a;
   a.data = (const uint4 *)dev;
   a.nvec = nbytes / 16;
@@ -533,6 +544,13 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   a.nrep = c->nrep;
   a.interleave = c->interleave;
   a.rep = c->d_rep + (size_t)c->cur * c->nrep * c->nout;
+  a.nblk = 1;
+  a.set_words = (uint64_t)c->nrep * c->nout;
+  if (blocks) {  // b2p_integrate_n: nblk whole integrations, this bank's sets
+    a.rep = c->d_mrep + (size_t)c->mbank * kMaxBlk * a.set_words;
+    a.nblk = nblk;
+    for (uint32_t b = 0; b < nblk; ++b) a.blk[b] = (const uint4 *)blocks[b];
+  }
   a.out = fused_out;
   a.ticket = c->d_ticket + c->cur;
   a.mean = c->g.mean;
@@ -543,17 +561,20 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   a.fin_rep = nullptr;
   a.fin_out = nullptr;
   a.fin_raw = 0;
+  a.fin_nblk = 0;
   const bool carry = c->pend.valid;
   if (carry) {
-    a.fin_rep = c->d_rep + (size_t)c->pend.set * c->nrep * c->nout;
+    a.fin_rep = c->pend.rep;
     a.fin_out = c->pend.dev_out;
     a.fin_raw = (uint32_t)c->pend.raw;
+    a.fin_nblk = c->pend.nblk;
     grid += 1;
   }
   EvPair p{nullptr, nullptr, nbytes, 0};
+  p.bytes = nbytes * a.nblk;
   if (c->timing == 2) {
     c->region_launches++;
-    c->region_bytes += nbytes;
+    c->region_bytes += nbytes * a.nblk;
   } else if (c->timing) {
     if (c->pending.size() >= kTimingRing) drain_timing(c);
     p.a = pool_event(c);
@@ -575,7 +596,8 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
 static int flush_pending(b2p_ctx_t *c) {
   if (!c->pend.valid) return B2P_OK;
   FinalizeArgs f;
-  f.rep = c->d_rep + (size_t)c->pend.set * c->nrep * c->nout;
+  f.rep = c->pend.rep;
+  f.nblk = c->pend.nblk;
   f.nrep = c->nrep;
   f.nout = c->nout;
   f.out = c->pend.dev_out;
@@ -696,7 +718,8 @@ static int finish_common(b2p_ctx_t *c, void *out, int out_is_device, int raw) {
   if (rc != B2P_OK) return rc;
   // defer: the next integrate launch (or b2p_sync) emits this integration
   c->pend.valid = 1;
-  c->pend.set = c->cur;
+  c->pend.rep = c->d_rep + (size_t)c->cur * c->nrep * c->nout;
+  c->pend.nblk = 1;
   c->pend.raw = raw;
   c->pend.dev_out = out_is_device ? (float *)out : c->d_out;
   c->pend.host_out = out_is_device ? nullptr : (float *)out;
@@ -804,6 +827,43 @@ int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, f
   if (!out_is_device)
     CK(c, hipMemcpyAsync(out, c->d_out, (size_t)c->nout * sizeof(float), hipMemcpyDeviceToHost, c->stream));
   c->cur ^= 1;
+  return B2P_OK;
+}
+
+int b2p_integrate_n(b2p_ctx_t *c, const void *const *bufs, uint32_t nblk, float *out, int out_is_device) {
+  if (!c || !bufs || !out || nblk < 1 || nblk > kMaxBlk) return B2P_EINVAL;
+  LIVE(c);
+  if (c->samples != 0) return set_err(c, B2P_EINVAL, "b2p_integrate_n with a push pending");
+  for (uint32_t b = 0; b < nblk; ++b) {
+    if (!bufs[b]) return set_err(c, B2P_EINVAL, "null block %u", b);
+    if ((uintptr_t)bufs[b] % 16) return set_err(c, B2P_EALIGN, "block %u not 16-B aligned", b);
+  }
+  CK(c, hipSetDevice(c->device));
+  if (!c->d_mrep) {
+    const size_t words = 2 * (size_t)kMaxBlk * c->nrep * c->nout;
+    if (hipMalloc(&c->d_mrep, words * sizeof(unsigned long long)) != hipSuccess)
+      return set_err(c, B2P_ENOMEM, "hipMalloc multi-block replicas");
+    CK(c, hipMemsetAsync(c->d_mrep, 0, words * sizeof(unsigned long long), c->stream));
+  }
+  // host output: one staging row per block (d_out holds one spectrum)
+  float *dev_out = out;
+  if (!out_is_device) {
+    if (!c->d_mout) {
+      if (hipMalloc(&c->d_mout, (size_t)kMaxBlk * c->nout * sizeof(unsigned long long)) != hipSuccess)
+        return set_err(c, B2P_ENOMEM, "hipMalloc multi-block output");
+    }
+    dev_out = c->d_mout;
+  }
+  // the previous launch's finalize rides on this one, as for b2p_integrate
+  int rc = enqueue_span(c, bufs[0], c->block_bytes, nullptr, bufs, nblk);
+  if (rc != B2P_OK) return rc;
+  c->pend.valid = 1;
+  c->pend.rep = c->d_mrep + (size_t)c->mbank * kMaxBlk * c->nrep * c->nout;
+  c->pend.nblk = nblk;
+  c->pend.raw = 0;
+  c->pend.dev_out = dev_out;
+  c->pend.host_out = out_is_device ? nullptr : out;
+  c->mbank ^= 1;
   return B2P_OK;
 }
 

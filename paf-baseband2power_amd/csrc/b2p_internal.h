@@ -7,6 +7,9 @@
 
 namespace b2p {
 
+// ring blocks one launch may integrate back to back (b2p_integrate_n)
+constexpr uint32_t kMaxBlk = 8;
+
 enum Mode : int { kI8 = 0, kI16LE = 1, kI16BE = 2 };
 
 // One launch of the detect+integrate kernel over one pushed span.
@@ -40,6 +43,13 @@ struct IntegrateArgs {
   float *fin_out;
   uint32_t fin_raw;             // 1: fin_out receives the exact uint64 sums
   uint32_t nwork;               // streaming workgroups (NC*G)
+  // several whole integrations in one launch (b2p_integrate_n): block b is
+  // read from blk[b] and sums into rep + b * set_words; the carried
+  // finalize then covers fin_nblk sets into fin_out + b * nout
+  uint32_t nblk;                // 1: the single span at data
+  uint32_t fin_nblk;
+  uint64_t set_words;           // nrep * nout
+  const uint4 *blk[kMaxBlk];
 };
 
 struct FinalizeArgs {
@@ -50,6 +60,7 @@ struct FinalizeArgs {
   uint32_t mean;
   double nsamp;
   uint32_t raw;                 // 1: out receives the exact uint64 sums
+  uint32_t nblk;                // sets (grid.y): set b at rep + b * nrep * nout -> out + b * nout
 };
 
 // fp32 from exact sums that were reduced elsewhere (b2p_finalize_sums)

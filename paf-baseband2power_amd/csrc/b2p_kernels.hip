@@ -153,20 +153,30 @@ b2p_integrate_kernel(IntegrateArgs a) {
   for (uint32_t j = t; j < a.nout; j += blockDim.x) lds[j] = 0;
 
   if (a.fin_out && blockIdx.x == gridDim.x - 1) {
-    // the previous integration's finalize (its set was completed by the
-    // previous launch on this stream; this launch sums into the other set)
-    __syncthreads();
+    // the previous launch's finalize (its sets were completed by the
+    // previous launch on this stream; this launch sums into other sets):
+    // one set per integration it carried
     const uint32_t nwords = a.nrep * a.nout;
-    for (uint32_t k = t; k < nwords; k += blockDim.x) {
-      const unsigned long long x = a.fin_rep[k];
-      if (x) atomicAdd(&lds[k % a.nout], x);
-      a.fin_rep[k] = 0;
+    for (uint32_t b = 0; b < a.fin_nblk; ++b) {
+      unsigned long long *fr = a.fin_rep + (uint64_t)b * a.set_words;
+      if (b) {
+        __syncthreads();
+        for (uint32_t j = t; j < a.nout; j += blockDim.x) lds[j] = 0;
+      }
+      __syncthreads();
+      for (uint32_t k = t; k < nwords; k += blockDim.x) {
+        const unsigned long long x = fr[k];
+        if (x) atomicAdd(&lds[k % a.nout], x);
+        fr[k] = 0;
+      }
+      __syncthreads();
+      if (a.fin_raw)
+        for (uint32_t j = t; j < a.nout; j += blockDim.x)
+          reinterpret_cast<unsigned long long *>(a.fin_out)[(uint64_t)b * a.nout + j] = lds[j];
+      else
+        for (uint32_t j = t; j < a.nout; j += blockDim.x)
+          a.fin_out[(uint64_t)b * a.nout + j] = to_output(lds[j], a.mean, a.nsamp);
     }
-    __syncthreads();
-    if (a.fin_raw)
-      for (uint32_t j = t; j < a.nout; j += blockDim.x) reinterpret_cast<unsigned long long *>(a.fin_out)[j] = lds[j];
-    else
-      for (uint32_t j = t; j < a.nout; j += blockDim.x) a.fin_out[j] = to_output(lds[j], a.mean, a.nsamp);
     return;
   }
   const uint32_t col = blockIdx.x % a.NC;
@@ -186,9 +196,6 @@ b2p_integrate_kernel(IntegrateArgs a) {
       ch[w] = chunk * a.nchan_chunk + (q * VW + w) % a.nchan_chunk;
   }
 
-  const u32x4 *data = reinterpret_cast<const u32x4 *>(a.data);
-  A acc;
-  acc.zero_all();
   const uint64_t full = a.nvec / a.S;  // rows with every vector valid
   // this group's rows: rstart + i * rstep, i < rcount
   uint64_t rstart, rstep, rcount;
@@ -200,6 +207,16 @@ b2p_integrate_kernel(IntegrateArgs a) {
     rstart = (uint64_t)grp * full / a.G;
     rstep = 1;
     rcount = (uint64_t)(grp + 1) * full / a.G - rstart;
+  }
+  // one integration per block: the rows of block b stream through the same
+  // lanes (same channels), then the workgroup's sums go to block b's set
+  for (uint32_t b = 0; b < a.nblk; ++b) {
+  const u32x4 *data = reinterpret_cast<const u32x4 *>(a.nblk > 1 ? a.blk[b] : a.data);
+  A acc;
+  acc.zero_all();
+  if (b) {  // LDS of the previous block was drained into its set
+    __syncthreads();
+    for (uint32_t j = t; j < a.nout; j += blockDim.x) lds[j] = 0;
   }
   if (active) {
     // row offsets are wave-uniform (scalar); the lane offset is invariant
@@ -237,11 +254,12 @@ b2p_integrate_kernel(IntegrateArgs a) {
       }
   }
   __syncthreads();
-  unsigned long long *rep = a.rep + (uint64_t)(blockIdx.x % a.nrep) * a.nout;
+  unsigned long long *rep = a.rep + (uint64_t)b * a.set_words + (uint64_t)(blockIdx.x % a.nrep) * a.nout;
   for (uint32_t j = t; j < a.nout; j += blockDim.x) {
     const unsigned long long x = lds[j];
     if (x) atomicAdd(&rep[j], x);
   }
+  }  // blocks
   if (!a.out) return;
 
   // ---- in-launch finalize by the last workgroup to arrive ----------------
@@ -287,10 +305,12 @@ __global__ void __launch_bounds__(256) b2p_finalize_kernel(FinalizeArgs a) {
   __shared__ unsigned long long part[4][64];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint32_t j = blockIdx.x * 64 + lane;
+  unsigned long long *set = a.rep + (uint64_t)blockIdx.y * a.nrep * a.nout;  // integration y
+  float *out = a.out + (uint64_t)blockIdx.y * a.nout * (a.raw ? 2 : 1);
   unsigned long long s = 0;
   if (j < a.nout) {
     for (uint32_t r = w; r < a.nrep; r += 4) {
-      unsigned long long *p = a.rep + (uint64_t)r * a.nout + j;
+      unsigned long long *p = set + (uint64_t)r * a.nout + j;
       s += *p;
       *p = 0;
     }
@@ -300,9 +320,9 @@ __global__ void __launch_bounds__(256) b2p_finalize_kernel(FinalizeArgs a) {
   if (w == 0 && j < a.nout) {
     const unsigned long long tot = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
     if (a.raw)
-      reinterpret_cast<unsigned long long *>(a.out)[j] = tot;
+      reinterpret_cast<unsigned long long *>(out)[j] = tot;
     else
-      a.out[j] = to_output(tot, a.mean, a.nsamp);
+      out[j] = to_output(tot, a.mean, a.nsamp);
   }
 }
 
@@ -511,8 +531,8 @@ hipError_t launch_finalize(const FinalizeArgs &a, hipStream_t s, hipEvent_t ev0,
   const uint32_t grid = (a.nout + 63) / 64;
   FinalizeArgs arg = a;
   void *args[] = {&arg};
-  return hipExtLaunchKernel(reinterpret_cast<const void *>(b2p_finalize_kernel), dim3(grid),
-                            dim3(256), args, 0, s, ev0, ev1, 0);
+  return hipExtLaunchKernel(reinterpret_cast<const void *>(b2p_finalize_kernel),
+                            dim3(grid, a.nblk ? a.nblk : 1), dim3(256), args, 0, s, ev0, ev1, 0);
 }
 
 // Launched once by b2p_open: loading this translation unit's code object

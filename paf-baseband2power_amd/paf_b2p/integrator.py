@@ -131,6 +131,21 @@ class Integrator:
                                       int(out_is_device)), self._ctx)
         return None
 
+    def integrate_n(self, bufs, out_ptr: int | None = None, out_is_device: bool = False):
+        """b2p_integrate_n: len(bufs) whole integrations (device buffers) in ONE
+        launch.  With out_ptr None the spectra are returned (blocking)."""
+        ptrs = [self._span(b, None, None)[0] for b in bufs]
+        arr = (C.c_void_p * len(ptrs))(*ptrs)
+        if out_ptr is None:
+            out = np.zeros((len(ptrs), self.nout), dtype=np.float32)
+            L.check(L.lib().b2p_integrate_n(self._ctx, arr, len(ptrs), out.ctypes.data_as(C.c_void_p), 0),
+                    self._ctx)
+            self.sync()
+            return out
+        L.check(L.lib().b2p_integrate_n(self._ctx, arr, len(ptrs), C.c_void_p(out_ptr), int(out_is_device)),
+                self._ctx)
+        return None
+
     def sync(self) -> None:
         L.check(L.lib().b2p_sync(self._ctx), self._ctx)
 

@@ -1,0 +1,92 @@
+"""b2p_integrate_n: several whole integrations in one launch must give the
+same bits as one b2p_integrate per block, and as the oracle, whatever the
+layout, block count, output placement and the calls around it."""
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+import paf_b2p
+from paf_b2p import _lib as L
+
+pytestmark = pytest.mark.gpu
+SEED = 20181105
+
+LAYOUTS = {
+    "int8_64": dict(nbit=8, nchan_chunk=64, nsamp_int=1 << 14),
+    "int8_256_p2": dict(nbit=8, nchan_chunk=256, nsamp_int=1 << 13, npol_out=2, mean=1),
+    "bmf_small": dict(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=128 * 16),
+    "tftfp_8x8": dict(nbit=16, big_endian=1, nchunk=8, nsamp_df=128, nchan_chunk=8, nsamp_int=128 * 32),
+}
+
+
+def same(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("name", sorted(LAYOUTS))
+@pytest.mark.parametrize("k", [1, 2, 5, 8])
+def test_integrate_n_equals_separate_and_oracle(gpu, name, k):
+    g = npo.Geom(**LAYOUTS[name])
+    hosts = [co.fill_synthetic(g, g.block_bytes, SEED, 4, b) for b in range(k)]
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        ds = [it.upload(h) for h in hosts]
+        multi = it.integrate_n(ds)                         # host output, blocking
+        single = np.stack([it.integrate(d) for d in ds])
+        for d in ds:
+            d.free()
+    assert multi.shape == (k, g.nout)
+    for b in range(k):
+        assert same(multi[b], single[b]), b
+        assert same(multi[b], co.power(g, hosts[b])), b
+
+
+def test_integrate_n_back_to_back_device_output(gpu):
+    """three multi launches and single integrations interleaved without a
+    host sync: each launch's deferred finalize rides on the next, the two
+    replica banks alternate, every spectrum lands in its own device row"""
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 14)
+    hosts = [co.fill_synthetic(g, g.block_bytes, SEED, 6, b) for b in range(6)]
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        ds = [it.upload(h) for h in hosts]
+        out = it.alloc(14 * g.nout * 4)
+        row = 0
+        plan = [[0, 1, 2], "s3", [3, 4, 5, 0], [1, 2], "s4", "s5", [5, 4, 3]]
+        want = []
+        for step in plan:
+            if isinstance(step, str):
+                b = int(step[1:])
+                it.integrate(ds[b], out.ptr + row * g.nout * 4, True)
+                want.append(b)
+                row += 1
+            else:
+                it.integrate_n([ds[b] for b in step], out.ptr + row * g.nout * 4, True)
+                want += step
+                row += len(step)
+        it.sync()
+        got = it.download(out, nbytes=row * g.nout * 4).view(np.float32).reshape(row, g.nout)
+        for d in ds:
+            d.free()
+        out.free()
+    for r, b in enumerate(want):
+        assert same(got[r], co.power(g, hosts[b])), (r, b)
+
+
+def test_integrate_n_refusals(gpu):
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 12)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        d = it.alloc(g.block_bytes)
+        it.fill_synthetic(d, SEED, 0, 0)
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.integrate_n([d] * 9)                    # more than B2P_MAX_BLOCKS
+        assert e.value.code == L.B2P_EINVAL
+        it.push((d, 0, g.frame_bytes))
+        with pytest.raises(paf_b2p.B2PError):
+            it.integrate_n([d, d])                     # a push is pending
+        it.finish(allow_partial=True)
+        with pytest.raises(paf_b2p.B2PError) as e:
+            it.integrate_n([(d.ptr + 4, g.block_bytes)])   # misaligned block
+        assert e.value.code == L.B2P_EALIGN
+        out = it.integrate_n([d, d])
+        assert same(out[0], out[1])
+        d.free()

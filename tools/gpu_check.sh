@@ -5,7 +5,7 @@
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
-#          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf capturemt
+#          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -76,6 +76,12 @@ for s in $STEPS; do
          run pmc_write_asm 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm ;;
     matrix) run perf_matrix 600 python3 tools/perf_matrix.py --steps 20 ;;
+    multi) run multi_1 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "int8 64ch" &&
+           run multi_8 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "int8 64ch" --multi 8 &&
+           run multi_tf1 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "TFTFP 8x8" &&
+           run multi_tf8 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "TFTFP 8x8" --multi 8 &&
+           run multi_c2 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "int8 256ch" &&
+           run multi_c2_4 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "int8 256ch" --multi 4 ;;
     idlerep) run idle_rep0 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 &&
              run idle_rep3 300 python3 tools/perf_matrix.py --steps 20 --only "int8 256ch" --npol-out 1 --repeat 4 \
                --sleep 3 &&

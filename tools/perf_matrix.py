@@ -37,7 +37,9 @@ CASES = [
 KEEP = []  # --keep: buffers are never freed (diagnostic: no hipFree between runs)
 
 
-def run(name, geom, steps, keep=False, tuning=None):
+def run(name, geom, steps, keep=False, tuning=None, multi=1):
+    """steps integrations region-timed; multi > 1: in launches of `multi`
+    integrations each (b2p_integrate_n), steps rounded up to a multiple"""
     it = paf_b2p.Integrator(geom, tuning=tuning)
     bb = it.block_bytes
     blocks = []
@@ -45,21 +47,29 @@ def run(name, geom, steps, keep=False, tuning=None):
         d = it.alloc(bb)
         it.fill_synthetic(d, 20181105, 0, b)
         blocks.append(d)
+    steps = -(-steps // multi) * multi
     out = it.alloc(it.nout * 4 * steps)
-    for k in range(3):
-        it.integrate(blocks[k % 2], out.ptr, True)
+
+    def launch(k):  # integrations k .. k + multi - 1
+        dst = out.ptr + k * it.nout * 4
+        if multi == 1:
+            it.integrate(blocks[k % 2], dst, True)
+        else:
+            it.integrate_n([blocks[(k + j) % 2] for j in range(multi)], dst, True)
+    for k in range(0, 3 * multi, multi):
+        launch(0)
     it.sync()
     it.reset_stats()
     it.set_timing(2)
-    for k in range(steps):
-        it.integrate(blocks[k % 2], out.ptr + k * it.nout * 4, True)
+    for k in range(0, steps, multi):
+        launch(k)
     it.set_timing(0)
     it.sync()
     st = it.stats()
     us = st["kernel_ms"] / steps * 1e3
     res = {"case": name, "npol_out": geom.npol_out, "bytes": bb, "us_per_integration": round(us, 1),
            "GBps": round(bb / us / 1e3, 1), "threads": it.info.threads, "unroll": it.info.unroll,
-           "row_groups": it.info.row_groups, "columns": it.info.columns}
+           "row_groups": it.info.row_groups, "columns": it.info.columns, "blocks_per_launch": multi}
     if keep:
         KEEP.append((it, blocks, out))
         return res
@@ -79,6 +89,8 @@ def main():
                     help="idle seconds before each run: the previous run freed GiBs, and launches "
                          "in the next seconds run 2-8 %% slower (profiles/r01_free_effect.txt)")
     ap.add_argument("--keep", action="store_true", help="never free a run's buffers")
+    ap.add_argument("--multi", type=int, default=1,
+                    help="integrations per launch (b2p_integrate_n), e.g. 8")
     ap.add_argument("--tuning", default="", help='b2p_tuning_t fields as JSON, e.g. \'{"unroll": 8}\'')
     a = ap.parse_args()
     knobs = json.loads(a.tuning) if a.tuning else None
@@ -89,7 +101,7 @@ def main():
             for rep in range(a.repeat):
                 if a.sleep > 0:
                     time.sleep(a.sleep)
-                r = run(name, mk(npol_out=npo), a.steps, a.keep, knobs)
+                r = run(name, mk(npol_out=npo), a.steps, a.keep, knobs, a.multi)
                 if knobs:
                     r["tuning"] = knobs
                 if a.repeat > 1:
