@@ -49,7 +49,7 @@ def test_integrate_n_back_to_back_device_output(gpu):
     hosts = [co.fill_synthetic(g, g.block_bytes, SEED, 6, b) for b in range(6)]
     with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
         ds = [it.upload(h) for h in hosts]
-        out = it.alloc(14 * g.nout * 4)
+        out = it.alloc(15 * g.nout * 4)
         row = 0
         plan = [[0, 1, 2], "s3", [3, 4, 5, 0], [1, 2], "s4", "s5", [5, 4, 3]]
         want = []
