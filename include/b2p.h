@@ -230,7 +230,9 @@ int b2p_integrate(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device,
  * launch's fixed cost (dispatch ramp and tail, ~2 us) is paid once, not
  * nblk times, which matters for short integrations (a 256 MiB block reads in
  * ~40 us).  Same output bits as nblk b2p_integrate calls; the finalize is
- * deferred as for b2p_finish_async.  Requires no pending push. */
+ * deferred as for b2p_finish_async.  Requires no pending push.  Layouts
+ * whose rows span several workgroups (frame-split: BMF, TFTFP) run one
+ * launch per block, which measured as fast there. */
 #define B2P_MAX_BLOCKS 8
 int b2p_integrate_n(b2p_ctx_t *ctx, const void *const *bufs, uint32_t nblk, float *out,
                     int out_is_device);
