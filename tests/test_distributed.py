@@ -46,6 +46,12 @@ def _worker(rank, world, port, q):
     if r == 0:
         assert all(torch.equal(a, b) for a, b in zip(got, got2))
     el = D.max_over_ranks(0.5 + r)
+    # what ran, read back: the live group and every rank's identity record
+    seen = D.observed_world()
+    assert seen == {"backend": "gloo", "world_size": w, "rccl_ranks": 0}
+    ids = D.gather_identities({"rank": r, "host": "h", "pci_bus_id": f"0000:{r % 2:02x}:00.0"})
+    assert [i["rank"] for i in ids] == list(range(w))
+    assert D.distinct_gpus(ids) == min(2, w)
     if r == 0:
         q.put(("gather", [t.numpy() for t in got], el))
     else:
