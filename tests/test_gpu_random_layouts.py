@@ -57,3 +57,25 @@ def test_random_layouts_match_oracle(gpu, case):
         d.free()
     want = co.power(g, buf, nthreads=8)
     assert np.array_equal(out.view(np.uint32), want.view(np.uint32)), (g, cuts, seed)
+
+
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(layouts(), st.integers(1, 8))
+def test_random_layouts_multi_block(gpu, case, nblk):
+    """b2p_integrate_n on random layouts: nblk distinct blocks in one call
+    (one launch where the row is one workgroup wide, else one per block),
+    every spectrum equal to the oracle's"""
+    g, _, seed = case
+    if g.block_bytes > (1 << 20):  # keep nblk blocks small
+        g = npo.Geom(**{**g.asdict(), "nsamp_int": max(1, (1 << 20) // g.frame_bytes) * g.nsamp_df})
+    bufs = [co.fill_synthetic(g, g.block_bytes, seed, seed % 7, b) for b in range(nblk)]
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        ds = [it.upload(b) for b in bufs]
+        out = it.integrate_n(ds)
+        for d in ds:
+            d.free()
+    for b in range(nblk):
+        want = co.power(g, bufs[b], nthreads=8)
+        assert np.array_equal(out[b].view(np.uint32), want.view(np.uint32)), (g, nblk, b, seed)
