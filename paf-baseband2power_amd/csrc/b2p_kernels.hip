@@ -398,9 +398,8 @@ __global__ void __launch_bounds__(256) b2p_fill_kernel(uint4 *dst, uint64_t nvec
 // One wave per data frame: every lane reads the (broadcast) 24-B header and
 // computes the frame index itself (capture.c:566, same double arithmetic),
 // so no barrier is needed; the 7168-B payload moves as 7 x 1 KiB wave loads
-// and stores to (idf * nchunk + chunk) * 7168.  K frames per iteration put
-// 7K loads in flight per lane before the first store.  Per-chunk counts go
-// through LDS and leave with one atomic per counter per workgroup.
+// and stores to (idf * nchunk + chunk) * 7168.  Per-chunk counts go through
+// LDS and leave with one atomic per counter per workgroup.
 __device__ __forceinline__ uint32_t asm_slot(const AssembleArgs &a, uint64_t d, int64_t &rel) {
   const unsigned char *df = a.dfs + d * (uint64_t)a.df_bytes;
   const uint64_t w0 = __builtin_bswap64(*(const uint64_t *)df);  // hdr.c:15-18
@@ -414,7 +413,6 @@ __device__ __forceinline__ uint32_t asm_slot(const AssembleArgs &a, uint64_t d, 
   return chunk;
 }
 
-template <bool NTL, bool NTS, int K, bool EAGER>
 __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
   __shared__ unsigned long long cnt[256 + 3];
   const uint32_t ncnt = a.nchunk + 3;
@@ -423,41 +421,22 @@ __global__ void __launch_bounds__(256) b2p_assemble_kernel(AssembleArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t d0 = wave * K; d0 < a.ndf; d0 += nwaves * K) {
-    uint32_t slot[K];
-    int64_t rel[K];
-    u32x4 v[K][7];
+  for (uint64_t d = wave; d < a.ndf; d += nwaves) {
+    // the payload loads do not wait for the header: every frame in the
+    // buffer is read (nontemporal: read once), the header only decides where
+    // (or whether) it lands
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.dfs + d * (uint64_t)a.df_bytes + a.hdr_bytes);
+    u32x4 v[7];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint64_t d = d0 + j;
-      const u32x4 *src = reinterpret_cast<const u32x4 *>(a.dfs + d * (uint64_t)a.df_bytes + a.hdr_bytes);
-      if (EAGER && d < a.ndf) {
-        // the payload loads do not wait for the header: every frame in the
-        // buffer is read, the header only decides where (or whether) it lands
+    for (int k = 0; k < 7; ++k) v[k] = __builtin_nontemporal_load(src + k * 64 + lane);
+    int64_t rel;
+    const uint32_t slot = asm_slot(a, d, rel);  // wave-uniform
+    if (lane == 0) atomicAdd(&cnt[slot], 1ull);
+    if (slot >= a.nchunk) continue;
+    const uint32_t chunk = a.chunk_of_df[d];
+    u32x4 *dst = reinterpret_cast<u32x4 *>(a.block + ((uint64_t)rel * a.nchunk + chunk) * 7168ull);
 #pragma unroll
-        for (int k = 0; k < 7; ++k)
-          v[j][k] = NTL ? __builtin_nontemporal_load(src + k * 64 + lane) : src[k * 64 + lane];
-      }
-      slot[j] = d < a.ndf ? asm_slot(a, d, rel[j]) : 0xffffffffu;
-      if (!EAGER && slot[j] < a.nchunk) {  // wave-uniform
-#pragma unroll
-        for (int k = 0; k < 7; ++k)
-          v[j][k] = NTL ? __builtin_nontemporal_load(src + k * 64 + lane) : src[k * 64 + lane];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if (slot[j] == 0xffffffffu) continue;
-      if (lane == 0) atomicAdd(&cnt[slot[j]], 1ull);
-      if (slot[j] >= a.nchunk) continue;
-      const uint32_t chunk = a.chunk_of_df[d0 + j];
-      u32x4 *dst = reinterpret_cast<u32x4 *>(a.block + ((uint64_t)rel[j] * a.nchunk + chunk) * 7168ull);
-#pragma unroll
-      for (int k = 0; k < 7; ++k) {
-        if (NTS) __builtin_nontemporal_store(v[j][k], dst + k * 64 + lane);
-        else dst[k * 64 + lane] = v[j][k];
-      }
-    }
+    for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(v[k], dst + k * 64 + lane);
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < ncnt; j += blockDim.x)
@@ -475,8 +454,7 @@ hipError_t launch_assemble(const AssembleArgs &a, uint32_t grid_cap, hipStream_t
   const uint64_t cap = grid_cap ? grid_cap : 8192;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((b2p_assemble_kernel<true, true, 1, true>), dim3((uint32_t)blocks), dim3(256),
-                     0, s, a);
+  hipLaunchKernelGGL(b2p_assemble_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
