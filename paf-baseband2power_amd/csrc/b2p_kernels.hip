@@ -136,7 +136,7 @@ __device__ __forceinline__ float to_output(unsigned long long tot, uint32_t mean
 
 // UNROLL rows are loaded before any is consumed (UNROLL x 1 KiB in flight
 // per wave); NT selects the non-temporal load policy.  Both are tuning
-// knobs (B2P_UNROLL, B2P_NT) measured on the box, see DESIGN.md.
+// variants (b2p_tuning_t unroll / nontemporal) measured on the box, see DESIGN.md.
 //
 // Row mapping (a.interleave): 0 = row group g owns a contiguous slice of the
 // rows; 1 = group g owns rows g, g+G, g+2G, ... so that the whole grid
