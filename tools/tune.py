@@ -97,7 +97,7 @@ def main():
     rows = []
     for i, v in enumerate(vs):
         ms = statistics.median(res[i])
-        rows.append({**{k: v.get(k) for k in KNOBS}, **info[i], "median_us": round(ms * 1e3, 2),
+        rows.append({**v, **info[i], "median_us": round(ms * 1e3, 2),
                      "min_us": round(min(res[i]) * 1e3, 2), "GBps": round(bb / (ms * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda r: r["median_us"])
     print(json.dumps({"config": a.config, "block_bytes": bb, "rounds": a.rounds, "variants": rows},
