@@ -5,24 +5,19 @@
  * The reference links PSRDADA statically and
  * calls this subset: dada_hdu_*, ipcbuf_*, ipcio_*, ascii_header_*,
  * multilog*, fileread (diskdb.cu:24-130, capture.c:590-781,
- * paf_baseband2power.cu:82-84).  Same names, argument meaning and return
- * conventions (0 / pointer on success, -1 / NULL on error), so a host that
- * compiles against libpsrdada compiles against this and vice versa
- * (INTEGRATION.md).  Also provides the READER half the reference never
- * wrote (lock_read, open_block_read, ...; SURVEY.md Appendix A last item).
+ * paf_baseband2power.cu:82-84).  Same names, prototypes, struct layouts and
+ * return conventions as that libpsrdada (its debug info, recorded in
+ * tests/golden/psrdada_abi.json by tools/psrdada_dwarf.py), so a host
+ * compiled against either library's headers links against the other.
+ * Also the READER half the reference never wrote (lock_read,
+ * open_block_read, ...; SURVEY.md Appendix A last item).
  *
- * Ring model (one writer, up to 8 readers):
- *  - a data ring at `key` and a header ring at `key+1` (dada_hdu_set_key,
- *    SURVEY.md 3.1); each ring = a small sync segment at its key plus one
- *    shared-memory segment per block (ids kept in the sync segment), and one
- *    semaphore set (clear / full-per-reader / lock semaphores);
- *  - a block filled with fewer than bufsz bytes ends the transfer (EOD),
- *    exactly as PSRDADA's ipcbuf_mark_filled does.  The EOD
- *    mark is kept per block, so a ring carries any number of transfers: a
- *    reader stops at its transfer's EOD block and takes the next transfer
- *    (header, then data) after unlock_read + lock_read;
- *  - wire compatibility with libpsrdada's own segment layout is NOT claimed:
- *    processes on both sides of a ring must use this library.
+ * Rings are PSRDADA rings on the wire (csrc/dada/dada_internal.h): the same
+ * sync segment, key schedule, semaphore sets and writer/reader protocol, so
+ * libpafdada and libpsrdada processes share a ring (one writer, up to 8
+ * readers; data ring at `key`, header ring at `key+1`; a block marked filled
+ * with fewer than bufsz bytes, or the 0-byte block ipcio_close appends after
+ * a full one, ends the transfer; up to 8 transfers in flight).
  */
 #ifndef B2P_DADA_H
 #define B2P_DADA_H
@@ -48,38 +43,38 @@ int multilog(multilog_t *log, int priority, const char *format, ...)
 int multilog_close(multilog_t *log);
 
 /* ---- ipcbuf: one ring of shared-memory blocks ---- */
-typedef struct ipcsync ipcsync_t; /* shared state (opaque) */
-typedef struct ipcbuf {
-  int state;              /* 0 disconnected, 1 connected, 2 writer, 3 reader */
-  key_t key;
-  int syncid;             /* shm id of the sync segment */
-  int semid;              /* semaphore set id */
+typedef struct ipcsync ipcsync_t; /* the shared sync segment (dada_internal.h) */
+typedef struct {                  /* PSRDADA's ipcbuf_t, 104 B */
+  int state;                      /* DISCON 0, VIEWER 1, WRITER 2, WRITING 3, WCHANGE 4,
+                                     READER 5, READING 6, RSTOP 7 (end of data) */
+  int syncid;
+  int semid_connect;
+  int *semid_data;
+  int *shmid;
   ipcsync_t *sync;
-  char **buffer;          /* attached block addresses */
-  uint64_t nbufs, bufsz;
-  int iread;              /* reader slot, -1 if not a reader */
-  uint64_t xfer_count;    /* blocks taken by this process */
-  int cur_open;           /* blocks open (writer: 0/1; reader: up to read_depth) */
-  uint64_t cur_index;     /* the block opened last */
-  int read_depth;         /* reader: blocks it may hold at once (0 = 1, PSRDADA) */
-  int eod_pending;        /* reader: the empty EOD block waits behind open ones */
-  int eod_seen;           /* reader: took this transfer's EOD block (reset by lock_read) */
-  int wrote_eod;          /* writer: this session ended its transfer (reset by lock_write) */
+  char **buffer;                  /* block addresses in this process */
+  void **shm_addr;
+  char *count;                    /* in the sync segment: fills not yet cleared, per block */
+  key_t *shmkey;                  /* in the sync segment */
+  uint64_t viewbuf;
+  uint64_t xfer;
+  uint64_t soclock_buf;
+  int iread;                      /* reader slot, -1 if not a reader */
 } ipcbuf_t;
-#define IPCBUF_INIT {0, 0, -1, -1, NULL, NULL, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0}
+#define IPCBUF_INIT {0, -1, -1, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, 0, 0, -1}
 
 int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers);
 /* device_id >= 0: blocks in that GPU's memory, owned by a holder process and
- * shared through HIP IPC handles (PSRDADA ipcbuf_create_work; the sync
- * segment's on_device_id).  -1: SysV shared memory. */
+ * shared through HIP IPC handles (PSRDADA's ipcbuf_create_work and
+ * on_device_id).  -1: SysV shared memory. */
 int ipcbuf_create_work(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz,
                        unsigned n_readers, int device_id);
 int ipcbuf_connect(ipcbuf_t *id, key_t key);
 int ipcbuf_disconnect(ipcbuf_t *id);
 int ipcbuf_destroy(ipcbuf_t *id);
-int ipcbuf_lock_write(ipcbuf_t *id);
+int ipcbuf_lock_write(ipcbuf_t *id);  /* waits for the writer lock */
 int ipcbuf_unlock_write(ipcbuf_t *id);
-int ipcbuf_lock_read(ipcbuf_t *id);
+int ipcbuf_lock_read(ipcbuf_t *id);   /* waits for a free reader slot */
 int ipcbuf_unlock_read(ipcbuf_t *id);
 char *ipcbuf_get_next_write(ipcbuf_t *id);
 int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes);
@@ -88,31 +83,39 @@ int ipcbuf_mark_cleared(ipcbuf_t *id); /* releases the OLDEST block this reader 
 /* Extension (not in PSRDADA): let a reader hold up to `depth` blocks at once,
  * so a GPU consumer can launch on block k+1 before block k's kernel has
  * finished with it.  ipcbuf_get_next_read / ipcio_open_block_read take the
- * next block; ipcbuf_mark_cleared / ipcio_close_block_read release the oldest. */
+ * next block; ipcbuf_mark_cleared / ipcio_close_block_read release the
+ * oldest.  The shared state moves exactly as for a reader taking the blocks
+ * one at a time, so writers and other readers see a plain PSRDADA reader. */
 int ipcbuf_set_read_depth(ipcbuf_t *id, int depth);
 int ipcbuf_enable_sod(ipcbuf_t *id, uint64_t start_buf, uint64_t start_byte);
 int ipcbuf_disable_sod(ipcbuf_t *id);
-int ipcbuf_enable_eod(ipcbuf_t *id); /* end the transfer with an empty block */
-int ipcbuf_eod(ipcbuf_t *id);        /* 1 once this reader has reached EOD */
+int ipcbuf_enable_eod(ipcbuf_t *id); /* the next mark_filled ends the transfer */
+int ipcbuf_eod(ipcbuf_t *id);        /* 1 once this reader has cleared its transfer's EOD block */
 int ipcbuf_sod(ipcbuf_t *id);
+int ipcbuf_reset(ipcbuf_t *id);      /* reader at EOD: ready for the next transfer */
+char ipcbuf_is_writer(ipcbuf_t *id);
+char ipcbuf_is_writing(ipcbuf_t *id);
+char ipcbuf_is_reader(ipcbuf_t *id);
 uint64_t ipcbuf_get_bufsz(ipcbuf_t *id);
 uint64_t ipcbuf_get_nbufs(ipcbuf_t *id);
-uint64_t ipcbuf_get_nreaders(ipcbuf_t *id);
+int ipcbuf_get_nreaders(ipcbuf_t *id);
+uint64_t ipcbuf_get_write_count(ipcbuf_t *id); /* blocks filled so far */
+uint64_t ipcbuf_get_write_index(ipcbuf_t *id);
+uint64_t ipcbuf_get_read_count(ipcbuf_t *id);  /* this reader's (slot 0's) blocks cleared */
+uint64_t ipcbuf_get_read_count_iread(ipcbuf_t *id, unsigned iread);
+uint64_t ipcbuf_get_read_index(ipcbuf_t *id);
 /* address of block i (for device registration; PSRDADA's
- * dada_cuda_dbregister walks the same list) */
+ * dada_cuda_dbregister walks the same list) -- extension */
 char *ipcbuf_get_buffer(ipcbuf_t *id, uint64_t i);
-/* blocks written / cleared so far (monitoring, dada_dbmonitor role) */
-uint64_t ipcbuf_get_write_count(ipcbuf_t *id);
 /* -1 for a host ring; else the HIP device holding the blocks, whose
  * addresses (ipcbuf_get_next_read/write, ipcio_open_block_*) are device
  * pointers valid in this process.  Writers finish their kernels before
  * ipcbuf_mark_filled; readers finish theirs before ipcbuf_mark_cleared. */
 int ipcbuf_get_device(ipcbuf_t *id);
-/* copy host or device memory into / out of a block of either kind
- * (memcpy, or a synchronous hipMemcpy for a device ring) */
+/* extension: copy host or device memory into / out of a block of either
+ * kind (memcpy, or a synchronous hipMemcpy for a device ring) */
 int ipcbuf_copy_in(ipcbuf_t *id, char *block, const void *src, uint64_t n);
 int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n);
-uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread);
 /* Extension: make every ring wait of this process (a reader waiting for a
  * block, a writer waiting for a free one) give up -- the call fails, e.g.
  * ipcio_open_block_read returns NULL -- instead of resuming, once a signal
@@ -122,24 +125,36 @@ uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread);
 void dada_interrupt_waits(void);
 
 /* ---- ipcio: block-level streaming over an ipcbuf ---- */
-typedef struct ipcio {
+typedef struct { /* PSRDADA's ipcio_t, 152 B */
   ipcbuf_t buf;
   char *curbuf;
   uint64_t curbufsz;
-  int rdwrt; /* 'R' or 'W' */
+  uint64_t bytes;
+  char rdwrt; /* 'R', 'W', 'w' (writer, start of data deferred) or 0 */
+  char marked_filled;
+  char sod_pending;
+  uint64_t sod_buf;
+  uint64_t sod_byte;
 } ipcio_t;
-#define IPCIO_INIT {IPCBUF_INIT, NULL, 0, 0}
+#define IPCIO_INIT {IPCBUF_INIT, NULL, 0, 0, 0, 0, 0, 0, 0}
 
+int ipcio_connect(ipcio_t *ipc, key_t key);
+int ipcio_disconnect(ipcio_t *ipc);
 int ipcio_open(ipcio_t *ipc, char rdwrt);
-int ipcio_close(ipcio_t *ipc); /* writer: ends the transfer (EOD) */
+int ipcio_is_open(ipcio_t *ipc);
+int ipcio_close(ipcio_t *ipc); /* writer: ends the open transfer (EOD) */
 char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id);
-int ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes);
-/* NULL at end of data (writer signalled EOD and every block was read) */
+ssize_t ipcio_update_block_write(ipcio_t *ipc, uint64_t bytes);
+ssize_t ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes);
+/* NULL once the reader is at end of data; the block that ends a transfer
+ * may hold 0 bytes (the writer's ipcio_close after a full block) */
 char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id);
-ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes); /* PSRDADA's type */
+ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes);
+ssize_t ipcio_write(ipcio_t *ipc, char *ptr, size_t bytes);
+ssize_t ipcio_read(ipcio_t *ipc, char *ptr, size_t bytes); /* < bytes at end of data */
 
 /* ---- dada_hdu: data ring at key + header ring at key+1 ---- */
-typedef struct dada_hdu {
+typedef struct dada_hdu { /* PSRDADA's dada_hdu_t, 48 B */
   multilog_t *log;
   ipcio_t *data_block;
   ipcbuf_t *header_block;
@@ -157,8 +172,10 @@ void dada_hdu_destroy(dada_hdu_t *hdu);
 int dada_hdu_lock_write(dada_hdu_t *hdu);
 int dada_hdu_unlock_write(dada_hdu_t *hdu);
 int dada_hdu_lock_read(dada_hdu_t *hdu);
-int dada_hdu_unlock_read(dada_hdu_t *hdu);
-/* reader: wait for the next header block and copy it into hdu->header */
+int dada_hdu_unlock_read(dada_hdu_t *hdu); /* releases the header block dada_hdu_open took */
+/* reader: wait for the next header block and copy it into hdu->header
+ * (PSRDADA's dada_hdu_open; dada_hdu_open_read is the same call) */
+int dada_hdu_open(dada_hdu_t *hdu);
 int dada_hdu_open_read(dada_hdu_t *hdu);
 
 /* ring creation / removal (the dada_db tool, paf-baseband2power.py:114-115,
@@ -181,7 +198,7 @@ int ascii_header_set(char *header, const char *keyword, const char *format, ...)
 int ascii_header_del(char *header, const char *keyword);
 
 /* read up to bufsz bytes of a file into buffer, NUL-terminated (futils) */
-int fileread(const char *filename, char *buffer, unsigned bufsz); /* bytes read, -1 on error */
+long fileread(const char *filename, char *buffer, unsigned bufsz); /* bytes read, -1 on error */
 
 #ifdef __cplusplus
 }

@@ -1,16 +1,19 @@
 /*
  * dada_device.c -- GPU-resident ring blocks.
  *
- * PSRDADA keeps a device ring's blocks in GPU memory and names the device
- * in the sync segment (`on_device_id`, ipcsync_t +512, SURVEY.md Appendix A;
- * `ipc_alloc_cuda` in the reference's linked libpsrdada).  Here:
+ * PSRDADA keeps a device ring's blocks in GPU memory: on_device_id in the
+ * sync segment names the device, and block i's shared segment (key + 0x10000
+ * * (10+i)) holds a 64-B IPC memory handle instead of the data
+ * (`ipc_alloc_cuda` in the reference's linked libpsrdada, @0x407ec0).  Here
+ * the handles are HIP ones, and:
  *
  *  - a holder process (double-forked from the creator, so it outlives it)
- *    allocates the blocks with hipMalloc, publishes one HIP IPC handle per
- *    block in the sync segment, and keeps the memory alive until the ring
- *    is destroyed (SIGTERM) or its sync segment disappears (and, when
- *    DADA_HOLDER_IDLE_S is set, after that many seconds with no process
- *    attached but itself -- a guard against rings orphaned by a killed run);
+ *    allocates the blocks with hipMalloc, publishes each block's handle in
+ *    its segment, and keeps the memory alive until the ring is destroyed
+ *    (SIGTERM) or its sync segment disappears (and, when DADA_HOLDER_IDLE_S
+ *    is set, after that many seconds with no process attached but itself --
+ *    a guard against rings orphaned by a killed run).  Its pid and state
+ *    follow the handle in block 0's segment (dev_seg_t);
  *  - every process that connects opens the handles (hipIpcOpenMemHandle),
  *    so ipcbuf_get_next_read/write hand out device pointers;
  *  - producers and consumers order their kernels against the ring with
@@ -95,9 +98,10 @@ static void report(int fd, const char *what, int code) {
 }
 
 /* the holder: owns the blocks until SIGTERM/SIGINT or the ring is removed */
-static void holder(int syncid, ipcsync_t *s, int device, int wfd) {
+static void holder(ipcbuf_t *id, int device, int wfd) {
   int rc;
-  const uint64_t n = s->nbufs;
+  const uint64_t n = id->sync->nbufs, bufsz = id->sync->bufsz;
+  dev_seg_t *seg0 = id->shm_addr[0];
   void **blk = calloc(n, sizeof(void *));
   if (!blk) {
     report(wfd, "calloc", -1);
@@ -113,19 +117,18 @@ static void holder(int syncid, ipcsync_t *s, int device, int wfd) {
   }
   for (uint64_t i = 0; i < n; i++) {
     ipc_handle_t h;
-    if ((rc = hip.malloc_(&blk[i], s->bufsz)) != 0 || (rc = hip.memset_(blk[i], 0, s->bufsz)) != 0 ||
+    if ((rc = hip.malloc_(&blk[i], bufsz)) != 0 || (rc = hip.memset_(blk[i], 0, bufsz)) != 0 ||
         (rc = hip.get_handle(&h, blk[i])) != 0) {
       report(wfd, "hipMalloc/hipIpcGetMemHandle", rc);
       for (uint64_t j = 0; j <= i; j++)
         if (blk[j]) hip.free_(blk[j]);
       _exit(1);
     }
-    memcpy(sync_handles(s) + i * DEV_HANDLE_BYTES, &h, DEV_HANDLE_BYTES);
+    memcpy(id->shm_addr[i], &h, DEV_HANDLE_BYTES);
   }
   hip.sync();
-  s->holder_pid = (int32_t)getpid();
-  s->on_device_id = device;
-  __atomic_store_n(&s->holder_state, 1, __ATOMIC_RELEASE);
+  seg0->holder_pid = (int32_t)getpid();
+  __atomic_store_n(&seg0->holder_state, 1, __ATOMIC_RELEASE);
   (void)!write(wfd, "R", 1);
   close(wfd);
 
@@ -141,17 +144,16 @@ static void holder(int syncid, ipcsync_t *s, int device, int wfd) {
     struct timespec one = {1, 0};
     if (sigtimedwait(&set, NULL, &one) > 0) break;
     struct shmid_ds ds;
-    if (shmctl(syncid, IPC_STAT, &ds) < 0 || (ds.shm_perm.mode & SHM_DEST)) break;
+    if (shmctl(id->syncid, IPC_STAT, &ds) < 0 || (ds.shm_perm.mode & SHM_DEST)) break;
     idle = ds.shm_nattch <= 1 ? idle + 1 : 0;
     if (idle_max > 0 && idle >= idle_max) break;
   }
   for (uint64_t i = 0; i < n; i++) hip.free_(blk[i]);
-  __atomic_store_n(&s->holder_state, 2, __ATOMIC_RELEASE);
-  shmdt(s);
+  __atomic_store_n(&seg0->holder_state, 2, __ATOMIC_RELEASE);
   _exit(0);
 }
 
-int dev_create_blocks(int syncid, ipcsync_t *s, int device) {
+int dev_create_blocks(ipcbuf_t *id, int device) {
   int fds[2];
   if (pipe(fds) < 0) return -1;
   /* block the stop signals before forking: the holder takes them with
@@ -176,7 +178,7 @@ int dev_create_blocks(int syncid, ipcsync_t *s, int device) {
       dup2(dn, 2);
       if (dn > 2) close(dn);
     }
-    holder(syncid, s, device, fds[1]);
+    holder(id, device, fds[1]);
   }
   pthread_sigmask(SIG_SETMASK, &old, NULL);
   close(fds[1]);
@@ -199,11 +201,11 @@ int dev_create_blocks(int syncid, ipcsync_t *s, int device) {
   return -1;
 }
 
-int dev_stop_holder(ipcsync_t *s) {
-  if (s->holder_pid <= 0 || __atomic_load_n(&s->holder_state, __ATOMIC_ACQUIRE) != 1) return 0;
-  if (kill(s->holder_pid, SIGTERM) < 0) return errno == ESRCH ? 0 : -1;
+int dev_stop_holder(dev_seg_t *seg0) {
+  if (seg0->holder_pid <= 0 || __atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) != 1) return 0;
+  if (kill(seg0->holder_pid, SIGTERM) < 0) return errno == ESRCH ? 0 : -1;
   for (int i = 0; i < 1000; i++) { /* <= 10 s for the holder to free its memory */
-    if (__atomic_load_n(&s->holder_state, __ATOMIC_ACQUIRE) == 2) return 0;
+    if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) == 2) return 0;
     struct timespec t = {0, 10 * 1000 * 1000};
     nanosleep(&t, NULL);
   }
@@ -211,19 +213,16 @@ int dev_stop_holder(ipcsync_t *s) {
 }
 
 int dev_open_blocks(ipcbuf_t *id) {
-  ipcsync_t *s = id->sync;
-  if (__atomic_load_n(&s->holder_state, __ATOMIC_ACQUIRE) != 1 || hip_load() < 0) {
+  const dev_seg_t *seg0 = id->shm_addr[0];
+  if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) != 1 || hip_load() < 0 ||
+      hip.set_device(id->sync->on_device_id) != 0) {
     errno = ENODEV;
     return -1;
   }
-  if (hip.set_device(s->on_device_id) != 0) {
-    errno = ENODEV;
-    return -1;
-  }
-  for (uint64_t i = 0; i < id->nbufs; i++) {
+  for (uint64_t i = 0; i < id->sync->nbufs; i++) {
     ipc_handle_t h;
     void *p = NULL;
-    memcpy(&h, sync_handles(s) + i * DEV_HANDLE_BYTES, DEV_HANDLE_BYTES);
+    memcpy(&h, id->shm_addr[i], DEV_HANDLE_BYTES);
     if (hip.open_handle(&p, h, 1 /* hipIpcMemLazyEnablePeerAccess */) != 0) {
       errno = ENODEV;
       return -1;
@@ -235,8 +234,11 @@ int dev_open_blocks(ipcbuf_t *id) {
 
 void dev_close_blocks(ipcbuf_t *id) {
   if (hip_load() < 0) return;
-  for (uint64_t i = 0; i < id->nbufs; i++)
-    if (id->buffer[i]) hip.close_handle(id->buffer[i]);
+  for (uint64_t i = 0; i < id->sync->nbufs; i++)
+    if (id->buffer[i]) {
+      hip.close_handle(id->buffer[i]);
+      id->buffer[i] = NULL;
+    }
 }
 
 int dev_copy(void *dst, const void *src, uint64_t n) {

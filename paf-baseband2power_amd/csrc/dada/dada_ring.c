@@ -1,16 +1,34 @@
 /*
- * dada_ring.c -- SysV shared-memory rings with the PSRDADA ipcbuf / ipcio /
- * dada_hdu call surface (include/b2p_dada.h).
+ * dada_ring.c -- PSRDADA rings (ipcbuf / ipcio / dada_hdu) on SysV IPC.
  *
  * The reference links PSRDADA and uses its writer half (diskdb.cu:24-124,
  * capture.c:586-642, sync.c:101-109); the reader half its baseband2power
- * stage needed was never written.  Semantics
- * kept from PSRDADA: data ring at key, header ring at key+1; one writer,
- * several readers, each sees every block; a block marked filled with fewer
- * than bufsz bytes ends the transfer; a writer that stops
- * on a full block ends it with an empty block (ipcbuf_enable_eod).
+ * stage needed was never written.  This is a
+ * fresh implementation of that library's ring protocol, as its code in the
+ * reference's own binaries runs it (debug info + disassembly, recorded in
+ * tests/golden/psrdada_abi.json; the addresses below are paf_diskdb's):
+ * the same shared segments, keys and semaphores (dada_internal.h), and the
+ * same writer / reader state machine, so a ring is shared with processes
+ * linked against libpsrdada itself (dada_db, dada_dbdisk, ...).
+ *
+ *  writer  lock_write (WRITE lock) -> [enable_sod] -> get_next_write (waits
+ *          CLEAR of every reader for a block still counted in count[]) ->
+ *          mark_filled (FULL of every reader +1; a short block, or any block
+ *          after enable_eod, ends the transfer: EODACK, e_buf / e_byte /
+ *          eod[xfer]) -> unlock_write
+ *  reader  lock_read (READ slot + the free reader slot with the lowest
+ *          r_bufs) -> get_next_read (FULL -1; the first block of a transfer
+ *          starts at s_buf / s_byte and acknowledges SODACK) -> mark_cleared
+ *          (CLEAR +1; the end-of-data block acknowledges EODACK and stops the
+ *          reader: ipcbuf_eod) -> unlock_read
+ *
+ * Extensions (not in PSRDADA, invisible on the wire): a reader may hold
+ * several blocks (ipcbuf_set_read_depth), ring waits can be interrupted
+ * from a signal handler (dada_interrupt_waits), and device rings keep their
+ * blocks in a holder process (dada_device.c).
  */
 #include <errno.h>
+#include <inttypes.h>
 #include <signal.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -30,9 +48,9 @@ static volatile sig_atomic_t g_interrupt;
 
 void dada_interrupt_waits(void) { g_interrupt = 1; }
 
-/* semop with EINTR retry (until dada_interrupt_waits); flags e.g.
- * SEM_UNDO | IPC_NOWAIT */
-static int sem_do(int semid, int num, int op, int flags) {
+/* ipc_semop (@0x4088a0) with EINTR retry until dada_interrupt_waits;
+ * flags e.g. SEM_UNDO | IPC_NOWAIT */
+static int sem_op(int semid, int num, int op, int flags) {
   struct sembuf sb;
   sb.sem_num = (unsigned short)num;
   sb.sem_op = (short)op;
@@ -97,65 +115,140 @@ int multilog_close(multilog_t *m) {
 }
 
 /* ------------------------------------------------------------------ */
-/* ipcbuf                                                               */
+/* ipcbuf: segments                                                     */
 
-/* Build the sync segment, the semaphores and the blocks: SysV segments for
- * a host ring, device memory held by a holder process for a device ring
- * (dada_device.c).  The magic is written last, so a connector never sees a
- * half-built ring. */
-static int ring_create(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers, int device) {
-  if (!nbufs || !bufsz || n_readers > IPCBUF_READERS || nbufs > 32767) return -1;
-  int syncid = shmget(key, sync_size(nbufs), IPC_CREAT | IPC_EXCL | 0666);
-  if (syncid < 0) return -1;
-  ipcsync_t *s = shmat(syncid, NULL, 0);
-  if (s == (void *)-1) {
-    shmctl(syncid, IPC_RMID, NULL);
+/* shmkey[] follows count[] at 520 + nbufs: possibly unaligned, so it is
+ * read and written by value */
+static key_t shmkey_get(const ipcbuf_t *id, uint64_t i) {
+  key_t k;
+  memcpy(&k, (const char *)id->shmkey + i * sizeof(key_t), sizeof k);
+  return k;
+}
+
+static void shmkey_set(ipcbuf_t *id, uint64_t i, key_t k) {
+  memcpy((char *)id->shmkey + i * sizeof(key_t), &k, sizeof k);
+}
+
+/* ipcsync_get (@0x402fe0): the sync segment, count[] and shmkey[] after it */
+static int sync_get(ipcbuf_t *id, key_t key, uint64_t nbufs, int flag) {
+  id->syncid = shmget(key, nbufs ? sync_size(nbufs) : sizeof(ipcsync_t), flag);
+  if (id->syncid < 0) return -1;
+  void *p = shmat(id->syncid, NULL, 0);
+  if (p == (void *)-1) {
+    id->syncid = -1;
     return -1;
   }
+  id->sync = p;
+  if (!nbufs) nbufs = id->sync->nbufs;
+  id->count = (char *)(id->sync + 1);
+  id->shmkey = (key_t *)(id->count + nbufs);
+  id->state = ST_DISCON;
+  id->viewbuf = 0;
+  return 0;
+}
+
+/* ipcbuf_get (@0x403090): the semaphore sets and the blocks; kc is the
+ * connect set's key (semkey_connect, published last by a creator) */
+static int ring_get(ipcbuf_t *id, key_t kc, int flag) {
+  ipcsync_t *s = id->sync;
+  const uint64_t n = s->nbufs;
+  id->semid_connect = semget(kc, NSEM_CONNECT, flag);
+  if (id->semid_connect < 0) return -1;
+  id->semid_data = malloc((s->n_readers ? s->n_readers : 1) * sizeof(int));
+  id->buffer = calloc(n, sizeof(char *));
+  id->shm_addr = calloc(n, sizeof(void *));
+  id->shmid = malloc(n * sizeof(int));
+  if (!id->semid_data || !id->buffer || !id->shm_addr || !id->shmid) return -1;
+  for (unsigned r = 0; r < s->n_readers; r++) id->semid_data[r] = -1;
+  for (unsigned r = 0; r < s->n_readers; r++) {
+    id->semid_data[r] = semget(s->semkey_data[r], NSEM_DATA, flag);
+    if (id->semid_data[r] < 0) return -1;
+  }
+  for (uint64_t i = 0; i < n; i++) id->shmid[i] = -1;
+  for (uint64_t i = 0; i < n; i++) {
+    const int dev = s->on_device_id >= 0;
+    /* a device ring's segment holds the handle (block 0: and the holder) */
+    const size_t sz = !dev ? s->bufsz : (flag & IPC_CREAT) ? (i ? DEV_HANDLE_BYTES : sizeof(dev_seg_t)) : 0;
+    id->shmid[i] = shmget(shmkey_get(id, i), sz, flag);
+    if (id->shmid[i] < 0) return -1;
+    void *p = shmat(id->shmid[i], NULL, 0);
+    if (p == (void *)-1) return -1;
+    id->shm_addr[i] = p;
+    if (!dev) id->buffer[i] = p;
+  }
+  return 0;
+}
+
+static void free_local(ipcbuf_t *id) {
+  if (id->shm_addr && id->sync) {
+    if (id->sync->on_device_id >= 0 && id->buffer) dev_close_blocks(id);
+    for (uint64_t i = 0; i < id->sync->nbufs; i++)
+      if (id->shm_addr[i]) shmdt(id->shm_addr[i]);
+  }
+  free(id->buffer);
+  free(id->shm_addr);
+  free(id->shmid);
+  free(id->semid_data);
+  id->buffer = NULL;
+  id->shm_addr = NULL;
+  id->shmid = NULL;
+  id->semid_data = NULL;
+}
+
+/* remove every segment and semaphore set a (possibly half-built) ring has */
+static void remove_ipc(ipcbuf_t *id) {
+  ipcsync_t *s = id->sync;
+  if (s->on_device_id >= 0 && id->shm_addr && id->shm_addr[0]) dev_stop_holder(id->shm_addr[0]);
+  for (uint64_t i = 0; id->shmid && i < s->nbufs; i++)
+    if (id->shmid[i] >= 0) shmctl(id->shmid[i], IPC_RMID, NULL);
+  for (unsigned r = 0; id->semid_data && r < s->n_readers; r++)
+    if (id->semid_data[r] >= 0) semctl(id->semid_data[r], 0, IPC_RMID);
+  if (id->semid_connect >= 0) semctl(id->semid_connect, 0, IPC_RMID);
+}
+
+static int ring_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
+                       int device, int open_device) {
+  const ipcbuf_t init = IPCBUF_INIT;
+  *id = init;
+  if (!nbufs || !bufsz || n_readers > IPCBUF_READERS || nbufs > 0x7fff) {
+    errno = EINVAL;
+    return -1;
+  }
+  if (sync_get(id, key, nbufs, IPC_CREAT | IPC_EXCL | 0666) < 0) return -1;
+  ipcsync_t *s = id->sync;
   memset(s, 0, sync_size(nbufs));
   s->nbufs = nbufs;
-  for (uint64_t i = 0; i < nbufs; i++) sync_shmids(s)[i] = -1;
   s->bufsz = bufsz;
   s->n_readers = n_readers;
-  s->on_device_id = -1;
-  s->semid = semget(IPC_PRIVATE, NSEMS, IPC_CREAT | 0666);
-  int ok = s->semid >= 0;
-  if (ok) {
-    unsigned short v[NSEMS];
-    memset(v, 0, sizeof v);
-    v[SEM_CLEAR] = (unsigned short)nbufs;
-    v[SEM_WLOCK] = 1;
-    for (int r = 0; r < IPCBUF_READERS; r++) v[SEM_RLOCK(r)] = 1;
-    union semun_u {
-      int val;
-      struct semid_ds *buf;
-      unsigned short *array;
-    } arg;
-    arg.array = v;
-    ok = semctl(s->semid, 0, SETALL, arg) == 0;
-  }
-  if (ok && device >= 0) {
-    ok = dev_create_blocks(syncid, s, device) == 0;
-  } else {
-    for (uint64_t i = 0; ok && i < nbufs; i++) {
-      int sid = shmget(IPC_PRIVATE, bufsz, IPC_CREAT | 0666);
-      sync_shmids(s)[i] = sid;
-      if (sid < 0) ok = 0;
-    }
-  }
+  s->on_device_id = device;
+  for (int x = 0; x < IPCBUF_XFERS; x++) s->eod[x] = 1; /* @0x403434 */
+  for (int r = 0; r < IPCBUF_READERS; r++) s->semkey_data[r] = key_data(key, r);
+  for (uint64_t i = 0; i < nbufs; i++) shmkey_set(id, i, key_block(key, i));
+  /* semkey_connect is published last (below): a connector that finds the
+   * segment before the ring is complete sees 0 there and backs off */
+  const key_t kc = key_connect(key);
+  int ok = ring_get(id, kc, IPC_CREAT | IPC_EXCL | 0666) == 0;
+  /* @0x403528-0x4035b1: WRITE 1, READ n_readers; per reader SODACK 8,
+   * EODACK 8, READER_CONN 1 */
+  if (ok) ok = sem_op(id->semid_connect, SEM_WRITE, 1, 0) == 0;
+  if (ok && n_readers) ok = sem_op(id->semid_connect, SEM_READ, (int)n_readers, 0) == 0;
+  for (unsigned r = 0; ok && r < n_readers; r++)
+    ok = sem_op(id->semid_data[r], SEM_SODACK, IPCBUF_XFERS, 0) == 0 &&
+         sem_op(id->semid_data[r], SEM_EODACK, IPCBUF_XFERS, 0) == 0 &&
+         sem_op(id->semid_data[r], SEM_READER_CONN, 1, 0) == 0;
+  if (ok && device >= 0) ok = dev_create_blocks(id, device) == 0 && (!open_device || dev_open_blocks(id) == 0);
   if (!ok) {
     const int e = errno;
-    for (uint64_t i = 0; i < nbufs; i++)
-      if (sync_shmids(s)[i] >= 0) shmctl(sync_shmids(s)[i], IPC_RMID, NULL);
-    if (s->semid >= 0) semctl(s->semid, 0, IPC_RMID);
+    remove_ipc(id);
+    free_local(id);
     shmdt(s);
-    shmctl(syncid, IPC_RMID, NULL);
+    shmctl(id->syncid, IPC_RMID, NULL);
+    *id = init;
     errno = e;
     return -1;
   }
-  s->version = SYNC_VERSION;
-  __atomic_store_n(&s->magic, SYNC_MAGIC, __ATOMIC_RELEASE);
-  shmdt(s);
+  __atomic_store_n(&s->semkey_connect, kc, __ATOMIC_RELEASE);
+  id->state = ST_VIEWER;
   return 0;
 }
 
@@ -165,229 +258,283 @@ int ipcbuf_create(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsig
 
 int ipcbuf_create_work(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
                        int device_id) {
-  if (!id || ring_create(key, nbufs, bufsz, n_readers, device_id) < 0) return -1;
-  return ipcbuf_connect(id, key);
+  if (!id) return -1;
+  return ring_create(id, key, nbufs, bufsz, n_readers, device_id < 0 ? -1 : device_id, 1);
 }
 
 int ipcbuf_connect(ipcbuf_t *id, key_t key) {
   if (!id) return -1;
-  ipcbuf_t init = IPCBUF_INIT;
+  const ipcbuf_t init = IPCBUF_INIT;
   *id = init;
-  id->key = key;
-  id->syncid = shmget(key, 0, 0);
-  if (id->syncid < 0) return -1;
-  id->sync = shmat(id->syncid, NULL, 0);
-  if (id->sync == (void *)-1) {
-    id->sync = NULL;
+  if (sync_get(id, key, 0, 0666) < 0) return -1;
+  if (__atomic_load_n(&id->sync->semkey_connect, __ATOMIC_ACQUIRE) == 0) { /* still being built */
+    ipcbuf_disconnect(id);
+    errno = EAGAIN;
     return -1;
   }
-  if (__atomic_load_n(&id->sync->magic, __ATOMIC_ACQUIRE) != SYNC_MAGIC ||
-      id->sync->version != SYNC_VERSION) {
-    shmdt(id->sync);
-    id->sync = NULL;
-    errno = EINVAL;
+  if (ring_get(id, id->sync->semkey_connect, 0666) < 0 ||
+      (id->sync->on_device_id >= 0 && dev_open_blocks(id) < 0)) {
+    const int e = errno;
+    ipcbuf_disconnect(id);
+    errno = e;
     return -1;
   }
-  id->nbufs = id->sync->nbufs;
-  id->bufsz = id->sync->bufsz;
-  id->semid = id->sync->semid;
-  id->buffer = calloc(id->nbufs, sizeof(char *));
-  if (!id->buffer) return -1;
-  if (id->sync->on_device_id >= 0) {
-    if (dev_open_blocks(id) < 0) {
-      ipcbuf_disconnect(id);
-      return -1;
-    }
-  } else {
-    for (uint64_t i = 0; i < id->nbufs; i++) {
-      void *p = shmat(sync_shmids(id->sync)[i], NULL, 0);
-      if (p == (void *)-1) {
-        ipcbuf_disconnect(id);
-        return -1;
-      }
-      id->buffer[i] = p;
-    }
-  }
-  id->state = 1;
+  id->state = ST_VIEWER;
   return 0;
 }
 
+/* ipcbuf_disconnect (@0x403780): detach; a lock still held stays with the
+ * process until it exits (SEM_UNDO) */
 int ipcbuf_disconnect(ipcbuf_t *id) {
   if (!id) return -1;
-  if (id->state == 2) ipcbuf_unlock_write(id);
-  if (id->state == 3) ipcbuf_unlock_read(id);
-  if (id->buffer) {
-    if (id->sync && id->sync->on_device_id >= 0) {
-      dev_close_blocks(id);
-    } else {
-      for (uint64_t i = 0; i < id->nbufs; i++)
-        if (id->buffer[i]) shmdt(id->buffer[i]);
-    }
-    free(id->buffer);
-    id->buffer = NULL;
-  }
+  free_local(id);
   if (id->sync) shmdt(id->sync);
   id->sync = NULL;
-  id->state = 0;
+  id->count = NULL;
+  id->shmkey = NULL;
+  id->state = ST_DISCON;
+  id->iread = -1;
   return 0;
 }
 
 int ipcbuf_destroy(ipcbuf_t *id) {
   if (!id || !id->sync) return -1;
-  int semid = id->semid, syncid = id->syncid;
-  uint64_t n = id->nbufs;
-  int32_t *ids = malloc(n * sizeof(int32_t));
-  if (!ids) return -1;
-  memcpy(ids, sync_shmids(id->sync), n * sizeof(int32_t));
-  ipcsync_t *s = shmat(syncid, NULL, 0); /* outlives the disconnect below */
+  const int syncid = id->syncid;
+  remove_ipc(id);
   ipcbuf_disconnect(id);
-  if (s != (void *)-1) {
-    if (s->on_device_id >= 0) dev_stop_holder(s);
-    shmdt(s);
-  }
-  for (uint64_t i = 0; i < n; i++)
-    if (ids[i] >= 0) shmctl(ids[i], IPC_RMID, NULL);
-  free(ids);
-  semctl(semid, 0, IPC_RMID);
   shmctl(syncid, IPC_RMID, NULL);
+  id->syncid = -1;
+  id->semid_connect = -1;
   return 0;
 }
 
-int ipcbuf_lock_write(ipcbuf_t *id) {
-  if (!id || id->state != 1) return -1;
-  if (sem_do(id->semid, SEM_WLOCK, -1, SEM_UNDO | IPC_NOWAIT) < 0) return -1;
-  id->state = 2;
-  id->xfer_count = id->sync->w_count;
-  id->wrote_eod = 0;
+/* ------------------------------------------------------------------ */
+/* ipcbuf: writer                                                       */
+
+char ipcbuf_is_writer(ipcbuf_t *id) { return id && id->state >= ST_WRITER && id->state <= ST_WCHANGE; }
+char ipcbuf_is_writing(ipcbuf_t *id) { return id && id->state == ST_WRITING; }
+char ipcbuf_is_reader(ipcbuf_t *id) { return id && id->state >= ST_READER && id->state <= ST_RSTOP; }
+
+int ipcbuf_lock_write(ipcbuf_t *id) {  /* @0x403b00 */
+  if (!id || id->state != ST_VIEWER) return -1;
+  if (sem_op(id->semid_connect, SEM_WRITE, -1, SEM_UNDO) < 0) return -1;
+  id->state = id->sync->w_state ? ST_WRITING : ST_WCHANGE;
+  id->xfer = id->sync->w_xfer % IPCBUF_XFERS;
   return 0;
 }
 
-int ipcbuf_unlock_write(ipcbuf_t *id) {
-  if (!id || id->state != 2) return -1;
-  sem_do(id->semid, SEM_WLOCK, 1, SEM_UNDO);
-  id->state = 1;
+int ipcbuf_unlock_write(ipcbuf_t *id) {  /* @0x403b90 */
+  if (!ipcbuf_is_writer(id)) return -1;
+  if (sem_op(id->semid_connect, SEM_WRITE, 1, SEM_UNDO) < 0) return -1;
+  id->state = ST_VIEWER;
   return 0;
 }
 
-int ipcbuf_lock_read(ipcbuf_t *id) {
-  if (!id || id->state != 1) return -1;
-  for (uint32_t r = 0; r < id->sync->n_readers; r++) {
-    if (sem_do(id->semid, SEM_RLOCK(r), -1, SEM_UNDO | IPC_NOWAIT) == 0) {
-      id->iread = (int)r;
-      id->state = 3;
-      id->xfer_count = id->sync->r_count[r];
-      id->eod_seen = 0; /* the next transfer starts after the last EOD taken */
-      return 0;
-    }
-  }
-  return -1;
+static uint64_t sod_minbuf(ipcbuf_t *id) {  /* ipcbuf_get_sod_minbuf @0x403ca0 */
+  const ipcsync_t *s = id->sync;
+  return s->w_buf - id->soclock_buf < s->nbufs ? id->soclock_buf : s->w_buf + 1 - s->nbufs;
 }
 
-int ipcbuf_unlock_read(ipcbuf_t *id) {
-  if (!id || id->state != 3) return -1;
-  sem_do(id->semid, SEM_RLOCK(id->iread), 1, SEM_UNDO);
-  id->iread = -1;
-  id->state = 1;
-  return 0;
-}
-
-char *ipcbuf_get_next_write(ipcbuf_t *id) {
-  if (!id || id->state != 2 || id->cur_open) return NULL;
-  if (sem_do(id->semid, SEM_CLEAR, -1, 0) < 0) return NULL;
-  id->cur_index = id->sync->w_count % id->nbufs;
-  id->cur_open = 1;
-  return id->buffer[id->cur_index];
-}
-
-int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {
-  if (!id || id->state != 2 || !id->cur_open || nbytes > id->bufsz) return -1;
+int ipcbuf_enable_sod(ipcbuf_t *id, uint64_t start_buf, uint64_t start_byte) {  /* @0x403cd0 */
+  if (!id || !(id->state == ST_WRITER || id->state == ST_WCHANGE)) return -1;
   ipcsync_t *s = id->sync;
-  sync_nbytes(s)[id->cur_index] = nbytes;
-  sync_eod(s)[id->cur_index] = nbytes < id->bufsz; /* short block = EOD */
-  if (nbytes < id->bufsz) id->wrote_eod = 1;
-  __atomic_store_n(&s->w_count, s->w_count + 1, __ATOMIC_RELEASE);
-  id->cur_open = 0;
-  id->xfer_count++;
-  for (uint32_t r = 0; r < s->n_readers; r++)
-    if (sem_do(id->semid, SEM_FULL(r), 1, 0) < 0) return -1;
+  if (start_buf > s->w_buf || start_buf < sod_minbuf(id) || start_byte > s->bufsz) return -1;
+  for (unsigned r = 0; r < s->n_readers; r++) /* every reader has acknowledged a start slot */
+    if (sem_op(id->semid_data[r], SEM_SODACK, -1, 0) < 0) return -1;
+  const uint64_t x = s->w_xfer % IPCBUF_XFERS;
+  id->xfer = x;
+  s->s_buf[x] = start_buf;
+  s->s_byte[x] = start_byte;
+  if (s->w_buf == 0)
+    s->eod[x] = 0;
+  else
+    for (uint64_t b = start_buf; b < s->w_buf; b++) id->count[b % s->nbufs]++;
+  const uint64_t new_bufs = s->w_buf - start_buf;
+  id->state = ST_WRITING;
+  s->w_state = ST_WRITING;
+  for (unsigned r = 0; new_bufs && r < s->n_readers; r++)
+    if (sem_op(id->semid_data[r], SEM_FULL, (int)(short)new_bufs, 0) < 0) return -1;
   return 0;
 }
 
-int ipcbuf_enable_eod(ipcbuf_t *id) {
-  if (!id || id->state != 2) return -1;
-  if (id->wrote_eod) return 0; /* this session's transfer already ended */
-  if (!ipcbuf_get_next_write(id)) return -1;
-  return ipcbuf_mark_filled(id, 0);
+int ipcbuf_disable_sod(ipcbuf_t *id) {  /* @0x403c60 */
+  if (!id || id->state != ST_WCHANGE) return -1;
+  id->state = ST_WRITER;
+  return 0;
+}
+
+int ipcbuf_enable_eod(ipcbuf_t *id) {  /* @0x403c20 */
+  if (!id || id->state != ST_WRITING) return -1;
+  id->state = ST_WCHANGE;
+  return 0;
+}
+
+char *ipcbuf_get_next_write(ipcbuf_t *id) {  /* @0x403f20 */
+  if (!ipcbuf_is_writer(id)) return NULL;
+  ipcsync_t *s = id->sync;
+  if (id->state == ST_WCHANGE && ipcbuf_enable_sod(id, s->w_buf, 0) < 0) return NULL;
+  const uint64_t b = s->w_buf % s->nbufs;
+  while (id->count[b]) { /* every reader has cleared the block's last fill */
+    for (unsigned r = 0; r < s->n_readers; r++)
+      if (sem_op(id->semid_data[r], SEM_CLEAR, -1, 0) < 0) return NULL;
+    id->count[b]--;
+  }
+  return id->buffer[b];
+}
+
+int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {  /* @0x404170 */
+  if (!ipcbuf_is_writer(id)) return -1;
+  ipcsync_t *s = id->sync;
+  if (nbytes > s->bufsz) return -1;
+  if (id->state == ST_WRITER) { /* start of data disabled: invisible to readers */
+    s->w_buf++;
+    return 0;
+  }
+  if (id->state == ST_WCHANGE || nbytes < s->bufsz) { /* this block ends the transfer */
+    for (unsigned r = 0; r < s->n_readers; r++)
+      if (sem_op(id->semid_data[r], SEM_EODACK, -1, 0) < 0) return -1;
+    s->e_buf[id->xfer] = s->w_buf;
+    s->e_byte[id->xfer] = nbytes;
+    s->eod[id->xfer] = 1;
+    s->w_xfer++;
+    id->xfer = s->w_xfer % IPCBUF_XFERS;
+    id->state = ST_WRITER;
+    s->w_state = 0;
+  }
+  id->count[s->w_buf % s->nbufs]++;
+  s->w_buf++;
+  for (unsigned r = 0; r < s->n_readers; r++)
+    if (sem_op(id->semid_data[r], SEM_FULL, 1, 0) < 0) return -1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* ipcbuf: reader                                                       */
+
+/* read depth (extension): viewbuf, unused by a reader in PSRDADA, holds
+ * this process's depth | blocks held << 8 | end-of-data block held << 16 */
+static int rd_depth(const ipcbuf_t *id) { return (int)(id->viewbuf & 0xff) ? (int)(id->viewbuf & 0xff) : 1; }
+static int rd_open(const ipcbuf_t *id) { return (int)((id->viewbuf >> 8) & 0xff); }
+static int rd_eod_held(const ipcbuf_t *id) { return (int)((id->viewbuf >> 16) & 1); }
+static void rd_set(ipcbuf_t *id, int open, int eod_held) {
+  id->viewbuf = (id->viewbuf & 0xff) | ((uint64_t)open << 8) | ((uint64_t)(eod_held != 0) << 16);
 }
 
 int ipcbuf_set_read_depth(ipcbuf_t *id, int depth) {
-  if (!id || depth < 1 || (uint64_t)depth > id->nbufs) return -1;
-  id->read_depth = depth;
+  if (!id || !id->sync || depth < 1 || depth > 255 || (uint64_t)depth > id->sync->nbufs) return -1;
+  id->viewbuf = (id->viewbuf & ~(uint64_t)0xff) | (uint64_t)depth;
   return 0;
 }
 
-char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {
-  if (!id || id->state != 3) return NULL;
-  if (id->cur_open >= (id->read_depth > 1 ? id->read_depth : 1)) return NULL;
-  if (id->eod_seen) return NULL; /* this transfer is over */
-  if (sem_do(id->semid, SEM_FULL(id->iread), -1, 0) < 0) return NULL;
-  id->cur_index = (id->sync->r_count[id->iread] + (uint64_t)id->cur_open) % id->nbufs;
-  id->cur_open++;
-  if (sync_eod(id->sync)[id->cur_index]) id->eod_seen = 1;
-  if (bytes) *bytes = sync_nbytes(id->sync)[id->cur_index];
-  return id->buffer[id->cur_index];
-}
-
-static int clear_oldest(ipcbuf_t *id) {
+int ipcbuf_lock_read(ipcbuf_t *id) {  /* @0x404360 */
+  if (!id || id->state != ST_VIEWER || id->iread != -1) return -1;
+  if (sem_op(id->semid_connect, SEM_READ, -1, SEM_UNDO) < 0) return -1;
   ipcsync_t *s = id->sync;
-  const uint64_t idx = s->r_count[id->iread] % id->nbufs;
-  s->r_count[id->iread]++;
-  id->cur_open--;
-  id->xfer_count++;
-  if (__atomic_add_fetch(&sync_clear(s)[idx], 1, __ATOMIC_ACQ_REL) == s->n_readers) {
-    __atomic_store_n(&sync_clear(s)[idx], 0, __ATOMIC_RELEASE);
-    if (sem_do(id->semid, SEM_CLEAR, 1, 0) < 0) return -1;
+  const unsigned n = s->n_readers;
+  int order[IPCBUF_READERS], used[IPCBUF_READERS] = {0};
+  for (unsigned k = 0; k < n; k++) { /* reader slots by r_bufs, lowest first */
+    uint64_t best = UINT64_MAX;
+    order[k] = -1;
+    for (unsigned i = 0; i < n; i++)
+      if (!used[i] && (order[k] < 0 || s->r_bufs[i] < best)) best = s->r_bufs[i], order[k] = (int)i;
+    used[order[k]] = 1;
   }
-  return 0;
-}
-
-int ipcbuf_mark_cleared(ipcbuf_t *id) {
-  if (!id || id->state != 3 || id->cur_open < 1) return -1;
-  if (clear_oldest(id) < 0) return -1;
-  /* an empty EOD block taken behind open ones goes once it is the oldest */
-  if (id->eod_pending && id->cur_open == 1) {
-    id->eod_pending = 0;
-    return clear_oldest(id);
+  for (unsigned k = 0; k < n && id->iread < 0; k++) {
+    if (sem_op(id->semid_data[order[k]], SEM_READER_CONN, -1, IPC_NOWAIT | SEM_UNDO) == 0)
+      id->iread = order[k];
+    else if (errno != EAGAIN)
+      break;
   }
+  if (id->iread < 0) {
+    sem_op(id->semid_connect, SEM_READ, 1, SEM_UNDO);
+    return -1;
+  }
+  id->state = s->r_states[id->iread] ? ST_READING : ST_READER;
+  id->xfer = s->r_xfers[id->iread] % IPCBUF_XFERS;
+  id->viewbuf = 0;
   return 0;
 }
 
-int ipcbuf_enable_sod(ipcbuf_t *id, uint64_t start_buf, uint64_t start_byte) {
-  if (!id || !id->sync) return -1;
-  id->sync->sod = 1;
-  id->sync->s_buf = start_buf;
-  id->sync->s_byte = start_byte;
+int ipcbuf_unlock_read(ipcbuf_t *id) {  /* @0x4045f0 */
+  if (!ipcbuf_is_reader(id) || id->iread < 0 || (unsigned)id->iread >= id->sync->n_readers) return -1;
+  if (sem_op(id->semid_data[id->iread], SEM_READER_CONN, 1, SEM_UNDO) < 0) return -1;
+  if (sem_op(id->semid_connect, SEM_READ, 1, SEM_UNDO) < 0) return -1;
+  id->state = ST_VIEWER;
+  id->iread = -1;
+  id->viewbuf = 0;
   return 0;
 }
 
-int ipcbuf_disable_sod(ipcbuf_t *id) {
-  if (!id || !id->sync) return -1;
-  id->sync->sod = 0;
+int ipcbuf_eod(ipcbuf_t *id) { return id && (id->state == ST_RSTOP || id->state == ST_VSTOP); }
+int ipcbuf_sod(ipcbuf_t *id) { return id && (id->state == ST_READING || id->state == ST_WRITING); }
+
+char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {  /* @0x404710 */
+  if (!ipcbuf_is_reader(id) || ipcbuf_eod(id)) return NULL;
+  ipcsync_t *s = id->sync;
+  const int r = id->iread, open = rd_open(id);
+  if (open >= rd_depth(id) || (open && rd_eod_held(id))) return NULL;
+  if (sem_op(id->semid_data[r], SEM_FULL, -1, 0) < 0) return NULL;
+  uint64_t start = 0;
+  if (id->state == ST_READER) { /* first block of a transfer */
+    id->xfer = s->r_xfers[r] % IPCBUF_XFERS;
+    id->state = ST_READING;
+    s->r_states[r] = ST_READING;
+    s->r_bufs[r] = s->s_buf[id->xfer];
+    start = s->s_byte[id->xfer];
+    if (sem_op(id->semid_data[r], SEM_SODACK, 1, 0) < 0) return NULL;
+  }
+  const uint64_t b = s->r_bufs[r] + (uint64_t)open;
+  const int last = s->eod[id->xfer] && s->e_buf[id->xfer] == b;
+  if (bytes) *bytes = (last ? s->e_byte[id->xfer] : s->bufsz) - start;
+  rd_set(id, open + 1, last);
+  return id->buffer[b % s->nbufs] + start;
+}
+
+int ipcbuf_mark_cleared(ipcbuf_t *id) {  /* @0x404b80: the oldest block held */
+  if (!id || id->state != ST_READING) return -1;
+  ipcsync_t *s = id->sync;
+  const int r = id->iread, open = rd_open(id);
+  if (sem_op(id->semid_data[r], SEM_CLEAR, 1, 0) < 0) return -1;
+  if (s->eod[id->xfer] && s->r_bufs[r] == s->e_buf[id->xfer]) { /* end of this transfer */
+    id->state = ST_RSTOP;
+    s->r_states[r] = 0;
+    s->r_xfers[r]++;
+    id->xfer = s->r_xfers[r] % IPCBUF_XFERS;
+    rd_set(id, 0, 0);
+    return sem_op(id->semid_data[r], SEM_EODACK, 1, 0);
+  }
+  s->r_bufs[r]++;
+  rd_set(id, open ? open - 1 : 0, rd_eod_held(id));
   return 0;
 }
 
-int ipcbuf_sod(ipcbuf_t *id) { return id && id->sync ? id->sync->sod : 0; }
-
-int ipcbuf_eod(ipcbuf_t *id) {
-  if (!id || !id->sync || id->iread < 0) return 0;
-  return id->eod_seen;
+int ipcbuf_reset(ipcbuf_t *id) {  /* @0x404ca0, reader half */
+  if (!id || id->state != ST_RSTOP) return -1;
+  id->state = ST_READER;
+  return 0;
 }
 
-uint64_t ipcbuf_get_bufsz(ipcbuf_t *id) { return id ? id->bufsz : 0; }
-uint64_t ipcbuf_get_nbufs(ipcbuf_t *id) { return id ? id->nbufs : 0; }
-uint64_t ipcbuf_get_nreaders(ipcbuf_t *id) { return id && id->sync ? id->sync->n_readers : 0; }
+/* ------------------------------------------------------------------ */
+/* ipcbuf: queries                                                      */
+
+uint64_t ipcbuf_get_bufsz(ipcbuf_t *id) { return id && id->sync ? id->sync->bufsz : 0; }
+uint64_t ipcbuf_get_nbufs(ipcbuf_t *id) { return id && id->sync ? id->sync->nbufs : 0; }
+int ipcbuf_get_nreaders(ipcbuf_t *id) { return id && id->sync ? (int)id->sync->n_readers : 0; }
+uint64_t ipcbuf_get_write_count(ipcbuf_t *id) { return id && id->sync ? id->sync->w_buf : 0; }
+uint64_t ipcbuf_get_write_index(ipcbuf_t *id) {
+  return id && id->sync ? id->sync->w_buf % id->sync->nbufs : 0;
+}
+uint64_t ipcbuf_get_read_count(ipcbuf_t *id) {
+  return id && id->sync ? id->sync->r_bufs[id->iread < 0 ? 0 : id->iread] : 0;
+}
+uint64_t ipcbuf_get_read_count_iread(ipcbuf_t *id, unsigned iread) {
+  return id && id->sync && iread < IPCBUF_READERS ? id->sync->r_bufs[iread] : 0;
+}
+uint64_t ipcbuf_get_read_index(ipcbuf_t *id) {
+  return id && id->sync ? ipcbuf_get_read_count(id) % id->sync->nbufs : 0;
+}
 char *ipcbuf_get_buffer(ipcbuf_t *id, uint64_t i) {
-  return id && id->buffer && i < id->nbufs ? id->buffer[i] : NULL;
+  return id && id->buffer && id->sync && i < id->sync->nbufs ? id->buffer[i] : NULL;
 }
 int ipcbuf_get_device(ipcbuf_t *id) { return id && id->sync ? id->sync->on_device_id : -1; }
 
@@ -405,77 +552,235 @@ int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n) {
   return 0;
 }
 
-uint64_t ipcbuf_get_write_count(ipcbuf_t *id) { return id && id->sync ? id->sync->w_count : 0; }
-uint64_t ipcbuf_get_read_count(ipcbuf_t *id, int iread) {
-  return id && id->sync && iread >= 0 && iread < IPCBUF_READERS ? id->sync->r_count[iread] : 0;
-}
-
 /* ------------------------------------------------------------------ */
 /* ipcio                                                                */
 
-int ipcio_open(ipcio_t *ipc, char rdwrt) {
-  if (!ipc) return -1;
-  ipc->rdwrt = rdwrt;
+static void ipcio_init(ipcio_t *ipc) {  /* @0x4057f0 */
+  ipc->bytes = 0;
+  ipc->rdwrt = 0;
   ipc->curbuf = NULL;
-  ipc->curbufsz = 0;
-  return rdwrt == 'W' ? ipcbuf_lock_write(&ipc->buf) : ipcbuf_lock_read(&ipc->buf);
+  ipc->marked_filled = 0;
+  ipc->sod_pending = 0;
+  ipc->sod_buf = 0;
+  ipc->sod_byte = 0;
 }
 
-int ipcio_close(ipcio_t *ipc) {
-  if (!ipc) return -1;
-  if (ipc->buf.state == 2) return ipcbuf_enable_eod(&ipc->buf);
+int ipcio_connect(ipcio_t *ipc, key_t key) {
+  if (!ipc || ipcbuf_connect(&ipc->buf, key) < 0) return -1;
+  ipcio_init(ipc);
   return 0;
 }
 
-char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id) {
-  if (!ipc) return NULL;
-  char *p = ipcbuf_get_next_write(&ipc->buf);
-  if (p && block_id) *block_id = ipc->buf.cur_index;
-  ipc->curbuf = p;
-  ipc->curbufsz = ipc->buf.bufsz;
-  return p;
+int ipcio_disconnect(ipcio_t *ipc) {
+  if (!ipc || ipcbuf_disconnect(&ipc->buf) < 0) return -1;
+  ipcio_init(ipc);
+  return 0;
 }
 
-int ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes) {
+int ipcio_open(ipcio_t *ipc, char rdwrt) {  /* @0x4059d0 */
   if (!ipc) return -1;
-  ipc->curbuf = NULL;
-  return ipcbuf_mark_filled(&ipc->buf, bytes);
-}
-
-char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id) {
-  if (!ipc) return NULL;
-  uint64_t bytes = 0;
-  char *p = ipcbuf_get_next_read(&ipc->buf, &bytes);
-  if (!p) return NULL;
-  if (bytes == 0 && ipcbuf_eod(&ipc->buf)) { /* empty EOD marker block */
-    if (ipc->buf.cur_open == 1)
-      ipcbuf_mark_cleared(&ipc->buf);
-    else
-      ipc->buf.eod_pending = 1; /* released after the blocks still open */
-    return NULL;
+  if (rdwrt == 'W' || rdwrt == 'w') {
+    ipc->rdwrt = 0;
+    ipc->bytes = 0;
+    ipc->curbuf = NULL;
+    if (ipcbuf_lock_write(&ipc->buf) < 0) return -1;
+    if (rdwrt == 'w' && ipcbuf_disable_sod(&ipc->buf) < 0) return -1;
+  } else if (rdwrt == 'R') {
+    ipc->rdwrt = 0;
+    ipc->bytes = 0;
+    ipc->curbuf = NULL;
+    if (ipcbuf_lock_read(&ipc->buf) < 0) return -1;
+  } else {
+    return -1; /* 'r' (viewer) is not provided */
   }
-  if (curbufsz) *curbufsz = bytes;
-  if (block_id) *block_id = ipc->buf.cur_index;
+  ipc->rdwrt = rdwrt;
+  return 0;
+}
+
+int ipcio_is_open(ipcio_t *ipc) {
+  return ipc && (ipc->rdwrt == 'R' || ipc->rdwrt == 'r' || ipc->rdwrt == 'W' || ipc->rdwrt == 'w');
+}
+
+static int check_pending_sod(ipcio_t *ipc) {  /* @0x405b20 */
+  if (!ipc->sod_pending || ipcbuf_get_write_count(&ipc->buf) <= ipc->sod_buf) return 0;
+  if (ipcbuf_enable_sod(&ipc->buf, ipc->sod_buf, ipc->sod_byte) < 0) return -1;
+  ipc->sod_pending = 0;
+  return 0;
+}
+
+/* ipcio_stop_close (@0x405c10) with close = 1: a writer with a transfer
+ * open ends it -- the block being written, or a 0-byte block after a full
+ * one, carries the end of data -- and unlocks.  Two departures, neither
+ * visible to a reader:
+ *  - the 0-byte block is taken like any other (get_next_write: the
+ *    readers' CLEAR for its slot's last fill first).  libpsrdada marks it
+ *    without that wait, so count[] runs one fill behind and the writer's
+ *    next transfer can reuse a block a slow reader has not cleared yet
+ *    (tests/test_dada.py::test_ring_transfers_property found it);
+ *  - a writer that locked and wrote no block at all ends an empty transfer
+ *    (a 0-byte end-of-data block) where libpsrdada would leave its readers
+ *    waiting for data that never comes. */
+int ipcio_close(ipcio_t *ipc) {
+  if (!ipc) return -1;
+  ipcbuf_t *b = &ipc->buf;
+  if (ipc->rdwrt == 'W') {
+    if (b->state == ST_WCHANGE && !b->sync->w_state && ipcbuf_enable_sod(b, b->sync->w_buf, 0) < 0)
+      return -1;
+    if (ipcbuf_is_writing(b)) {
+      if (!ipc->curbuf && !ipcbuf_get_next_write(b)) return -1;
+      if (ipcbuf_enable_eod(b) < 0 || ipcbuf_mark_filled(b, ipc->bytes) < 0 || check_pending_sod(ipc) < 0)
+        return -1;
+      ipc->marked_filled = 1;
+      if (ipc->bytes == ipcbuf_get_bufsz(&ipc->buf)) ipc->curbuf = NULL;
+    }
+    ipc->rdwrt = 'w';
+  }
+  if (ipc->rdwrt == 'w') {
+    ipcsync_t *s = ipc->buf.sync;
+    if (s->w_xfer) s->w_buf = s->e_buf[(s->w_xfer - 1) % IPCBUF_XFERS] + 1;
+    if (ipcbuf_unlock_write(&ipc->buf) < 0) return -1;
+    ipc->rdwrt = 0;
+    return 0;
+  }
+  if (ipc->rdwrt == 'R') {
+    if (ipcbuf_unlock_read(&ipc->buf) < 0) return -1;
+    ipc->rdwrt = 0;
+    return 0;
+  }
+  return -1;
+}
+
+char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id) {  /* @0x406340 */
+  if (!ipc || ipc->bytes || ipc->curbuf || ipc->rdwrt != 'W') return NULL;
+  ipc->curbuf = ipcbuf_get_next_write(&ipc->buf);
+  if (!ipc->curbuf) return NULL;
+  if (block_id) *block_id = ipcbuf_get_write_index(&ipc->buf);
+  ipc->marked_filled = 0;
+  ipc->bytes = 0;
+  return ipc->curbuf;
+}
+
+ssize_t ipcio_update_block_write(ipcio_t *ipc, uint64_t bytes) {  /* @0x406490 */
+  if (!ipc || ipc->bytes || !ipc->curbuf || ipc->rdwrt != 'W' || bytes > ipcbuf_get_bufsz(&ipc->buf))
+    return -1;
+  ipc->bytes += bytes;
+  return 0;
+}
+
+ssize_t ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes) {  /* @0x406580 */
+  if (ipcio_update_block_write(ipc, bytes) < 0) return -1;
+  if (ipc->marked_filled) return 0;
+  if (ipcbuf_mark_filled(&ipc->buf, ipc->bytes) < 0) return -2;
+  if (check_pending_sod(ipc) < 0) return -3;
+  ipc->marked_filled = 1;
+  ipc->curbuf = NULL;
+  ipc->bytes = 0;
+  return 0;
+}
+
+char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id) {  /* @0x4060b0 */
+  if (!ipc || ipc->bytes || ipc->rdwrt != 'R') return NULL;
+  ipcbuf_t *id = &ipc->buf;
+  if (ipc->curbuf && rd_depth(id) <= 1) return NULL; /* one block at a time (PSRDADA) */
+  if (ipcbuf_eod(id)) return NULL;
+  uint64_t sz = 0;
+  char *p = ipcbuf_get_next_read(id, &sz);
+  if (!p) return NULL;
   ipc->curbuf = p;
-  ipc->curbufsz = bytes;
+  ipc->curbufsz = sz;
+  if (block_id) *block_id = (id->sync->r_bufs[id->iread] + (uint64_t)rd_open(id) - 1) % id->sync->nbufs;
+  if (curbufsz) *curbufsz = sz;
+  ipc->bytes = 0;
   return p;
 }
 
-ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes) {
-  (void)bytes;
-  if (!ipc) return -1;
+/* the block is released once `bytes` add up to its size (PSRDADA); a
+ * reader holding several blocks (read depth > 1) releases the oldest */
+ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes) {  /* @0x406200 */
+  if (!ipc || ipc->rdwrt != 'R' || !ipc->curbuf) return -1;
+  ipcbuf_t *id = &ipc->buf;
+  if (rd_depth(id) > 1) {
+    if (ipcbuf_mark_cleared(id) < 0) return -1;
+    if (!rd_open(id)) ipc->curbuf = NULL;
+    ipc->bytes = 0;
+    return 0;
+  }
+  if (ipc->bytes) return -1;
+  if (bytes != ipc->curbufsz) {
+    ipc->bytes += bytes;
+    if (ipc->bytes != ipc->curbufsz) return 0;
+  }
+  if (ipcbuf_mark_cleared(id) < 0) return -1;
   ipc->curbuf = NULL;
-  return ipcbuf_mark_cleared(&ipc->buf);
+  ipc->bytes = 0;
+  return 0;
+}
+
+/* ipcio_write (@0x405e40): a byte stream over the blocks */
+ssize_t ipcio_write(ipcio_t *ipc, char *ptr, size_t bytes) {
+  if (!ipc || (ipc->rdwrt != 'W' && ipc->rdwrt != 'w')) return -1;
+  const uint64_t bufsz = ipcbuf_get_bufsz(&ipc->buf);
+  size_t left = bytes;
+  while (left) {
+    if (ipc->bytes == bufsz) { /* the current block is full */
+      if (!ipc->marked_filled) {
+        if (ipcbuf_mark_filled(&ipc->buf, ipc->bytes) < 0 || check_pending_sod(ipc) < 0) return -1;
+      }
+      ipc->curbuf = NULL;
+      ipc->bytes = 0;
+      ipc->marked_filled = 1;
+    }
+    if (!ipc->curbuf) {
+      ipc->curbuf = ipcbuf_get_next_write(&ipc->buf);
+      if (!ipc->curbuf) return -1;
+      ipc->marked_filled = 0;
+      ipc->bytes = 0;
+    }
+    uint64_t n = bufsz - ipc->bytes;
+    if (n > left) n = left;
+    if (ipcbuf_copy_in(&ipc->buf, ipc->curbuf + ipc->bytes, ptr, n) < 0) return -1;
+    ipc->bytes += n;
+    ptr += n;
+    left -= n;
+  }
+  return (ssize_t)bytes;
+}
+
+/* ipcio_read (@0x406660): fewer bytes than asked at the end of data */
+ssize_t ipcio_read(ipcio_t *ipc, char *ptr, size_t bytes) {
+  if (!ipc || ipc->rdwrt != 'R') return -1;
+  size_t left = bytes;
+  while (left && !ipcbuf_eod(&ipc->buf)) {
+    if (!ipc->curbuf) {
+      ipc->curbuf = ipcbuf_get_next_read(&ipc->buf, &ipc->curbufsz);
+      if (!ipc->curbuf) return -1;
+      ipc->bytes = 0;
+    }
+    uint64_t n = ipc->curbufsz - ipc->bytes;
+    if (n > left) n = left;
+    if (ptr) {
+      if (ipcbuf_copy_out(&ipc->buf, ptr, ipc->curbuf + ipc->bytes, n) < 0) return -1;
+      ptr += n;
+    }
+    ipc->bytes += n;
+    left -= n;
+    if (ipc->bytes == ipc->curbufsz) {
+      if (ipcbuf_mark_cleared(&ipc->buf) < 0) return -1;
+      ipc->curbuf = NULL;
+      ipc->bytes = 0;
+    }
+  }
+  return (ssize_t)(bytes - left);
 }
 
 /* ------------------------------------------------------------------ */
 /* dada_hdu                                                             */
 
-dada_hdu_t *dada_hdu_create(multilog_t *log) {
+dada_hdu_t *dada_hdu_create(multilog_t *log) {  /* @0x407490 */
   dada_hdu_t *h = calloc(1, sizeof(*h));
   if (!h) return NULL;
   h->log = log;
-  h->data_block_key = 0xdada;  /* PSRDADA default key */
+  h->data_block_key = 0xdada; /* PSRDADA's default key */
   h->header_block_key = 0xdadb;
   return h;
 }
@@ -486,69 +791,70 @@ void dada_hdu_set_key(dada_hdu_t *h, key_t key) {
   h->header_block_key = key + 1; /* header key = key+1 */
 }
 
-int dada_hdu_connect(dada_hdu_t *h) {
-  if (!h) return -1;
-  ipcio_t io = IPCIO_INIT;
-  ipcbuf_t hb = IPCBUF_INIT;
-  h->data_block = malloc(sizeof(ipcio_t));
+int dada_hdu_connect(dada_hdu_t *h) {  /* @0x407500: header ring first */
+  if (!h || h->data_block) return -1;
+  const ipcbuf_t hb = IPCBUF_INIT;
+  const ipcio_t io = IPCIO_INIT;
   h->header_block = malloc(sizeof(ipcbuf_t));
-  if (!h->data_block || !h->header_block) return -1;
-  *h->data_block = io;
-  *h->header_block = hb;
-  if (ipcbuf_connect(&h->data_block->buf, h->data_block_key) < 0) {
-    if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_connect: no data ring at key %x", h->data_block_key);
-    return -1;
-  }
-  if (ipcbuf_connect(h->header_block, h->header_block_key) < 0) {
-    if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_connect: no header ring at key %x", h->header_block_key);
-    ipcbuf_disconnect(&h->data_block->buf);
-    return -1;
-  }
-  return 0;
+  h->data_block = malloc(sizeof(ipcio_t));
+  if (h->header_block) *h->header_block = hb;
+  if (h->data_block) *h->data_block = io;
+  const char *what = NULL;
+  if (!h->header_block || !h->data_block)
+    what = "out of memory";
+  else if (ipcbuf_connect(h->header_block, h->header_block_key) < 0)
+    what = "no header ring at key";
+  else if (ipcio_connect(h->data_block, h->data_block_key) < 0)
+    what = "no data ring at key";
+  if (!what) return 0;
+  if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_connect: %s %x", what, (unsigned)h->data_block_key);
+  if (h->header_block && h->header_block->sync) ipcbuf_disconnect(h->header_block);
+  free(h->header_block);
+  free(h->data_block);
+  h->header_block = NULL;
+  h->data_block = NULL;
+  return -1;
 }
 
 int dada_hdu_disconnect(dada_hdu_t *h) {
-  if (!h) return -1;
-  if (h->data_block) {
-    ipcbuf_disconnect(&h->data_block->buf);
-    free(h->data_block);
-    h->data_block = NULL;
-  }
-  if (h->header_block) {
-    ipcbuf_disconnect(h->header_block);
-    free(h->header_block);
-    h->header_block = NULL;
-  }
+  if (!h || !h->data_block) return -1;
+  ipcio_disconnect(h->data_block);
+  ipcbuf_disconnect(h->header_block);
+  free(h->header_block);
+  free(h->data_block);
+  h->header_block = NULL;
+  h->data_block = NULL;
   return 0;
 }
 
 void dada_hdu_destroy(dada_hdu_t *h) {
   if (!h) return;
-  if (h->data_block || h->header_block) dada_hdu_disconnect(h);
+  if (h->data_block) dada_hdu_disconnect(h);
   free(h->header);
   free(h);
 }
 
-int dada_hdu_lock_write(dada_hdu_t *h) {
+int dada_hdu_lock_write_spec(dada_hdu_t *h, char mode) {  /* @0x407970 */
   if (!h || !h->data_block) return -1;
   if (ipcbuf_lock_write(h->header_block) < 0) return -1;
-  if (ipcio_open(h->data_block, 'W') < 0) {
+  if (ipcio_open(h->data_block, mode) < 0) {
     ipcbuf_unlock_write(h->header_block);
     return -1;
   }
   return 0;
 }
 
-int dada_hdu_unlock_write(dada_hdu_t *h) {
+int dada_hdu_lock_write(dada_hdu_t *h) { return dada_hdu_lock_write_spec(h, 'W'); }
+
+int dada_hdu_unlock_write(dada_hdu_t *h) {  /* @0x407a20 */
   if (!h || !h->data_block) return -1;
-  if (h->data_block->curbuf) ipcio_close_block_write(h->data_block, 0);
-  ipcio_close(h->data_block);
-  ipcbuf_unlock_write(&h->data_block->buf);
-  ipcbuf_unlock_write(h->header_block);
-  return 0;
+  int rc = 0;
+  if (ipcio_is_open(h->data_block) && ipcio_close(h->data_block) < 0) rc = -1;
+  if (ipcbuf_unlock_write(h->header_block) < 0) rc = -1;
+  return rc;
 }
 
-int dada_hdu_lock_read(dada_hdu_t *h) {
+int dada_hdu_lock_read(dada_hdu_t *h) {  /* @0x407810 */
   if (!h || !h->data_block) return -1;
   if (ipcbuf_lock_read(h->header_block) < 0) return -1;
   if (ipcio_open(h->data_block, 'R') < 0) {
@@ -558,66 +864,111 @@ int dada_hdu_lock_read(dada_hdu_t *h) {
   return 0;
 }
 
-int dada_hdu_unlock_read(dada_hdu_t *h) {
+int dada_hdu_unlock_read(dada_hdu_t *h) {  /* @0x4078b0 */
   if (!h || !h->data_block) return -1;
-  ipcbuf_unlock_read(&h->data_block->buf);
-  ipcbuf_unlock_read(h->header_block);
+  int rc = ipcio_is_open(h->data_block) && ipcio_close(h->data_block) < 0 ? -1 : 0;
+  if (h->header) { /* the header block dada_hdu_open took goes back now */
+    free(h->header);
+    h->header = NULL;
+    if (h->header_block->state == ST_READING) ipcbuf_mark_cleared(h->header_block);
+  }
+  if (ipcbuf_unlock_read(h->header_block) < 0) rc = -1;
+  return rc;
+}
+
+/* dada_hdu_open (@0x407bc0): the next header block, empty end-of-data
+ * header blocks skipped; kept (not cleared) until dada_hdu_unlock_read */
+int dada_hdu_open(dada_hdu_t *h) {
+  if (!h || !h->header_block || h->header) return -1;
+  ipcbuf_t *hb = h->header_block;
+  uint64_t size = 0;
+  char *p = NULL;
+  while (!size) {
+    p = ipcbuf_get_next_read(hb, &size);
+    if (!p) {
+      if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_open: could not get next header block");
+      return -1;
+    }
+    if (!size) {
+      if (hb->state == ST_READING) ipcbuf_mark_cleared(hb);
+      if (!ipcbuf_eod(hb)) {
+        if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_open: empty header block");
+        return -1;
+      }
+      ipcbuf_reset(hb);
+    }
+  }
+  size = ipcbuf_get_bufsz(hb);
+  uint64_t hdr_size = 0;
+  if (ascii_header_get(p, "HDR_SIZE", "%" SCNu64, &hdr_size) != 1 || hdr_size == 0) hdr_size = size;
+  if (hdr_size > size) {
+    if (h->log) multilog(h->log, LOG_ERR, "dada_hdu_open: HDR_SIZE %" PRIu64 " > block %" PRIu64,
+                         hdr_size, size);
+    return -1;
+  }
+  h->header = malloc(hdr_size + 1);
+  if (!h->header) return -1;
+  memcpy(h->header, p, hdr_size);
+  h->header[hdr_size] = 0;
+  h->header_size = hdr_size;
   return 0;
 }
 
-int dada_hdu_open_read(dada_hdu_t *h) {
-  if (!h || !h->header_block) return -1;
-  uint64_t bytes = 0;
-  char *p = ipcbuf_get_next_read(h->header_block, &bytes);
-  if (!p) return -1;
-  uint64_t hsz = ipcbuf_get_bufsz(h->header_block);
-  if (!h->header) {
-    h->header = calloc(1, hsz + 1);
-    if (!h->header) return -1;
-  }
-  h->header_size = hsz;
-  memcpy(h->header, p, bytes < hsz ? bytes : hsz);
-  h->header[hsz] = 0;
-  return ipcbuf_mark_cleared(h->header_block);
-}
+int dada_hdu_open_read(dada_hdu_t *h) { return dada_hdu_open(h); }
+
+/* ------------------------------------------------------------------ */
+/* ring pairs (the dada_db tool)                                        */
 
 int dada_db_create(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers, uint64_t hdr_nbufs,
                    uint64_t hdr_bufsz) {
   return dada_db_create_work(key, nbufs, bufsz, n_readers, hdr_nbufs, hdr_bufsz, -1);
 }
 
-/* the creator does not attach: a device ring's blocks are opened only by
+/* the creator does not open a device ring's blocks: they are opened only by
  * the processes that use them */
 int dada_db_create_work(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_readers,
                         uint64_t hdr_nbufs, uint64_t hdr_bufsz, int device_id) {
-  if (ring_create(key, nbufs, bufsz, n_readers, device_id) < 0) return -1;
-  if (ring_create(key + 1, hdr_nbufs, hdr_bufsz, n_readers, -1) < 0) {
+  ipcbuf_t d, hb;
+  if (ring_create(&d, key, nbufs, bufsz, n_readers, device_id < 0 ? -1 : device_id, 0) < 0) return -1;
+  ipcbuf_disconnect(&d);
+  if (ring_create(&hb, key + 1, hdr_nbufs, hdr_bufsz, n_readers, -1, 1) < 0) {
     const int e = errno;
     dada_db_destroy(key);
     errno = e;
     return -1;
   }
+  ipcbuf_disconnect(&hb);
   return 0;
 }
 
-/* removes one ring without attaching its blocks (a device ring's holder is
+/* removes one ring without opening its blocks (a device ring's holder is
  * stopped instead) */
 static int ring_remove(key_t key) {
-  int syncid = shmget(key, 0, 0);
-  if (syncid < 0) return -1;
-  ipcsync_t *s = shmat(syncid, NULL, 0);
-  if (s == (void *)-1) return -1;
+  ipcbuf_t id = IPCBUF_INIT;
+  if (sync_get(&id, key, 0, 0) < 0) return -1;
+  ipcsync_t *s = id.sync;
   int rc = 0;
-  if (s->magic == SYNC_MAGIC && s->version == SYNC_VERSION) {
-    if (s->on_device_id >= 0) rc = dev_stop_holder(s);
-    for (uint64_t i = 0; i < s->nbufs; i++)
-      if (sync_shmids(s)[i] >= 0) shmctl(sync_shmids(s)[i], IPC_RMID, NULL);
-    semctl(s->semid, 0, IPC_RMID);
-  } else {
-    rc = -1;
+  if (s->semkey_connect == 0) rc = -1; /* not a (complete) ring */
+  if (s->on_device_id >= 0) {
+    const int sid = shmget(shmkey_get(&id, 0), 0, 0);
+    void *seg0 = sid >= 0 ? shmat(sid, NULL, 0) : (void *)-1;
+    if (seg0 != (void *)-1) {
+      if (dev_stop_holder(seg0) < 0) rc = -1;
+      shmdt(seg0);
+    }
   }
+  for (uint64_t i = 0; i < s->nbufs; i++) {
+    const int sid = shmget(shmkey_get(&id, i), 0, 0);
+    if (sid >= 0) shmctl(sid, IPC_RMID, NULL);
+  }
+  for (unsigned r = 0; r < s->n_readers && r < IPCBUF_READERS; r++) {
+    const int sem = semget(s->semkey_data[r], 0, 0);
+    if (sem >= 0) semctl(sem, 0, IPC_RMID);
+  }
+  const int sem = semget(key_connect(key), 0, 0);
+  if (sem >= 0) semctl(sem, 0, IPC_RMID);
   shmdt(s);
-  shmctl(syncid, IPC_RMID, NULL);
+  shmctl(id.syncid, IPC_RMID, NULL);
   return rc;
 }
 
@@ -626,12 +977,12 @@ int dada_db_destroy(key_t key) {
   return a == 0 && b == 0 ? 0 : -1;
 }
 
-int fileread(const char *filename, char *buffer, unsigned bufsz) {
+long fileread(const char *filename, char *buffer, unsigned bufsz) {
   if (!filename || !buffer || !bufsz) return -1;
   FILE *fp = fopen(filename, "r");
   if (!fp) return -1;
   memset(buffer, 0, bufsz);
   size_t n = fread(buffer, 1, bufsz - 1, fp);
   fclose(fp);
-  return (int)n;
+  return (long)n;
 }

@@ -312,7 +312,9 @@ static void *worker(void *arg) {
   for (;;) {
     uint64_t bytes = 0;
     char *blk = g_stop ? NULL : next_block(s->in, &bytes);
-    sh->have[w->r] = !blk ? -1 : (bytes == s->rbufsz ? 1 : 0);
+    /* a 0-byte block only carries the end of data (PSRDADA's ipcio_close
+     * after a full block): it ends the loop like a NULL one */
+    sh->have[w->r] = !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
     pthread_barrier_wait(&sh->bar); /* all sub-bands agree on this round */
     int stop = sh->failed, skip = 0;
     for (int r = 0; r < sh->nsub; r++) {
@@ -416,9 +418,11 @@ static void run_device_pipelined(shared_t *sh) {
         if (write_output(sh, SPEC(written)) < 0) sh->failed = 1;
       if (blk) {
         ipcio_close_block_read(in, bytes);
-        sh->nskipped++;
-        multilog(sh->log, LOG_INFO, "partial integration skipped (a block held %" PRIu64 " of %" PRIu64
-                 " B)", bytes, s->rbufsz);
+        if (bytes) { /* a 0-byte block only carries the end of data */
+          sh->nskipped++;
+          multilog(sh->log, LOG_INFO, "partial integration skipped (a block held %" PRIu64 " of %" PRIu64
+                   " B)", bytes, s->rbufsz);
+        }
       }
       if (!blk || sh->failed) break;
       continue;
@@ -465,7 +469,7 @@ static void *worker_split(void *arg) {
       sh->blk_bytes = 0;
       sh->blk = g_stop ? NULL : next_block(s0->in, &sh->blk_bytes);
       pin_block(s0, sh->blk, sh->log);
-      sh->have[0] = !sh->blk ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
+      sh->have[0] = !sh->blk || !sh->blk_bytes ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
     }
     pthread_barrier_wait(&sh->bar);
     if (sh->have[0] <= 0 || sh->failed) {

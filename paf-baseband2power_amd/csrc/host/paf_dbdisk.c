@@ -77,7 +77,7 @@ int main(int argc, char **argv) {
     if (bytes && fwrite(stage ? stage : b, 1, bytes, fp) != bytes) rc = EXIT_FAILURE;
     ipcio_close_block_read(hdu->data_block, bytes);
     total += bytes;
-    nblk++;
+    if (bytes) nblk++; /* a 0-byte block only carries the end of data */
   }
   free(stage);
   fclose(fp);

@@ -58,6 +58,8 @@ def dlib():
         L.ipcbuf_eod.argtypes = [P]
         L.ipcbuf_enable_eod.argtypes = [P]
         L.ipcbuf_get_write_count.restype = C.c_uint64
+        L.ipcbuf_get_read_count.restype = C.c_uint64
+        L.ipcbuf_get_read_count.argtypes = [P]
         L.ipcbuf_get_write_count.argtypes = [P]
         L.ipcbuf_get_device.argtypes = [P]
         L.ipcbuf_set_read_depth.argtypes = [P, C.c_int]
@@ -148,6 +150,7 @@ class Hdu:
     def __init__(self, key: int, mode: str):
         L = dlib()
         self.mode = mode
+        self._held, self._eod_held = 0, False  # read depth > 1: blocks held, EOD block behind them
         self.h = L.dada_hdu_create(None)
         L.dada_hdu_set_key(self.h, key)
         if L.dada_hdu_connect(self.h) != 0:
@@ -196,11 +199,16 @@ class Hdu:
         return C.string_at(s.header)
 
     def read_block(self):
-        """bytes of the next block, or None at end of data"""
+        """bytes of the next block, or None at end of data (the 0-byte block
+        PSRDADA's ipcio_close appends after a full one is taken and released
+        here: it only carries the end of data)"""
         L = dlib()
         n, bid = C.c_uint64(), C.c_uint64()
         p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
         if not p:
+            return None
+        if not n.value:
+            L.ipcio_close_block_read(self.data, 0)
             return None
         buf = C.create_string_buffer(n.value)
         if n.value and L.ipcbuf_copy_out(self.data, buf, p, n.value) != 0:
@@ -216,8 +224,9 @@ class Hdu:
         p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
         if not p:
             return None
-        if not n.value:
-            return np.empty(0, dtype=np.uint8)
+        if not n.value:  # the end-of-data block
+            L.ipcio_close_block_read(self.data, 0)
+            return None
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n.value,))
 
     def release_block(self, nbytes: int) -> None:
@@ -228,23 +237,38 @@ class Hdu:
         """hold up to `depth` blocks at once (extension, include/b2p_dada.h)"""
         if dlib().ipcbuf_set_read_depth(self.data, depth) != 0:
             raise ValueError(f"read depth {depth}")
+        self._held, self._eod_held = 0, False
 
     def open_block(self):
-        """(bytes of the next block, its length) without releasing it, or None
-        at end of data; release with close_block (oldest first)"""
+        """bytes of the next block, kept held, or None at end of data;
+        release with close_block (oldest first).  A 0-byte end-of-data block
+        is not returned: it goes back to the ring after the blocks before it"""
         L = dlib()
         n, bid = C.c_uint64(), C.c_uint64()
         p = L.ipcio_open_block_read(self.data, C.byref(n), C.byref(bid))
         if not p:
             return None
+        if not n.value:
+            if self._held:
+                self._eod_held = True
+            elif L.ipcio_close_block_read(self.data, 0) != 0:
+                raise OSError("close_block_read")
+            return None
         buf = C.create_string_buffer(n.value)
-        if n.value and L.ipcbuf_copy_out(self.data, buf, p, n.value) != 0:
+        if L.ipcbuf_copy_out(self.data, buf, p, n.value) != 0:
             raise OSError("copy out of block")
+        self._held += 1
         return buf.raw
 
     def close_block(self) -> None:
-        if dlib().ipcio_close_block_read(self.data, 0) != 0:
+        L = dlib()
+        if L.ipcio_close_block_read(self.data, 0) != 0:
             raise OSError("close_block_read")
+        self._held -= 1
+        if self._eod_held and not self._held:
+            self._eod_held = False
+            if L.ipcio_close_block_read(self.data, 0) != 0:
+                raise OSError("close_block_read")
 
     def eod(self) -> bool:
         return bool(dlib().ipcbuf_eod(self.data))

@@ -32,13 +32,16 @@ NCHAN        336                    # number of channels here
 """
 
 _key_lock = threading.Lock()
-_next_key = [0x5a00 + (os.getpid() % 64) * 16]
+_key_base = 0x1000 + (os.getpid() % 48) * 0x100  # one window of 128 keys per test process
+_next_key = [0]
 
 
 def fresh_key() -> int:
+    """a ring key of this process's own window (xdist workers never share
+    one: destroying "leftovers" must not remove another worker's live ring)"""
     with _key_lock:
-        k = _next_key[0]
-        _next_key[0] += 2
+        k = _key_base + 2 * (_next_key[0] % 128)
+        _next_key[0] += 1
     dada.destroy_ring(k)  # leftovers of an aborted run
     return k
 
@@ -222,12 +225,25 @@ def test_two_readers_each_see_every_block(ring):
 
 
 def test_single_writer_lock(ring):
+    """one writer at a time: a second lock_write waits for the first writer's
+    unlock (PSRDADA's WRITE semaphore, ipcbuf_lock_write @0x403b00)"""
     k = ring(2, 512)
-    with dada.Hdu(k, "W"):
-        with pytest.raises(OSError):
-            dada.Hdu(k, "W")
-    with dada.Hdu(k, "W"):  # released by close
-        pass
+    events = []
+    w1 = dada.Hdu(k, "W")
+
+    def second():
+        with dada.Hdu(k, "W"):
+            events.append("second locked")
+
+    t = threading.Thread(target=second)
+    t.start()
+    t.join(0.5)
+    assert t.is_alive() and not events  # waiting on the lock
+    events.append("first unlocks")
+    w1.close()
+    t.join(30)
+    assert not t.is_alive()
+    assert events == ["first unlocks", "second locked"]
 
 
 def test_connect_missing_ring_fails():
