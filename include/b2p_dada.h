@@ -191,7 +191,8 @@ int dada_db_destroy(key_t key);
 
 /* ---- ASCII header (ascii_header_set at capture.c:758-778) ---- */
 /* returns the number of items scanned (>= 1), or -1 if the key is absent */
-int ascii_header_get(const char *header, const char *keyword, const char *format, void *result);
+int ascii_header_get(const char *header, const char *keyword, const char *format, ...)
+    __attribute__((format(scanf, 3, 4)));
 /* replaces the value of an existing key or appends "KEY value"; 0 / -1 */
 int ascii_header_set(char *header, const char *keyword, const char *format, ...)
     __attribute__((format(printf, 3, 4)));

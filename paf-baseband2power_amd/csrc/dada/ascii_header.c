@@ -26,8 +26,8 @@ static const char *find_key(const char *header, const char *keyword) {
   return NULL;
 }
 
-int ascii_header_get(const char *header, const char *keyword, const char *format, void *result) {
-  if (!header || !keyword || !format || !result) return -1;
+int ascii_header_get(const char *header, const char *keyword, const char *format, ...) {
+  if (!header || !keyword || !format) return -1;
   const char *line = find_key(header, keyword);
   if (!line) return -1;
   const char *v = line;
@@ -40,7 +40,10 @@ int ascii_header_get(const char *header, const char *keyword, const char *format
   if (n >= sizeof val) n = sizeof val - 1;
   memcpy(val, v, n);
   val[n] = 0;
-  int rc = sscanf(val, format, result);
+  va_list ap;
+  va_start(ap, format);
+  int rc = vsscanf(val, format, ap);
+  va_end(ap);
   return rc >= 1 ? rc : -1;
 }
 

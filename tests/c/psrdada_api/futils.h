@@ -2,5 +2,5 @@
 #ifndef __FUTILS_H
 #define __FUTILS_H
 #include <stdint.h>
-int fileread(const char *filename, char *buffer, unsigned bufsz);
+long fileread(const char *filename, char *buffer, unsigned bufsz);
 #endif

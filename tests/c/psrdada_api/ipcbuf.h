@@ -1,5 +1,5 @@
 /* declarations only -- see README.txt.  ipcbuf_t as laid out in the
- * reference's libpsrdada. */
+ * reference's libpsrdada (its DWARF: tests/golden/psrdada_abi.json, 104 B). */
 #ifndef __DADA_IPCBUF_H
 #define __DADA_IPCBUF_H
 #include <stdint.h>
@@ -14,9 +14,9 @@ typedef struct {
   ipcsync_t *sync;
   char **buffer;
   void **shm_addr;
-  uint64_t *count;
+  char *count;
   key_t *shmkey;
-  int viewbuf;
+  uint64_t viewbuf;
   uint64_t xfer;
   uint64_t soclock_buf;
   int iread;

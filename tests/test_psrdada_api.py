@@ -41,12 +41,13 @@ def undefined(obj):
     return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
 
 
-# Return types Appendix A does not pin (INTEGRATION.md "PSRDADA API assumed"):
-# the alternative header set swaps each between int and a wider signed type.
+# The stand-ins' return types are the DWARF's (tests/test_psrdada_abi.py); the
+# alternative header set swaps each return type the hosts consume between int
+# and a wider signed type, so the hosts depend on none of them beyond "< 0".
 ALTERNATIVES = {
     "ipcio.h": [("ssize_t ipcio_close_block_read(", "int ipcio_close_block_read("),
-                ("int ipcio_close_block_write(", "ssize_t ipcio_close_block_write(")],
-    "futils.h": [("int fileread(", "int64_t fileread(")],
+                ("ssize_t ipcio_close_block_write(", "int ipcio_close_block_write(")],
+    "futils.h": [("long fileread(", "int fileread(")],
     "ipcbuf.h": [("int ipcbuf_mark_filled(", "ssize_t ipcbuf_mark_filled("),
                  ("int ipcbuf_mark_cleared(", "ssize_t ipcbuf_mark_cleared("),
                  ("int ipcbuf_eod(", "long ipcbuf_eod(")],
