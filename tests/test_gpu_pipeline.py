@@ -181,3 +181,73 @@ def test_stage_stops_cleanly_on_sigterm(gpu, tmp_path):
                 p.wait()
         dada.destroy_ring(kin)
         dada.destroy_ring(kout)
+
+
+def test_stage_between_psrdada_neighbours(gpu, tmp_path):
+    """The drop-in on the wire: paf_baseband2power (libpafdada) between
+    PSRDADA processes -- its input ring written, and its output ring drained,
+    by tests/psrdada_model.py, the independent statement of the reference's
+    libpsrdada protocol.  Two integrations and a short
+    block; spectra equal the oracle, the header carries the stage's keys."""
+    import subprocess
+    import threading
+
+    import psrdada_model as pm
+
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 14)
+    kin, kout = 0x6f40 + (os.getpid() % 16) * 4, 0x6fc0 + (os.getpid() % 16) * 4
+    for k in (kin, kout):
+        dada.destroy_ring(k)
+    dada.create_ring(kin, 3, g.block_bytes)
+    dada.create_ring(kout, 4, g.nout * 4)
+    blocks = [co.fill_synthetic(g, g.block_bytes, SEED, 8, k) for k in range(2)]
+    got = {}
+
+    def drain():  # a PSRDADA reader on the output ring (dada_dbdisk's role)
+        hdr, data = pm.Ring(kout + 1), pm.Ring(kout)
+        try:
+            hdr.lock_read()
+            data.lock_read()
+            p, n = hdr.get_next_read()
+            got["header"] = pm.C.string_at(p, n).split(b"\0")[0].decode()
+            hdr.mark_cleared()
+            got["spectra"] = data.read_transfer()
+            data.unlock_read()
+            hdr.unlock_read()
+        finally:
+            hdr.close()
+            data.close()
+
+    reader = threading.Thread(target=drain)
+    reader.start()
+    stage = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_baseband2power"), "-a", f"{kin:x}",
+                              "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0"],
+                             stderr=subprocess.PIPE, text=True)
+    hdr, data = pm.Ring(kin + 1), pm.Ring(kin)
+    try:  # a PSRDADA writer on the input ring (paf_diskdb / capture's role)
+        hdr.lock_write()
+        data.lock_write()
+        hdr.write_block(pm.header_block(hdr, b"HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\n"
+                                             b"NCHAN 256\nTSAMP 0.84375\n"))
+        for b in blocks:
+            data.write_block(b.tobytes())
+        data.write_block(b"\1" * 999)  # a short block ends the transfer (skipped by the stage)
+        data.unlock_write()
+        hdr.unlock_write()
+        assert stage.wait(120) == 0, stage.stderr.read()
+        reader.join(60)
+        assert not reader.is_alive()
+    finally:
+        hdr.close()
+        data.close()
+        if stage.poll() is None:
+            stage.kill()
+            stage.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+    assert len(got["spectra"]) == 2
+    for k in range(2):
+        sp = np.frombuffer(got["spectra"][k], dtype=np.float32)
+        assert np.array_equal(sp.view(np.uint32), co.power(g, blocks[k]).view(np.uint32))
+    assert dada.header_get(got["header"], "NBIT", "%d") == 32
+    assert dada.header_get(got["header"], "NCHAN", "%d") == 256
