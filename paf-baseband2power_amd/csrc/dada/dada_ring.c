@@ -147,6 +147,11 @@ static int sync_get(ipcbuf_t *id, key_t key, uint64_t nbufs, int flag) {
   return 0;
 }
 
+static size_t seg_size(int shmid) {
+  struct shmid_ds ds;
+  return shmctl(shmid, IPC_STAT, &ds) == 0 ? ds.shm_segsz : 0;
+}
+
 /* ipcbuf_get (@0x403090): the semaphore sets and the blocks; kc is the
  * connect set's key (semkey_connect, published last by a creator) */
 static int ring_get(ipcbuf_t *id, key_t kc, int flag) {
@@ -171,6 +176,10 @@ static int ring_get(ipcbuf_t *id, key_t kc, int flag) {
     const size_t sz = !dev ? s->bufsz : (flag & IPC_CREAT) ? (i ? DEV_HANDLE_BYTES : sizeof(dev_seg_t)) : 0;
     id->shmid[i] = shmget(shmkey_get(id, i), sz, flag);
     if (id->shmid[i] < 0) return -1;
+    if (dev && i == 0 && !(flag & IPC_CREAT) && seg_size(id->shmid[0]) < sizeof(dev_seg_t)) {
+      errno = ENODEV; /* a device ring without a libpafdada holder (e.g. PSRDADA's CUDA one) */
+      return -1;
+    }
     void *p = shmat(id->shmid[i], NULL, 0);
     if (p == (void *)-1) return -1;
     id->shm_addr[i] = p;
@@ -951,7 +960,7 @@ static int ring_remove(key_t key) {
   if (s->semkey_connect == 0) rc = -1; /* not a (complete) ring */
   if (s->on_device_id >= 0) {
     const int sid = shmget(shmkey_get(&id, 0), 0, 0);
-    void *seg0 = sid >= 0 ? shmat(sid, NULL, 0) : (void *)-1;
+    void *seg0 = sid >= 0 && seg_size(sid) >= sizeof(dev_seg_t) ? shmat(sid, NULL, 0) : (void *)-1;
     if (seg0 != (void *)-1) {
       if (dev_stop_holder(seg0) < 0) rc = -1;
       shmdt(seg0);

@@ -355,3 +355,15 @@ def test_transfers_alternate_between_libraries(ring):
     t.join(60)
     assert not t.is_alive()
     assert got == [(f"XFER {i}".encode(), want[i]) for i in range(3)]
+
+
+def test_foreign_device_ring_is_refused(ring):
+    """a PSRDADA device ring made by libpsrdada (64-B CUDA handle segments,
+    no libpafdada holder) is refused cleanly, not read past its segments"""
+    k = ring(2, 64)                      # block segments of a CUDA-handle's size
+    r = pm.Ring(k)
+    r.s.set("on_device_id", 0)           # as libpsrdada's dada_db -g would leave it
+    r.close()
+    with pytest.raises(OSError):
+        dada.Hdu(k, "R")
+    assert dada.destroy_ring(k) or True  # removal does not touch the absent holder
