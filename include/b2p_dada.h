@@ -93,6 +93,9 @@ int ipcbuf_enable_eod(ipcbuf_t *id); /* the next mark_filled ends the transfer *
 int ipcbuf_eod(ipcbuf_t *id);        /* 1 once this reader has cleared its transfer's EOD block */
 int ipcbuf_sod(ipcbuf_t *id);
 int ipcbuf_reset(ipcbuf_t *id);      /* reader at EOD: ready for the next transfer */
+int ipcbuf_lock(ipcbuf_t *id);       /* pin the segments in RAM (SHM_LOCK; dada_db -l) */
+int ipcbuf_unlock(ipcbuf_t *id);
+int ipcbuf_page(ipcbuf_t *id);       /* zero every host block (dada_db -p) */
 char ipcbuf_is_writer(ipcbuf_t *id);
 char ipcbuf_is_writing(ipcbuf_t *id);
 char ipcbuf_is_reader(ipcbuf_t *id);

@@ -561,6 +561,27 @@ int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n) {
   return 0;
 }
 
+/* ipcbuf_lock / _unlock (@0x405050 / @0x405100): pin the sync segment and
+ * every host block in RAM (shmctl SHM_LOCK), as dada_db -l does */
+static int lock_segments(ipcbuf_t *id, int cmd) {
+  if (!id || !id->sync || id->syncid < 0 || !id->shmid) return -1;
+  if (shmctl(id->syncid, cmd, NULL) < 0) return -1;
+  for (uint64_t i = 0; id->sync->on_device_id < 0 && i < id->sync->nbufs; i++)
+    if (shmctl(id->shmid[i], cmd, NULL) < 0) return -1;
+  return 0;
+}
+
+int ipcbuf_lock(ipcbuf_t *id) { return lock_segments(id, SHM_LOCK); }
+int ipcbuf_unlock(ipcbuf_t *id) { return lock_segments(id, SHM_UNLOCK); }
+
+/* ipcbuf_page (@0x4051b0): touch (zero) every block so its pages exist */
+int ipcbuf_page(ipcbuf_t *id) {
+  if (!id || !id->sync || !id->buffer) return -1;
+  if (id->sync->on_device_id >= 0) return 0; /* device blocks are zeroed by their holder */
+  for (uint64_t i = 0; i < id->sync->nbufs; i++) memset(id->buffer[i], 0, id->sync->bufsz);
+  return 0;
+}
+
 /* ------------------------------------------------------------------ */
 /* ipcio                                                                */
 

@@ -256,6 +256,12 @@ def test_dada_db_tool_create_destroy():
     k = fresh_key()
     r = subprocess.run([f"{BIN}/dada_db", "-k", f"{k:x}", "-b", "8192", "-n", "4", "-r", "1",
                         "-l", "-p"], capture_output=True, text=True)
+    if r.returncode != 0:  # -l needs CAP_IPC_LOCK or RLIMIT_MEMLOCK room: refused cleanly
+        assert "cannot lock the ring in RAM" in r.stderr
+        with pytest.raises(OSError):
+            dada.Hdu(k, "W")
+        r = subprocess.run([f"{BIN}/dada_db", "-k", f"{k:x}", "-b", "8192", "-n", "4", "-r", "1", "-p"],
+                           capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     with dada.Hdu(k, "W") as w:
         assert w.bufsz == 8192
