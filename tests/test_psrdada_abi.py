@@ -367,3 +367,49 @@ def test_foreign_device_ring_is_refused(ring):
     with pytest.raises(OSError):
         dada.Hdu(k, "R")
     assert dada.destroy_ring(k)           # removed without touching an absent holder
+
+
+def test_two_readers_one_from_each_library(ring):
+    """a 2-reader ring: one libpafdada reader and one PSRDADA reader (the
+    model) each take every block of the transfer libpafdada writes; the
+    writer waits for both (CLEAR of every reader, get_next_write @0x403f20)"""
+    k = ring(2, 2048, nreaders=2)
+    rng = np.random.default_rng(10)
+    want = [rng.integers(0, 256, 2048, dtype=np.uint8).tobytes() for _ in range(7)] + [b"t" * 5]
+    got = {}
+
+    def ours():
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            blocks = []
+            while (b := r.read_block()) is not None:
+                blocks.append(b)
+            got["libpafdada"] = blocks
+
+    def model():
+        hdr, data = pm.Ring(k + 1), pm.Ring(k)
+        try:
+            hdr.lock_read()
+            data.lock_read()
+            hdr.get_next_read()
+            hdr.mark_cleared()
+            got["psrdada"] = data.read_transfer()
+            got["slot"] = data.iread
+            data.unlock_read()
+            hdr.unlock_read()
+        finally:
+            hdr.close()
+            data.close()
+
+    ts = [threading.Thread(target=ours), threading.Thread(target=model)]
+    for t in ts:
+        t.start()
+    with dada.Hdu(k, "W") as w:
+        w.write_header("HDR_SIZE 4096\n")
+        for b in want:
+            w.write_block(b)
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts)
+    assert got["libpafdada"] == want and got["psrdada"] == want
+    assert got["slot"] in (0, 1)
