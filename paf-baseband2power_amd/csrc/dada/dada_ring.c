@@ -975,7 +975,21 @@ int dada_db_create_work(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_re
  * stopped instead) */
 static int ring_remove(key_t key) {
   ipcbuf_t id = IPCBUF_INIT;
-  if (sync_get(&id, key, 0, 0) < 0) return -1;
+  if (sync_get(&id, key, 0, 0) < 0) {
+    /* no sync segment: remove what a creation that died half-way may have
+     * left at the ring's keys (semaphores, blocks 0, 1, ... while present),
+     * so the key can be used again; still "nothing to destroy" */
+    for (int r = -1; r < IPCBUF_READERS; r++) {
+      const int sem = semget(r < 0 ? key_connect(key) : key_data(key, r), 0, 0);
+      if (sem >= 0) semctl(sem, 0, IPC_RMID);
+    }
+    for (uint64_t i = 0; i < 0x7fff; i++) {
+      const int sid = shmget(key_block(key, i), 0, 0);
+      if (sid < 0) break;
+      shmctl(sid, IPC_RMID, NULL);
+    }
+    return -1;
+  }
   ipcsync_t *s = id.sync;
   int rc = 0;
   if (s->semkey_connect == 0) rc = -1; /* not a (complete) ring */

@@ -413,3 +413,16 @@ def test_two_readers_one_from_each_library(ring):
     assert not any(t.is_alive() for t in ts)
     assert got["libpafdada"] == want and got["psrdada"] == want
     assert got["slot"] in (0, 1)
+
+
+def test_destroy_cleans_a_half_built_ring(ring):
+    """a ring whose creator died after the semaphores and blocks but before
+    the sync segment was complete (here: the sync segment removed) leaves
+    no object behind dada_db -d, so its key can be used again"""
+    k = ring(3, 4096)
+    sid = pm._libc.shmget(k, 0, 0)
+    pm._libc.shmctl(sid, pm.IPC_RMID, None)   # only the sync segment goes
+    assert not dada.destroy_ring(k)           # nothing complete to destroy ...
+    assert pm._libc.semget(k + 0x10000, 0, 0) < 0
+    assert all(pm._libc.shmget(k + 0x10000 * (10 + i), 0, 0) < 0 for i in range(3))
+    dada.create_ring(k, 3, 4096)              # ... and the key is free again
