@@ -251,3 +251,37 @@ def test_stage_between_psrdada_neighbours(gpu, tmp_path):
         assert np.array_equal(sp.view(np.uint32), co.power(g, blocks[k]).view(np.uint32))
     assert dada.header_get(got["header"], "NBIT", "%d") == 32
     assert dada.header_get(got["header"], "NCHAN", "%d") == 256
+
+
+def test_stage_on_an_empty_transfer(gpu, tmp_path):
+    """a writer that locks, writes the header and no block (libpafdada ends
+    such a transfer with one 0-byte end-of-data block): the stage writes its
+    output header, no spectrum, ends its output transfer and exits 0"""
+    import subprocess
+
+    kin, kout = 0x6e80 + (os.getpid() % 16) * 4, 0x6ec0 + (os.getpid() % 16) * 4
+    for k in (kin, kout):
+        dada.destroy_ring(k)
+    dada.create_ring(kin, 2, 1 << 24)
+    dada.create_ring(kout, 2, 256 * 4)
+    out = tmp_path / "power.dada"
+    try:
+        sink = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                stderr=subprocess.PIPE, text=True)
+        stage = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_baseband2power"), "-a", f"{kin:x}",
+                                  "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0"],
+                                 stderr=subprocess.PIPE, text=True)
+        with dada.Hdu(kin, "W") as w:
+            w.write_header("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\nTSAMP 0.84375\n")
+        assert stage.wait(120) == 0, stage.stderr.read()
+        assert sink.wait(60) == 0, sink.stderr.read()
+        hdr, data = dada.read_dada_file(str(out))
+        assert data.size == 0 and dada.header_get(hdr, "NBIT", "%d") == 32
+        assert "FINISH PAF_PROCESS: 0 integrations" in (tmp_path / "paf_baseband2power.log").read_text()
+    finally:
+        for p in (locals().get("stage"), locals().get("sink")):
+            if p is not None and p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
