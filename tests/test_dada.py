@@ -172,7 +172,8 @@ def test_ring_full_last_block_then_empty_eod(ring):
 
 
 def test_ring_carries_several_transfers(ring):
-    """EOD is marked per block: a second transfer on the same ring is read in
+    """End of data is kept per transfer (e_buf / e_byte / eod of transfer
+    x % 8, PSRDADA): a second transfer on the same ring is read in
     full after the first one's EOD, and a reader that is behind stops at the
     first transfer's (empty or short) EOD block instead of reading it as data
     (PSRDADA rings carry one transfer after another)"""
@@ -433,7 +434,7 @@ def test_ring_transfers_property(ring):
     """Random transfers through a small ring with a concurrent reader: each
     transfer's blocks arrive in order and unchanged, its end is a short,
     empty or (at unlock_write) appended empty block, and the next transfer
-    follows after unlock_read + lock_read (per-block EOD marks)"""
+    follows after unlock_read + lock_read (end of data per transfer: e_buf / e_byte)"""
     from hypothesis import HealthCheck, given, settings
     from hypothesis import strategies as st
 
