@@ -638,6 +638,30 @@ static int check_pending_sod(ipcio_t *ipc) {  /* @0x405b20 */
   return 0;
 }
 
+/* The slot of the 0-byte end-of-data block ipcio_close marks: taken as
+ * get_next_write takes one (every reader's CLEAR for its last fill), but
+ * waiting at most EOD_WAIT_S per reader, so a writer whose readers have gone
+ * still ends its transfer -- then without the wait, as libpsrdada always
+ * does (CLEARs taken in this round are given back first). */
+#define EOD_WAIT_S 60
+static int take_eod_slot(ipcbuf_t *id) {
+  ipcsync_t *s = id->sync;
+  const uint64_t b = s->w_buf % s->nbufs;
+  while (id->count[b]) {
+    for (unsigned r = 0; r < s->n_readers; r++) {
+      struct sembuf sb = {SEM_CLEAR, -1, 0};
+      struct timespec t = {EOD_WAIT_S, 0};
+      while (semtimedop(id->semid_data[r], &sb, 1, &t) != 0) {
+        if (errno == EINTR && !g_interrupt) continue;
+        for (unsigned q = 0; q < r; q++) sem_op(id->semid_data[q], SEM_CLEAR, 1, 0);
+        return errno == EAGAIN ? 0 : -1; /* EAGAIN: timed out */
+      }
+    }
+    id->count[b]--;
+  }
+  return 0;
+}
+
 /* ipcio_stop_close (@0x405c10) with close = 1: a writer with a transfer
  * open ends it -- the block being written, or a 0-byte block after a full
  * one, carries the end of data -- and unlocks.  Two departures, neither
@@ -657,7 +681,7 @@ int ipcio_close(ipcio_t *ipc) {
     if (b->state == ST_WCHANGE && !b->sync->w_state && ipcbuf_enable_sod(b, b->sync->w_buf, 0) < 0)
       return -1;
     if (ipcbuf_is_writing(b)) {
-      if (!ipc->curbuf && !ipcbuf_get_next_write(b)) return -1;
+      if (!ipc->curbuf && take_eod_slot(b) < 0) return -1;
       if (ipcbuf_enable_eod(b) < 0 || ipcbuf_mark_filled(b, ipc->bytes) < 0 || check_pending_sod(ipc) < 0)
         return -1;
       ipc->marked_filled = 1;
