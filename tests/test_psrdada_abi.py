@@ -426,3 +426,82 @@ def test_destroy_cleans_a_half_built_ring(ring):
     assert pm._libc.semget(k + 0x10000, 0, 0) < 0
     assert all(pm._libc.shmget(k + 0x10000 * (10 + i), 0, 0) < 0 for i in range(3))
     dada.create_ring(k, 3, 4096)              # ... and the key is free again
+
+
+def test_mixed_library_transfers_property(ring):
+    """Random transfers (more than the 8 in-flight transfer slots, so xfer
+    indices wrap), each written by libpafdada or by the PSRDADA model and
+    then read by libpafdada or by the model: every transfer arrives whole
+    and in order, and the shared counters agree with the protocol"""
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+
+    xfer = st.tuples(st.sampled_from(["paf", "model"]), st.sampled_from(["paf", "model"]),
+                     st.integers(0, 3), st.sampled_from(["short", "full"]), st.integers(1, 255))
+
+    @settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+    @given(xfers=st.lists(xfer, min_size=1, max_size=12), nbufs=st.integers(4, 6),
+           seed=st.integers(0, 1 << 30))
+    def check(xfers, nbufs, seed):
+        bufsz = 256
+        k = ring(nbufs, bufsz)
+        rng = np.random.default_rng(seed)
+        nblocks = 0
+        for t, (wlib, rlib, nfull, end, short) in enumerate(xfers):
+            blocks = [rng.integers(0, 256, bufsz, dtype=np.uint8).tobytes() for _ in range(nfull)]
+            if end == "short":
+                blocks.append(rng.integers(0, 256, short, dtype=np.uint8).tobytes())
+            head = f"XFER {t}\n".encode()
+            if wlib == "paf":
+                with dada.Hdu(k, "W") as w:
+                    w.write_header(head)
+                    for b in blocks:
+                        w.write_block(b)
+            else:
+                hdr, data = pm.Ring(k + 1), pm.Ring(k)
+                hdr.lock_write()
+                data.lock_write()
+                hdr.write_block(pm.header_block(hdr, head))
+                for b in blocks:
+                    data.write_block(b)
+                if end == "full":
+                    if blocks:
+                        data.end_transfer()
+                    else:  # libpsrdada writes nothing for an empty transfer: end it explicitly
+                        data.get_next_write()
+                        data.mark_filled(0)
+                data.unlock_write()
+                hdr.unlock_write()
+                hdr.close()
+                data.close()
+            nblocks += len(blocks) + (end == "full")
+            if rlib == "paf":
+                with dada.Hdu(k, "R") as r:
+                    h = r.read_header()
+                    got = []
+                    while (b := r.read_block()) is not None:
+                        got.append(b)
+                    assert r.eod()
+            else:
+                hdr, data = pm.Ring(k + 1), pm.Ring(k)
+                hdr.lock_read()
+                data.lock_read()
+                p, n = hdr.get_next_read()
+                h = pm.C.string_at(p, n)
+                hdr.mark_cleared()
+                got = data.read_transfer()
+                data.unlock_read()
+                hdr.unlock_read()
+                hdr.close()
+                data.close()
+            assert h.split(b"\0")[0] == head and got == blocks, (t, wlib, rlib)
+        r = pm.Ring(k)
+        try:
+            assert (r.s.get("w_buf"), r.s.get("w_xfer"), r.s.get("r_xfers", 0)) == \
+                (nblocks, len(xfers), len(xfers))
+            assert [pm.semval(r.semid_data[0], i) for i in (0, 1, 2)] == [8, 8, 0]  # SODACK EODACK FULL
+        finally:
+            r.close()
+        dada.destroy_ring(k)
+
+    check()
