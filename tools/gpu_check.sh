@@ -5,7 +5,7 @@
 #   usage: tools/gpu_check.sh [steps...]
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
-#          probe skew overlap spikes patterns h2d diskdb idlerep keeprep tune tunebmf capturemt multi
+#          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -101,6 +101,7 @@ for s in $STEPS; do
               -- python3 bench.py --steps 200 --warmup 5 --cpu-seconds 0 ;;
     h2d) run h2d_probe 300 paf-baseband2power_amd/bin/h2d_probe ;;
     patterns) run read_patterns 300 paf-baseband2power_amd/bin/read_pattern_probe 40 ;;
+    asmprobe) run asmprobe 300 paf-baseband2power_amd/bin/assemble_probe 10 ;;
     diskdb) run bench_diskdb 600 python3 tools/bench_diskdb.py --nint 8 --threads 16 ;;
     capture) run bench_capture 600 python3 tools/bench_capture.py ;;
     capturemt) run bench_capture_mt 900 python3 tools/bench_capture.py --rates 3200,4800,6400,8000 \
