@@ -313,12 +313,26 @@ int main(int argc, char **argv) {
   const char *hfile = NULL, *ip = "0.0.0.0", *mapping = "ip", *ofile = NULL, *ocfile = NULL,
              *logdir = NULL, *efile = NULL;
   uint64_t rbuf_ndf = 8192, nblocks = 0, ref_idf = 0, ref_sec = 0;
-  int have_ref = 0, have_freq = 0, nrx_req = 0;
+  int have_ref = 0, have_freq = 0, nrx_req = 0, sod = -1;
   double length = 0, idle_s = 2.0, freq = 0;
   while ((arg = getopt(argc, argv, "a:b:c:d:f:g:i:j:k:I:P:N:R:m:x:s:n:t:o:O:Zh")) != -1) {
     switch (arg) {
       case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
-      case 'b': case 'd': break; /* sod / record-header flags: accepted (paf_capture.c:75-85) */
+      case 'b': /* start of data (paf_capture.c:75-77, capture.c:622-639) */
+        if (sscanf(optarg, "%d", &sod) != 1) {
+          fprintf(stderr, "paf_capture: -b takes 0 or 1, not %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        break;
+      case 'd': { /* record headers (paf_capture.c:83-85, capture.c:216,222) */
+        int hdr = 0;
+        if (sscanf(optarg, "%d", &hdr) != 1 || hdr != 0) {
+          fprintf(stderr, "paf_capture: -d %s: only payload-only blocks (-d 0) are recorded; the "
+                          "stage integrates TFTFP payload, not frames with their headers\n", optarg);
+          return EXIT_FAILURE;
+        }
+        break;
+      }
       case 'c': rbuf_ndf = strtoull(optarg, NULL, 10); break;
       case 'f': hfile = optarg; break;
       case 'g': efile = optarg; break;
@@ -345,7 +359,7 @@ int main(int argc, char **argv) {
       case 'Z': nozero = 1; break;
       default:
         fprintf(stdout,
-                "paf_capture -a key -f header [-g epoch_file] [-i freq] [-c rbuf_ndf] [-j seconds | -n blocks]\n"
+                "paf_capture -a key -f header [-g epoch_file] [-i freq] [-b sod] [-d 0] [-c rbuf_ndf] [-j seconds | -n blocks]\n"
                 "            [-I ip] [-P port0] [-N nports] [-R rx_threads] [-m ip|freq:F0] [-x ref_idf -s ref_sec]\n"
                 "            [-t idle_s] [-k dir] [-Z]\n"
                 "paf_capture -o frames.df -O chunks.u8 [-I ip] [-P port0] [-N nports] [-m ...] [-t idle_s]\n");
@@ -442,6 +456,16 @@ int main(int argc, char **argv) {
     }
     locked = 1;
     ipcbuf_t *db = &c.hdu->data_block->buf;
+    /* -b 1: the readers see data from the first block written (the
+     * reference's enable_sod(db, 0, 0), which assumes a fresh ring, as
+     * enable_sod at the ring's next block); -b 0: blocks are written with the
+     * start of data disabled, invisible to readers (capture.c:633); no -b:
+     * the start of data is the first block written (PSRDADA's default) */
+    if ((sod == 1 && ipcbuf_enable_sod(db, ipcbuf_get_write_count(db), 0) < 0) ||
+        (sod == 0 && ipcbuf_disable_sod(db) < 0)) {
+      multilog(c.log, LOG_ERR, "Can not write data before start (capture.c:626)");
+      goto done;
+    }
     if (ipcbuf_get_device(db) < 0) {
       multilog(c.log, LOG_ERR, "ring %x is not GPU-resident (dada_db -g)", (unsigned)key);
       goto done;

@@ -128,3 +128,15 @@ def test_capture_refuses_bad_freq(tmp_path):
     r = subprocess.run([os.path.join(BIN, "paf_capture"), "-a", "7e00", "-f", str(hdr), "-i", "abc"],
                        capture_output=True, text=True, timeout=30)
     assert r.returncode == 1 and "-i takes" in r.stderr
+
+
+@pytest.mark.parametrize("args,msg", [(["-d", "1"], "only payload-only blocks"),
+                                      (["-b", "on"], "-b takes 0 or 1")])
+def test_capture_refuses_unsupported_record_flags(tmp_path, args, msg):
+    """-d 1 (frames recorded with their headers, capture.c:216,222) is refused
+    rather than ignored, and -b (start of data) must be 0 or 1"""
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text("HDR_SIZE 4096\n")
+    r = subprocess.run([os.path.join(BIN, "paf_capture"), "-a", "7e00", "-f", str(hdr)] + args,
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and msg in r.stderr

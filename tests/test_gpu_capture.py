@@ -68,7 +68,7 @@ def test_udp_capture_to_spectra(gpu, tmp_path, inject):
                  subprocess.Popen([os.path.join(BIN, "paf_capture"), "-a", f"{kin:x}", "-f", str(hdr),
                                    "-c", str(block_ndf), "-n", str(nblk), "-P", str(port), "-N", "3",
                                    "-m", "freq:1300", "-x", "249990", "-s", "54", "-t", "1",
-                                   "-g", str(efile), "-i", "1340.5"],
+                                   "-g", str(efile), "-i", "1340.5", "-b", "1", "-d", "0"],
                                   stderr=subprocess.PIPE, text=True)]
         time.sleep(3)  # capture opens its context and binds before the sender starts
         snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-P",
