@@ -4,27 +4,36 @@
  * :94-95).  Attaches as a reader, waits for the header, writes
  * "<dir>/<UTC_START>_<OBS_OFFSET>.000000.dada" = 4096-B header + every data
  * block until end of data.
- *   -k key   -D dir   -b cpu (accepted, ignored)   -W (accepted: overwrite)
+ *   -k key   -D dir   -b core (bind to that CPU core)   -W (overwrite an
+ *   existing file; without it an existing file is an error, as in
+ *   dada_dbdisk)   -s (single transfer: the only mode here -- the sink
+ *   exits after the first end of data, where dada_dbdisk without -s waits
+ *   for the next transfer)
  *   -o file  explicit output path (instead of the DADA naming rule)
  */
+#include <errno.h>
+#include <fcntl.h>
 #include <getopt.h>
+#include <sched.h>
 #include <inttypes.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <unistd.h>
 
 #include "b2p_dada.h"
 
 static void usage(void) {
   fprintf(stdout,
           "paf_dbdisk - write a DADA ring buffer to a file\n"
-          "Usage: paf_dbdisk -k key -D dir [-o file] [-W] [-b cpu]\n");
+          "Usage: paf_dbdisk -k key -D dir [-o file] [-W] [-b core] [-s]\n");
 }
 
 int main(int argc, char **argv) {
   key_t key = 0xdada;
   char dir[512] = ".", ofile[1024] = "";
-  int arg;
+  int arg, overwrite = 0, core = -1;
   while ((arg = getopt(argc, argv, "k:D:o:b:Wsh")) != -1) {
     switch (arg) {
       case 'k':
@@ -35,12 +44,30 @@ int main(int argc, char **argv) {
         break;
       case 'D': snprintf(dir, sizeof dir, "%s", optarg); break;
       case 'o': snprintf(ofile, sizeof ofile, "%s", optarg); break;
-      case 'b': case 'W': case 's': break;
+      case 'b':
+        if (sscanf(optarg, "%d", &core) != 1 || core < 0) {
+          fprintf(stderr, "paf_dbdisk: -b takes a CPU core number, not %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        break;
+      case 'W': overwrite = 1; break;
+      case 's': break; /* single transfer: always */
       default: usage(); return EXIT_FAILURE;
     }
   }
+  if (ofile[0] && !overwrite && access(ofile, F_OK) == 0) { /* an explicit name: refused up front */
+    fprintf(stderr, "paf_dbdisk: %s exists; -W overwrites\n", ofile);
+    return EXIT_FAILURE;
+  }
   multilog_t *log = multilog_open("paf_dbdisk", 0);
   multilog_add(log, stderr);
+  if (core >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(core, &set);
+    if (sched_setaffinity(0, sizeof set, &set) < 0)
+      multilog(log, LOG_WARNING, "cannot bind to core %d (%s); running unbound", core, strerror(errno));
+  }
   dada_hdu_t *hdu = dada_hdu_create(log);
   dada_hdu_set_key(hdu, key);
   if (dada_hdu_connect(hdu) < 0 || dada_hdu_lock_read(hdu) < 0) {
@@ -58,9 +85,11 @@ int main(int argc, char **argv) {
     ascii_header_get(hdu->header, "OBS_OFFSET", "%" SCNu64, &off);
     snprintf(ofile, sizeof ofile, "%s/%s_%016" PRIu64 ".000000.dada", dir, utc, off);
   }
-  FILE *fp = fopen(ofile, "wb");
+  const int fd = open(ofile, O_WRONLY | O_CREAT | (overwrite ? O_TRUNC : O_EXCL), 0644);
+  FILE *fp = fd >= 0 ? fdopen(fd, "wb") : NULL;
   if (!fp) {
-    fprintf(stderr, "paf_dbdisk: cannot open %s\n", ofile);
+    fprintf(stderr, "paf_dbdisk: cannot open %s (%s)%s\n", ofile, strerror(errno),
+            errno == EEXIST ? "; -W overwrites" : "");
     return EXIT_FAILURE;
   }
   int rc = EXIT_SUCCESS;

@@ -482,3 +482,24 @@ def test_ring_transfers_property(ring):
         dada.destroy_ring(k)
 
     check()
+
+
+def test_dbdisk_overwrites_only_with_W(tmp_path, ring):
+    """as dada_dbdisk: an existing output file is an error unless -W is given"""
+    out = tmp_path / "o.dada"
+    out.write_bytes(b"old")
+    for flags, want_rc in (([], 1), (["-W", "-b", "0"], 0)):
+        k = ring(2, 1024)
+        sink = subprocess.Popen([f"{BIN}/paf_dbdisk", "-k", f"{k:x}", "-o", str(out)] + flags,
+                                stderr=subprocess.PIPE, text=True)
+        if want_rc == 0:
+            with dada.Hdu(k, "W") as w:
+                w.write_header(TEMPLATE)
+                w.write_block(b"\5" * 1024)
+        rc = sink.wait(30)
+        err = sink.stderr.read()
+        assert rc == want_rc, err
+        if want_rc:
+            assert "-W overwrites" in err and out.read_bytes() == b"old"
+    h, data = dada.read_dada_file(str(out))
+    assert h.decode() == TEMPLATE and data.tobytes() == b"\5" * 1024
