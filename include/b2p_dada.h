@@ -41,12 +41,20 @@ int multilog_add(multilog_t *log, FILE *fptr);
 int multilog(multilog_t *log, int priority, const char *format, ...)
     __attribute__((format(printf, 3, 4)));
 int multilog_close(multilog_t *log);
+/* one "[date-time] ERR: message" line to a stream, as multilog writes it */
+int multilog_fprintf(FILE *stream, int priority, const char *format, ...)
+    __attribute__((format(printf, 3, 4)));
+
+/* ---- SysV helpers (ipcutil) ---- */
+void *ipc_alloc(key_t key, size_t size, int flag, int *shmid); /* shmget + shmat, NULL on error */
+int ipc_semop(int semid, short int num, short int op, short int flag); /* one semop, 0 / -1 */
 
 /* ---- ipcbuf: one ring of shared-memory blocks ---- */
 typedef struct ipcsync ipcsync_t; /* the shared sync segment (dada_internal.h) */
 typedef struct {                  /* PSRDADA's ipcbuf_t, 104 B */
   int state;                      /* DISCON 0, VIEWER 1, WRITER 2, WRITING 3, WCHANGE 4,
-                                     READER 5, READING 6, RSTOP 7 (end of data) */
+                                     READER 5, READING 6, RSTOP 7 (end of data),
+                                     VIEWING 8, VSTOP 9 */
   int syncid;
   int semid_connect;
   int *semid_data;
@@ -72,13 +80,20 @@ int ipcbuf_create_work(ipcbuf_t *id, key_t key, uint64_t nbufs, uint64_t bufsz,
 int ipcbuf_connect(ipcbuf_t *id, key_t key);
 int ipcbuf_disconnect(ipcbuf_t *id);
 int ipcbuf_destroy(ipcbuf_t *id);
+/* the semaphore sets and blocks of a ring whose sync segment is attached
+ * (a step of ipcbuf_connect; n_readers is not used) */
+int ipcbuf_get(ipcbuf_t *id, int flag, int n_readers);
 int ipcbuf_lock_write(ipcbuf_t *id);  /* waits for the writer lock */
 int ipcbuf_unlock_write(ipcbuf_t *id);
 int ipcbuf_lock_read(ipcbuf_t *id);   /* waits for a free reader slot */
 int ipcbuf_unlock_read(ipcbuf_t *id);
 char *ipcbuf_get_next_write(ipcbuf_t *id);
 int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes);
+/* a reader takes its next block; a viewer (ipcio_open 'r') is given the
+ * next block the writer fills, without taking it */
 char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes);
+char *ipcbuf_get_next_read_work(ipcbuf_t *id, uint64_t *bytes, int flag); /* flag: semop flags */
+char *ipcbuf_get_next_readable(ipcbuf_t *id, uint64_t *bytes);
 int ipcbuf_mark_cleared(ipcbuf_t *id); /* releases the OLDEST block this reader holds */
 /* Extension (not in PSRDADA): let a reader hold up to `depth` blocks at once,
  * so a GPU consumer can launch on block k+1 before block k's kernel has
@@ -92,7 +107,11 @@ int ipcbuf_disable_sod(ipcbuf_t *id);
 int ipcbuf_enable_eod(ipcbuf_t *id); /* the next mark_filled ends the transfer */
 int ipcbuf_eod(ipcbuf_t *id);        /* 1 once this reader has cleared its transfer's EOD block */
 int ipcbuf_sod(ipcbuf_t *id);
-int ipcbuf_reset(ipcbuf_t *id);      /* reader at EOD: ready for the next transfer */
+/* reader at EOD: ready for the next transfer.  writer: once every block is
+ * cleared and every transfer acknowledged, the ring is as created */
+int ipcbuf_reset(ipcbuf_t *id);
+int ipcbuf_hard_reset(ipcbuf_t *id); /* the same, without waiting for anyone */
+int ipcbuf_zero_next_write(ipcbuf_t *id); /* writer: zero the block after this one once free */
 int ipcbuf_lock(ipcbuf_t *id);       /* pin the segments in RAM (SHM_LOCK; dada_db -l) */
 int ipcbuf_unlock(ipcbuf_t *id);
 int ipcbuf_page(ipcbuf_t *id);       /* zero every host block (dada_db -p) */
@@ -107,6 +126,26 @@ uint64_t ipcbuf_get_write_index(ipcbuf_t *id);
 uint64_t ipcbuf_get_read_count(ipcbuf_t *id);  /* this reader's (slot 0's) blocks cleared */
 uint64_t ipcbuf_get_read_count_iread(ipcbuf_t *id, unsigned iread);
 uint64_t ipcbuf_get_read_index(ipcbuf_t *id);
+/* semaphore counts of reader iread (iread < 0: see dada_query.c) */
+uint64_t ipcbuf_get_nfull(ipcbuf_t *id);   /* blocks filled, not yet taken */
+uint64_t ipcbuf_get_nfull_iread(ipcbuf_t *id, int iread);
+uint64_t ipcbuf_get_nclear(ipcbuf_t *id);  /* blocks cleared, not yet reused */
+uint64_t ipcbuf_get_nclear_iread(ipcbuf_t *id, int iread);
+uint64_t ipcbuf_get_sodack(ipcbuf_t *id);
+uint64_t ipcbuf_get_sodack_iread(ipcbuf_t *id, int iread);
+uint64_t ipcbuf_get_eodack(ipcbuf_t *id);
+uint64_t ipcbuf_get_eodack_iread(ipcbuf_t *id, int iread);
+int ipcbuf_get_reader_conn(ipcbuf_t *id);
+int ipcbuf_get_reader_conn_iread(ipcbuf_t *id, int iread);
+int ipcbuf_get_read_semaphore_count(ipcbuf_t *id); /* free reader slots */
+/* byte positions in this process's transfer */
+uint64_t ipcbuf_tell(ipcbuf_t *id, uint64_t bufnum);
+int64_t ipcbuf_tell_write(ipcbuf_t *id);
+int64_t ipcbuf_tell_read(ipcbuf_t *id);
+uint64_t ipcbuf_get_write_byte_xfer(ipcbuf_t *id);
+uint64_t ipcbuf_get_write_count_xfer(ipcbuf_t *id);
+uint64_t ipcbuf_get_sod_minbuf(ipcbuf_t *id);  /* earliest block a start of data may name */
+uint64_t ipcbuf_set_soclock_buf(ipcbuf_t *id); /* = the block after the last transfer's end */
 /* address of block i (for device registration; PSRDADA's
  * dada_cuda_dbregister walks the same list) -- extension */
 char *ipcbuf_get_buffer(ipcbuf_t *id, uint64_t i);
@@ -133,7 +172,7 @@ typedef struct { /* PSRDADA's ipcio_t, 152 B */
   char *curbuf;
   uint64_t curbufsz;
   uint64_t bytes;
-  char rdwrt; /* 'R', 'W', 'w' (writer, start of data deferred) or 0 */
+  char rdwrt; /* 'R', 'r' (viewer), 'W', 'w' (writer, start of data deferred) or 0 */
   char marked_filled;
   char sod_pending;
   uint64_t sod_buf;
@@ -141,11 +180,28 @@ typedef struct { /* PSRDADA's ipcio_t, 152 B */
 } ipcio_t;
 #define IPCIO_INIT {IPCBUF_INIT, NULL, 0, 0, 0, 0, 0, 0, 0}
 
+void ipcio_init(ipcio_t *ipc);
+int ipcio_create(ipcio_t *ipc, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned num_read);
+int ipcio_create_work(ipcio_t *ipc, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned num_read,
+                      int device_id);
+int ipcio_destroy(ipcio_t *ipc);
 int ipcio_connect(ipcio_t *ipc, key_t key);
 int ipcio_disconnect(ipcio_t *ipc);
+/* 'W' writer, 'w' writer with the start of data deferred, 'R' reader, 'r' viewer */
 int ipcio_open(ipcio_t *ipc, char rdwrt);
 int ipcio_is_open(ipcio_t *ipc);
-int ipcio_close(ipcio_t *ipc); /* writer: ends the open transfer (EOD) */
+int ipcio_close(ipcio_t *ipc); /* writer: ends the open transfer (EOD) and unlocks */
+int ipcio_stop(ipcio_t *ipc);  /* writer: ends the open transfer, keeps the lock ('w') */
+int ipcio_stop_close(ipcio_t *ipc, char unlock);
+int ipcio_start(ipcio_t *ipc, uint64_t byte); /* 'w' writer: a transfer from stream byte `byte` */
+int ipcio_check_pending_sod(ipcio_t *ipc);
+uint64_t ipcio_tell(ipcio_t *ipc);
+int64_t ipcio_seek(ipcio_t *ipc, int64_t offset, int whence);
+int64_t ipcio_space_left(ipcio_t *ipc);
+float ipcio_percent_full(ipcio_t *ipc); /* nfull / nbufs */
+uint64_t ipcio_get_soclock_byte(ipcio_t *ipc);
+uint64_t ipcio_get_start_minimum(ipcio_t *ipc);
+int ipcio_zero_next_block(ipcio_t *ipc);
 char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id);
 ssize_t ipcio_update_block_write(ipcio_t *ipc, uint64_t bytes);
 ssize_t ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes);
@@ -173,6 +229,7 @@ int dada_hdu_connect(dada_hdu_t *hdu);
 int dada_hdu_disconnect(dada_hdu_t *hdu);
 void dada_hdu_destroy(dada_hdu_t *hdu);
 int dada_hdu_lock_write(dada_hdu_t *hdu);
+int dada_hdu_lock_write_spec(dada_hdu_t *hdu, char writemode); /* 'W', or 'w' (ipcio_start later) */
 int dada_hdu_unlock_write(dada_hdu_t *hdu);
 int dada_hdu_lock_read(dada_hdu_t *hdu);
 int dada_hdu_unlock_read(dada_hdu_t *hdu); /* releases the header block dada_hdu_open took */
@@ -180,6 +237,10 @@ int dada_hdu_unlock_read(dada_hdu_t *hdu); /* releases the header block dada_hdu
  * (PSRDADA's dada_hdu_open; dada_hdu_open_read is the same call) */
 int dada_hdu_open(dada_hdu_t *hdu);
 int dada_hdu_open_read(dada_hdu_t *hdu);
+int dada_hdu_open_view(dada_hdu_t *hdu);  /* view the data ring (ipcio 'r') */
+int dada_hdu_close_view(dada_hdu_t *hdu);
+char **dada_hdu_db_addresses(dada_hdu_t *hdu, uint64_t *nbufs, uint64_t *bufsz);
+char **dada_hdu_hb_addresses(dada_hdu_t *hdu, uint64_t *nbufs, uint64_t *bufsz);
 
 /* ring creation / removal (the dada_db tool, paf-baseband2power.py:114-115,
  * :129-130).  Header ring: hdr_nbufs blocks of hdr_bufsz bytes. */
@@ -200,6 +261,9 @@ int ascii_header_get(const char *header, const char *keyword, const char *format
 int ascii_header_set(char *header, const char *keyword, const char *format, ...)
     __attribute__((format(printf, 3, 4)));
 int ascii_header_del(char *header, const char *keyword);
+char *ascii_header_find(const char *header, const char *keyword); /* the keyword, or NULL */
+size_t ascii_header_get_size(char *filename); /* HDR_SIZE of a DADA file, (size_t)-1 on error */
+size_t ascii_header_get_size_fd(int fd);
 
 /* read up to bufsz bytes of a file into buffer, NUL-terminated (futils) */
 long fileread(const char *filename, char *buffer, unsigned bufsz); /* bytes read, -1 on error */

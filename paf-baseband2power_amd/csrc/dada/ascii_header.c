@@ -3,10 +3,13 @@
  * header_baseband2power.txt:1-45), get/set as used at capture.c:758-778.
  * A key matches only at the start of a line and only as a whole word.
  */
+#include <fcntl.h>
+#include <inttypes.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "b2p_dada.h"
 
@@ -102,4 +105,57 @@ int ascii_header_del(char *header, const char *keyword) {
   else
     *line = 0;
   return 0;
+}
+
+/* ascii_header_find (@0x4081e0): the keyword itself, where it starts the
+ * header or follows a newline (or a backslash) and is followed by a blank;
+ * NULL if absent.  As PSRDADA's, an occurrence at the very start of the
+ * header is taken without looking at what follows it. */
+char *ascii_header_find(const char *header, const char *keyword) {
+  if (!header || !keyword || !*keyword) return NULL;
+  const size_t kl = strlen(keyword);
+  const char *k = strstr(header, keyword);
+  while (k && k > header) {
+    if ((k[-1] == '\n' || k[-1] == '\\') && (k[kl] == '\t' || k[kl] == ' ')) break;
+    k = strstr(k + 1, keyword);
+  }
+  return (char *)k;
+}
+
+/* HDR_SIZE of the header at the start of an open file: one page read from
+ * offset 0, the file offset put back to 0 (@0x408660); (size_t)-1 if the
+ * page cannot be read or holds no HDR_SIZE */
+size_t ascii_header_get_size_fd(int fd) {
+  const long page = sysconf(_SC_PAGESIZE);
+  size_t hdr_size = (size_t)-1;
+  char *buf = page > 0 ? malloc((size_t)page + 1) : NULL;
+  if (!buf) {
+    fprintf(stderr, "ascii_header_get_size: failed to allocate %ld bytes\n", page + 1);
+    return hdr_size;
+  }
+  lseek(fd, 0, SEEK_SET);
+  if (read(fd, buf, (size_t)page) != (ssize_t)page) {
+    fprintf(stderr, "ascii_header_get_size: failed to read %ld bytes from file\n", page);
+  } else {
+    buf[page] = 0;
+    uint64_t v;
+    if (ascii_header_get(buf, "HDR_SIZE", "%" SCNu64, &v) == 1)
+      hdr_size = (size_t)v;
+    else
+      fprintf(stderr, "ascii_header_get_size: failed to read HDR_SIZE from header\n");
+  }
+  lseek(fd, 0, SEEK_SET);
+  free(buf);
+  return hdr_size;
+}
+
+size_t ascii_header_get_size(char *filename) {  /* @0x408790 */
+  const int fd = filename ? open(filename, O_RDONLY) : -1;
+  if (fd < 0) {
+    fprintf(stderr, "ascii_header_get_size: failed to open %s for reading\n", filename ? filename : "(null)");
+    return (size_t)-1;
+  }
+  const size_t n = ascii_header_get_size_fd(fd);
+  close(fd);
+  return n;
 }

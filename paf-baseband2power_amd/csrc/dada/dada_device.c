@@ -246,3 +246,10 @@ int dev_copy(void *dst, const void *src, uint64_t n) {
   if (hip_load() < 0) return -1;
   return hip.memcpy_(dst, src, n, 4 /* hipMemcpyDefault */) == 0 ? 0 : -1;
 }
+
+/* zero n bytes of a device block, finished on return (ipc_zero_buffer_cuda) */
+int dev_zero(void *dst, uint64_t n) {
+  if (!n) return 0;
+  if (hip_load() < 0) return -1;
+  return hip.memset_(dst, 0, n) == 0 && hip.sync() == 0 ? 0 : -1;
+}

@@ -99,5 +99,6 @@ int dev_stop_holder(dev_seg_t *seg0);
 int dev_open_blocks(ipcbuf_t *id);
 void dev_close_blocks(ipcbuf_t *id);
 int dev_copy(void *dst, const void *src, uint64_t n); /* hipMemcpyDefault */
+int dev_zero(void *dst, uint64_t n);                  /* hipMemset, synchronised */
 
 #endif

@@ -61,6 +61,29 @@ static int sem_op(int semid, int num, int op, int flags) {
   }
 }
 
+/* the exported one: a single semop, 0 or -1 */
+int ipc_semop(int semid, short num, short op, short flag) {
+  struct sembuf sb = {(unsigned short)num, op, flag};
+  return semop(semid, &sb, 1) < 0 ? -1 : 0;
+}
+
+/* ipc_alloc (@0x408800): attach (creating with IPC_CREAT in flag) a segment */
+void *ipc_alloc(key_t key, size_t size, int flag, int *shmid) {
+  const int id = shmget(key, size, flag);
+  if (id < 0) {
+    fprintf(stderr, "ipc_alloc: shmget (key=%x, size=%zu, flag=%x) %s\n", (unsigned)key, size, (unsigned)flag,
+            strerror(errno));
+    return NULL;
+  }
+  void *p = shmat(id, NULL, 0);
+  if (p == (void *)-1) {
+    fprintf(stderr, "ipc_alloc: shmat (shmid=%d) %s\n", id, strerror(errno));
+    return NULL;
+  }
+  if (shmid) *shmid = id;
+  return p;
+}
+
 /* ------------------------------------------------------------------ */
 /* multilog                                                            */
 
@@ -86,6 +109,20 @@ int multilog_add(multilog_t *m, FILE *fptr) {
   return 0;
 }
 
+/* one line as multilog (@0x402ad0) writes it: "[%Y-%m-%d-%H:%M:%S] ", "ERR: "
+ * for LOG_ERR or "WARN: " for LOG_WARNING, the message.  Departure: a
+ * message without a trailing newline gets one */
+static int log_line(FILE *fp, int priority, const char *msg) {
+  char ts[64];
+  time_t now = time(NULL);
+  struct tm tmv;
+  strftime(ts, sizeof ts, "%Y-%m-%d-%H:%M:%S", localtime_r(&now, &tmv));
+  const char *tag = priority == LOG_ERR ? "ERR: " : priority == LOG_WARNING ? "WARN: " : "";
+  const int rc = fprintf(fp, "[%s] %s%s%s", ts, tag, msg, (msg[0] && msg[strlen(msg) - 1] == '\n') ? "" : "\n");
+  fflush(fp);
+  return rc < 0 ? -1 : 0;
+}
+
 int multilog(multilog_t *m, int priority, const char *format, ...) {
   if (!m) return -1;
   char msg[1024];
@@ -93,16 +130,20 @@ int multilog(multilog_t *m, int priority, const char *format, ...) {
   va_start(ap, format);
   vsnprintf(msg, sizeof msg, format, ap);
   va_end(ap);
-  char ts[64];
-  time_t now = time(NULL);
-  struct tm tmv;
-  strftime(ts, sizeof ts, "%Y-%m-%d-%H:%M:%S", localtime_r(&now, &tmv));
-  for (int i = 0; i < m->nfp; i++) {
-    fprintf(m->fp[i], "[%s] %s%s%s", ts, priority <= LOG_ERR ? "ERR " : "", msg,
-            (msg[0] && msg[strlen(msg) - 1] == '\n') ? "" : "\n");
-    fflush(m->fp[i]);
-  }
+  for (int i = 0; i < m->nfp; i++) log_line(m->fp[i], priority, msg);
   if (m->use_syslog) syslog(priority, "%s", msg);
+  return 0;
+}
+
+/* multilog_fprintf (@0x402dd0): the same line to one stream */
+int multilog_fprintf(FILE *stream, int priority, const char *format, ...) {
+  if (!stream) return -1;
+  char msg[1024];
+  va_list ap;
+  va_start(ap, format);
+  vsnprintf(msg, sizeof msg, format, ap);
+  va_end(ap);
+  if (log_line(stream, priority, msg) < 0) perror("multilog: error vfprintf");
   return 0;
 }
 
@@ -186,6 +227,14 @@ static int ring_get(ipcbuf_t *id, key_t kc, int flag) {
     if (!dev) id->buffer[i] = p;
   }
   return 0;
+}
+
+/* the exported ipcbuf_get, on an attached sync segment; n_readers is not
+ * used (nor is it by the binary's) */
+int ipcbuf_get(ipcbuf_t *id, int flag, int n_readers) {
+  (void)n_readers;
+  if (!id || !id->sync) return -1;
+  return ring_get(id, id->sync->semkey_connect, flag);
 }
 
 static void free_local(ipcbuf_t *id) {
@@ -339,7 +388,9 @@ int ipcbuf_unlock_write(ipcbuf_t *id) {  /* @0x403b90 */
   return 0;
 }
 
-static uint64_t sod_minbuf(ipcbuf_t *id) {  /* ipcbuf_get_sod_minbuf @0x403ca0 */
+/* the earliest block a start of data may name: the last transfer's end
+ * (soclock_buf) while it is still in the ring, else the oldest block left */
+uint64_t ipcbuf_get_sod_minbuf(ipcbuf_t *id) {  /* @0x403ca0 */
   const ipcsync_t *s = id->sync;
   return s->w_buf - id->soclock_buf < s->nbufs ? id->soclock_buf : s->w_buf + 1 - s->nbufs;
 }
@@ -347,7 +398,7 @@ static uint64_t sod_minbuf(ipcbuf_t *id) {  /* ipcbuf_get_sod_minbuf @0x403ca0 *
 int ipcbuf_enable_sod(ipcbuf_t *id, uint64_t start_buf, uint64_t start_byte) {  /* @0x403cd0 */
   if (!id || !(id->state == ST_WRITER || id->state == ST_WCHANGE)) return -1;
   ipcsync_t *s = id->sync;
-  if (start_buf > s->w_buf || start_buf < sod_minbuf(id) || start_byte > s->bufsz) return -1;
+  if (start_buf > s->w_buf || start_buf < ipcbuf_get_sod_minbuf(id) || start_byte > s->bufsz) return -1;
   for (unsigned r = 0; r < s->n_readers; r++) /* every reader has acknowledged a start slot */
     if (sem_op(id->semid_data[r], SEM_SODACK, -1, 0) < 0) return -1;
   const uint64_t x = s->w_xfer % IPCBUF_XFERS;
@@ -389,6 +440,36 @@ char *ipcbuf_get_next_write(ipcbuf_t *id) {  /* @0x403f20 */
     id->count[b]--;
   }
   return id->buffer[b];
+}
+
+/* ipcbuf_zero_next_write (@0x404060): zero the block after the one being
+ * written, once it is free, polling every 10 ms.  Departure: "free" is
+ * decided from count[] and every reader's CLEAR (the fills still pending in
+ * this block and the current one all cleared); libpsrdada only waits for
+ * every CLEAR to be non-zero, which never happens on a fresh ring and does
+ * not say which block was cleared */
+int ipcbuf_zero_next_write(ipcbuf_t *id) {
+  if (!ipcbuf_is_writer(id)) {
+    fprintf(stderr, "ipcbuf_get_next_write: process is not writer\n");
+    return -1;
+  }
+  ipcsync_t *s = id->sync;
+  const uint64_t cur = s->w_buf % s->nbufs, next = (s->w_buf + 1) % s->nbufs;
+  for (;;) {
+    const int need = id->count[next] ? id->count[next] + (next != cur ? id->count[cur] : 0) : 0;
+    int ok = 1;
+    for (unsigned r = 0; ok && r < s->n_readers && need; r++) {
+      const int v = semctl(id->semid_data[r], SEM_CLEAR, GETVAL);
+      if (v < 0) return -1;
+      ok = v >= need;
+    }
+    if (ok) break;
+    if (g_interrupt) return -1;
+    nanosleep(&(struct timespec){0, 10000000}, NULL);
+  }
+  if (s->on_device_id >= 0) return dev_zero(id->buffer[next], s->bufsz);
+  memset(id->buffer[next], 0, s->bufsz);
+  return 0;
 }
 
 int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {  /* @0x404170 */
@@ -477,12 +558,52 @@ int ipcbuf_unlock_read(ipcbuf_t *id) {  /* @0x4045f0 */
 int ipcbuf_eod(ipcbuf_t *id) { return id && (id->state == ST_RSTOP || id->state == ST_VSTOP); }
 int ipcbuf_sod(ipcbuf_t *id) { return id && (id->state == ST_READING || id->state == ST_WRITING); }
 
-char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {  /* @0x404710 */
-  if (!ipcbuf_is_reader(id) || ipcbuf_eod(id)) return NULL;
+/* A viewer (ipcio_open 'r': no lock, takes nothing) follows the writer:
+ * its first block is the newest one written (or its transfer's start), then
+ * each next one as it is written, polled every 0.1 s, skipping ahead when
+ * the writer laps it; it stops (VSTOP, ipcbuf_eod) once reader 0 is at the
+ * transfer's end-of-data block.  Departures: the view that stops returns a
+ * 0-byte block (libpsrdada returns the unwritten block at the view
+ * position), and a block's size is that block's own (libpsrdada sizes it by
+ * reader 0's position). */
+static char *view_next(ipcbuf_t *id, uint64_t *bytes) {
+  ipcsync_t *s = id->sync;
+  uint64_t start = 0;
+  if (id->state == ST_VIEWER) {
+    id->xfer = s->r_xfers[0] % IPCBUF_XFERS;
+    id->state = ST_VIEWING;
+    id->viewbuf = s->s_buf[id->xfer];
+    if (s->w_buf > id->viewbuf + 1)
+      id->viewbuf = s->w_buf - 1;
+    else
+      start = s->s_byte[id->xfer];
+  }
+  while (s->w_buf <= id->viewbuf) {
+    if (s->eod[id->xfer] && s->r_bufs[0] && s->r_bufs[0] == s->e_buf[id->xfer]) {
+      id->state = ST_VSTOP;
+      if (bytes) *bytes = 0;
+      return id->buffer[id->viewbuf % s->nbufs];
+    }
+    if (g_interrupt) return NULL;
+    nanosleep(&(struct timespec){0, 100000000}, NULL);
+  }
+  if (id->viewbuf + s->nbufs < s->w_buf) id->viewbuf = s->w_buf - s->nbufs + 1;
+  const uint64_t b = id->viewbuf++;
+  const int last = s->eod[id->xfer] && s->e_buf[id->xfer] == b;
+  if (bytes) *bytes = (last ? s->e_byte[id->xfer] : s->bufsz) - start;
+  return id->buffer[b % s->nbufs] + start;
+}
+
+/* ipcbuf_get_next_read_work (@0x404710); flag goes to the reader's FULL and
+ * SODACK semops */
+char *ipcbuf_get_next_read_work(ipcbuf_t *id, uint64_t *bytes, int flag) {
+  if (!id || !id->sync || ipcbuf_eod(id)) return NULL;
+  if (id->state == ST_VIEWER || id->state == ST_VIEWING) return view_next(id, bytes);
+  if (!ipcbuf_is_reader(id)) return NULL;
   ipcsync_t *s = id->sync;
   const int r = id->iread, open = rd_open(id);
   if (open >= rd_depth(id) || (open && rd_eod_held(id))) return NULL;
-  if (sem_op(id->semid_data[r], SEM_FULL, -1, 0) < 0) return NULL;
+  if (sem_op(id->semid_data[r], SEM_FULL, -1, flag) < 0) return NULL;
   uint64_t start = 0;
   if (id->state == ST_READER) { /* first block of a transfer */
     id->xfer = s->r_xfers[r] % IPCBUF_XFERS;
@@ -490,13 +611,21 @@ char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) {  /* @0x404710 */
     s->r_states[r] = ST_READING;
     s->r_bufs[r] = s->s_buf[id->xfer];
     start = s->s_byte[id->xfer];
-    if (sem_op(id->semid_data[r], SEM_SODACK, 1, 0) < 0) return NULL;
+    if (sem_op(id->semid_data[r], SEM_SODACK, 1, flag) < 0) return NULL;
   }
   const uint64_t b = s->r_bufs[r] + (uint64_t)open;
   const int last = s->eod[id->xfer] && s->e_buf[id->xfer] == b;
   if (bytes) *bytes = (last ? s->e_byte[id->xfer] : s->bufsz) - start;
   rd_set(id, open + 1, last);
   return id->buffer[b % s->nbufs] + start;
+}
+
+char *ipcbuf_get_next_read(ipcbuf_t *id, uint64_t *bytes) { return ipcbuf_get_next_read_work(id, bytes, 0); }
+
+/* @0x4049d0: the binary passes 0x1000 (SEM_UNDO), so it waits as
+ * ipcbuf_get_next_read does */
+char *ipcbuf_get_next_readable(ipcbuf_t *id, uint64_t *bytes) {
+  return ipcbuf_get_next_read_work(id, bytes, SEM_UNDO);
 }
 
 int ipcbuf_mark_cleared(ipcbuf_t *id) {  /* @0x404b80: the oldest block held */
@@ -517,9 +646,58 @@ int ipcbuf_mark_cleared(ipcbuf_t *id) {  /* @0x404b80: the oldest block held */
   return 0;
 }
 
-int ipcbuf_reset(ipcbuf_t *id) {  /* @0x404ca0, reader half */
-  if (!id || id->state != ST_RSTOP) return -1;
-  id->state = ST_READER;
+/* ipcbuf_reset (@0x404ca0).  A reader at end of data gets ready for the
+ * next transfer.  A writer takes the ring back to its created state once
+ * every reader has cleared every block and acknowledged every transfer
+ * (CLEARs for count[], SODACK and EODACK down by 8 and back up); a ring
+ * never written to is left as it is. */
+int ipcbuf_reset(ipcbuf_t *id) {
+  if (!id) return -1;
+  if (id->state == ST_RSTOP) {
+    id->state = ST_READER;
+    return 0;
+  }
+  if (!ipcbuf_is_writer(id)) return -1;
+  ipcsync_t *s = id->sync;
+  if (!s->w_buf) return 0;
+  for (uint64_t b = 0; b < s->nbufs; b++)
+    for (; id->count[b]; id->count[b]--)
+      for (unsigned r = 0; r < s->n_readers; r++)
+        if (sem_op(id->semid_data[r], SEM_CLEAR, -1, 0) < 0) return -1;
+  for (unsigned r = 0; r < s->n_readers; r++) {
+    if (sem_op(id->semid_data[r], SEM_SODACK, -IPCBUF_XFERS, 0) < 0 ||
+        sem_op(id->semid_data[r], SEM_EODACK, -IPCBUF_XFERS, 0) < 0 ||
+        sem_op(id->semid_data[r], SEM_SODACK, IPCBUF_XFERS, 0) < 0 ||
+        sem_op(id->semid_data[r], SEM_EODACK, IPCBUF_XFERS, 0) < 0)
+      return -1;
+    s->r_bufs[r] = 0;
+    s->r_xfers[r] = 0;
+  }
+  s->w_buf = 0;
+  s->w_xfer = 0;
+  for (int x = 0; x < IPCBUF_XFERS; x++) s->eod[x] = 1;
+  return 0;
+}
+
+/* ipcbuf_hard_reset (@0x404f70): the same end state without waiting for
+ * anyone -- FULL and CLEAR of every reader set to 0.  Departure: count[] is
+ * zeroed too (libpsrdada leaves it, and the next writer then waits for
+ * CLEARs that were just discarded) */
+int ipcbuf_hard_reset(ipcbuf_t *id) {
+  if (!id || !id->sync) return -1;
+  ipcsync_t *s = id->sync;
+  s->w_buf = 0;
+  s->w_xfer = 0;
+  for (int x = 0; x < IPCBUF_XFERS; x++) s->eod[x] = 1;
+  memset(id->count, 0, s->nbufs);
+  for (unsigned r = 0; r < s->n_readers; r++) {
+    s->r_bufs[r] = 0;
+    s->r_xfers[r] = 0;
+    if (semctl(id->semid_data[r], SEM_FULL, SETVAL, 0) < 0 || semctl(id->semid_data[r], SEM_CLEAR, SETVAL, 0) < 0) {
+      perror("ipcbuf_hard_reset: semctl (IPCBUF_FULL, SETVAL)");
+      return -1;
+    }
+  }
   return 0;
 }
 
@@ -585,7 +763,7 @@ int ipcbuf_page(ipcbuf_t *id) {
 /* ------------------------------------------------------------------ */
 /* ipcio                                                                */
 
-static void ipcio_init(ipcio_t *ipc) {  /* @0x4057f0 */
+void ipcio_init(ipcio_t *ipc) {  /* @0x4057f0 */
   ipc->bytes = 0;
   ipc->rdwrt = 0;
   ipc->curbuf = NULL;
@@ -607,21 +785,42 @@ int ipcio_disconnect(ipcio_t *ipc) {
   return 0;
 }
 
+int ipcio_create_work(ipcio_t *ipc, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned num_read,
+                      int device_id) {  /* @0x405830 */
+  if (!ipc || ipcbuf_create_work(&ipc->buf, key, nbufs, bufsz, num_read, device_id) < 0) {
+    fprintf(stderr, "ipcio_create: ipcbuf_create error\n");
+    return -1;
+  }
+  ipcio_init(ipc);
+  return 0;
+}
+
+int ipcio_create(ipcio_t *ipc, key_t key, uint64_t nbufs, uint64_t bufsz, unsigned num_read) {
+  return ipcio_create_work(ipc, key, nbufs, bufsz, num_read, -1);
+}
+
+int ipcio_destroy(ipcio_t *ipc) {  /* @0x405990 */
+  if (!ipc) return -1;
+  ipcio_init(ipc);
+  return ipcbuf_destroy(&ipc->buf);
+}
+
+/* 'W' writer, 'w' writer with the start of data deferred (ipcio_start),
+ * 'R' reader, 'r' viewer (no lock: follows the writer, takes nothing) */
 int ipcio_open(ipcio_t *ipc, char rdwrt) {  /* @0x4059d0 */
   if (!ipc) return -1;
+  if (rdwrt != 'W' && rdwrt != 'w' && rdwrt != 'R' && rdwrt != 'r') {
+    fprintf(stderr, "ipcio_open: invalid rdwrt = '%c'\n", rdwrt);
+    return -1;
+  }
+  ipc->rdwrt = 0;
+  ipc->bytes = 0;
+  ipc->curbuf = NULL;
   if (rdwrt == 'W' || rdwrt == 'w') {
-    ipc->rdwrt = 0;
-    ipc->bytes = 0;
-    ipc->curbuf = NULL;
     if (ipcbuf_lock_write(&ipc->buf) < 0) return -1;
     if (rdwrt == 'w' && ipcbuf_disable_sod(&ipc->buf) < 0) return -1;
   } else if (rdwrt == 'R') {
-    ipc->rdwrt = 0;
-    ipc->bytes = 0;
-    ipc->curbuf = NULL;
     if (ipcbuf_lock_read(&ipc->buf) < 0) return -1;
-  } else {
-    return -1; /* 'r' (viewer) is not provided */
   }
   ipc->rdwrt = rdwrt;
   return 0;
@@ -631,7 +830,7 @@ int ipcio_is_open(ipcio_t *ipc) {
   return ipc && (ipc->rdwrt == 'R' || ipc->rdwrt == 'r' || ipc->rdwrt == 'W' || ipc->rdwrt == 'w');
 }
 
-static int check_pending_sod(ipcio_t *ipc) {  /* @0x405b20 */
+int ipcio_check_pending_sod(ipcio_t *ipc) {  /* @0x405b20 */
   if (!ipc->sod_pending || ipcbuf_get_write_count(&ipc->buf) <= ipc->sod_buf) return 0;
   if (ipcbuf_enable_sod(&ipc->buf, ipc->sod_buf, ipc->sod_byte) < 0) return -1;
   ipc->sod_pending = 0;
@@ -662,32 +861,35 @@ static int take_eod_slot(ipcbuf_t *id) {
   return 0;
 }
 
-/* ipcio_stop_close (@0x405c10) with close = 1: a writer with a transfer
- * open ends it -- the block being written, or a 0-byte block after a full
- * one, carries the end of data -- and unlocks.  Two departures, neither
- * visible to a reader:
+/* ipcio_stop_close (@0x405c10).  A writer with a transfer open ends it --
+ * the block being written, or a 0-byte block after a full one, carries the
+ * end of data -- and stays locked in 'w' mode (ipcio_start opens the next
+ * transfer); with unlock it also resets w_buf to the last transfer's end
+ * and unlocks.  A reader unlocks.  Departures, none visible to a reader:
  *  - the 0-byte block is taken like any other (get_next_write: the
  *    readers' CLEAR for its slot's last fill first).  libpsrdada marks it
  *    without that wait, so count[] runs one fill behind and the writer's
  *    next transfer can reuse a block a slow reader has not cleared yet
  *    (tests/test_dada.py::test_ring_transfers_property found it);
  *  - a writer that locked and wrote no block at all ends an empty transfer
- *    (a 0-byte end-of-data block) where libpsrdada would leave its readers
- *    waiting for data that never comes. */
-int ipcio_close(ipcio_t *ipc) {
+ *    on close (a 0-byte end-of-data block) where libpsrdada would leave its
+ *    readers waiting for data that never comes;
+ *  - a viewer closes (back to VIEWER; libpsrdada refuses 'r' here). */
+int ipcio_stop_close(ipcio_t *ipc, char unlock) {
   if (!ipc) return -1;
   ipcbuf_t *b = &ipc->buf;
   if (ipc->rdwrt == 'W') {
-    if (b->state == ST_WCHANGE && !b->sync->w_state && ipcbuf_enable_sod(b, b->sync->w_buf, 0) < 0)
+    if (unlock && b->state == ST_WCHANGE && !b->sync->w_state && ipcbuf_enable_sod(b, b->sync->w_buf, 0) < 0)
       return -1;
     if (ipcbuf_is_writing(b)) {
-      if (!ipc->curbuf && take_eod_slot(b) < 0) return -1;
-      if (ipcbuf_enable_eod(b) < 0 || ipcbuf_mark_filled(b, ipc->bytes) < 0 || check_pending_sod(ipc) < 0)
+      if ((!ipc->curbuf || ipc->marked_filled) && take_eod_slot(b) < 0) return -1;
+      if (ipcbuf_enable_eod(b) < 0 || ipcbuf_mark_filled(b, ipc->bytes) < 0 || ipcio_check_pending_sod(ipc) < 0)
         return -1;
       ipc->marked_filled = 1;
       if (ipc->bytes == ipcbuf_get_bufsz(&ipc->buf)) ipc->curbuf = NULL;
     }
     ipc->rdwrt = 'w';
+    if (!unlock) return 0;
   }
   if (ipc->rdwrt == 'w') {
     ipcsync_t *s = ipc->buf.sync;
@@ -701,7 +903,42 @@ int ipcio_close(ipcio_t *ipc) {
     ipc->rdwrt = 0;
     return 0;
   }
+  if (ipc->rdwrt == 'r') {
+    b->state = ST_VIEWER;
+    ipc->rdwrt = 0;
+    ipc->curbuf = NULL;
+    ipc->bytes = 0;
+    return 0;
+  }
+  fprintf(stderr, "ipcio_close: invalid ipcio_t\n");
   return -1;
+}
+
+int ipcio_close(ipcio_t *ipc) { return ipcio_stop_close(ipc, 1); }  /* @0x405e10 */
+
+/* ipcio_stop (@0x405dd0): end the transfer, keep the writer lock */
+int ipcio_stop(ipcio_t *ipc) {
+  if (!ipc || ipc->rdwrt != 'W') {
+    fprintf(stderr, "ipcio_stop: not writing!\n");
+    return -1;
+  }
+  return ipcio_stop_close(ipc, 0);
+}
+
+/* ipcio_start (@0x405b90): a 'w' writer starts a transfer at byte `byte`
+ * of its stream (block byte / bufsz, byte % bufsz into it), as soon as that
+ * block has been written */
+int ipcio_start(ipcio_t *ipc, uint64_t byte) {
+  if (!ipc || ipc->rdwrt != 'w') {
+    fprintf(stderr, "ipcio_start: invalid ipcio_t (%c)\n", ipc ? ipc->rdwrt : '?');
+    return -1;
+  }
+  const uint64_t bufsz = ipcbuf_get_bufsz(&ipc->buf);
+  ipc->sod_pending = 1;
+  ipc->rdwrt = 'W';
+  ipc->sod_buf = byte / bufsz;
+  ipc->sod_byte = byte % bufsz;
+  return ipcio_check_pending_sod(ipc);
 }
 
 char *ipcio_open_block_write(ipcio_t *ipc, uint64_t *block_id) {  /* @0x406340 */
@@ -725,7 +962,7 @@ ssize_t ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes) {  /* @0x406580 */
   if (ipcio_update_block_write(ipc, bytes) < 0) return -1;
   if (ipc->marked_filled) return 0;
   if (ipcbuf_mark_filled(&ipc->buf, ipc->bytes) < 0) return -2;
-  if (check_pending_sod(ipc) < 0) return -3;
+  if (ipcio_check_pending_sod(ipc) < 0) return -3;
   ipc->marked_filled = 1;
   ipc->curbuf = NULL;
   ipc->bytes = 0;
@@ -733,16 +970,19 @@ ssize_t ipcio_close_block_write(ipcio_t *ipc, uint64_t bytes) {  /* @0x406580 */
 }
 
 char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id) {  /* @0x4060b0 */
-  if (!ipc || ipc->bytes || ipc->rdwrt != 'R') return NULL;
+  if (!ipc || ipc->bytes || (ipc->rdwrt != 'R' && ipc->rdwrt != 'r')) return NULL;
   ipcbuf_t *id = &ipc->buf;
-  if (ipc->curbuf && rd_depth(id) <= 1) return NULL; /* one block at a time (PSRDADA) */
+  const int reader = ipc->rdwrt == 'R';
+  if (ipc->curbuf && (!reader || rd_depth(id) <= 1)) return NULL; /* one block at a time (PSRDADA) */
   if (ipcbuf_eod(id)) return NULL;
   uint64_t sz = 0;
   char *p = ipcbuf_get_next_read(id, &sz);
   if (!p) return NULL;
   ipc->curbuf = p;
   ipc->curbufsz = sz;
-  if (block_id) *block_id = (id->sync->r_bufs[id->iread] + (uint64_t)rd_open(id) - 1) % id->sync->nbufs;
+  if (block_id)
+    *block_id = (reader ? id->sync->r_bufs[id->iread] + (uint64_t)rd_open(id) - 1 : id->viewbuf - 1) %
+                id->sync->nbufs;
   if (curbufsz) *curbufsz = sz;
   ipc->bytes = 0;
   return p;
@@ -751,6 +991,11 @@ char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id
 /* the block is released once `bytes` add up to its size (PSRDADA); a
  * reader holding several blocks (read depth > 1) releases the oldest */
 ssize_t ipcio_close_block_read(ipcio_t *ipc, uint64_t bytes) {  /* @0x406200 */
+  if (ipc && ipc->rdwrt == 'r' && ipc->curbuf) { /* a viewer: nothing to release (libpsrdada refuses) */
+    ipc->curbuf = NULL;
+    ipc->bytes = 0;
+    return 0;
+  }
   if (!ipc || ipc->rdwrt != 'R' || !ipc->curbuf) return -1;
   ipcbuf_t *id = &ipc->buf;
   if (rd_depth(id) > 1) {
@@ -778,7 +1023,7 @@ ssize_t ipcio_write(ipcio_t *ipc, char *ptr, size_t bytes) {
   while (left) {
     if (ipc->bytes == bufsz) { /* the current block is full */
       if (!ipc->marked_filled) {
-        if (ipcbuf_mark_filled(&ipc->buf, ipc->bytes) < 0 || check_pending_sod(ipc) < 0) return -1;
+        if (ipcbuf_mark_filled(&ipc->buf, ipc->bytes) < 0 || ipcio_check_pending_sod(ipc) < 0) return -1;
       }
       ipc->curbuf = NULL;
       ipc->bytes = 0;
@@ -802,7 +1047,7 @@ ssize_t ipcio_write(ipcio_t *ipc, char *ptr, size_t bytes) {
 
 /* ipcio_read (@0x406660): fewer bytes than asked at the end of data */
 ssize_t ipcio_read(ipcio_t *ipc, char *ptr, size_t bytes) {
-  if (!ipc || ipc->rdwrt != 'R') return -1;
+  if (!ipc || (ipc->rdwrt != 'R' && ipc->rdwrt != 'r')) return -1;
   size_t left = bytes;
   while (left && !ipcbuf_eod(&ipc->buf)) {
     if (!ipc->curbuf) {
@@ -819,7 +1064,7 @@ ssize_t ipcio_read(ipcio_t *ipc, char *ptr, size_t bytes) {
     ipc->bytes += n;
     left -= n;
     if (ipc->bytes == ipc->curbufsz) {
-      if (ipcbuf_mark_cleared(&ipc->buf) < 0) return -1;
+      if (ipc->rdwrt == 'R' && ipcbuf_mark_cleared(&ipc->buf) < 0) return -1;
       ipc->curbuf = NULL;
       ipc->bytes = 0;
     }
@@ -969,6 +1214,50 @@ int dada_hdu_open(dada_hdu_t *h) {
 }
 
 int dada_hdu_open_read(dada_hdu_t *h) { return dada_hdu_open(h); }
+
+/* dada_hdu_open_view / _close_view (@0x407ac0 / @0x407b40): view the data
+ * ring (ipcio 'r'); the header ring is not touched */
+int dada_hdu_open_view(dada_hdu_t *h) {
+  if (!h || !h->data_block) {
+    fprintf(stderr, "dada_hdu_open_view: not connected\n");
+    return -1;
+  }
+  if (ipcio_open(h->data_block, 'r') < 0) {
+    if (h->log) multilog(h->log, LOG_ERR, "Could not open Data Block for viewing\n");
+    return -1;
+  }
+  return 0;
+}
+
+int dada_hdu_close_view(dada_hdu_t *h) {
+  if (!h || !h->data_block) {
+    fprintf(stderr, "dada_hdu_close_view: not connected\n");
+    return -1;
+  }
+  if (ipcio_close(h->data_block) < 0) {
+    if (h->log) multilog(h->log, LOG_ERR, "Could not close Data Block view\n");
+    return -1;
+  }
+  return 0;
+}
+
+/* dada_hdu_db_addresses / _hb_addresses (@0x407e50 / @0x407e80): the block
+ * address list of the data / header ring, with its geometry */
+char **dada_hdu_db_addresses(dada_hdu_t *h, uint64_t *nbufs, uint64_t *bufsz) {
+  if (!h || !h->data_block) return NULL;
+  ipcbuf_t *b = &h->data_block->buf;
+  if (nbufs) *nbufs = ipcbuf_get_nbufs(b);
+  if (bufsz) *bufsz = ipcbuf_get_bufsz(b);
+  return b->buffer;
+}
+
+char **dada_hdu_hb_addresses(dada_hdu_t *h, uint64_t *nbufs, uint64_t *bufsz) {
+  if (!h || !h->header_block) return NULL;
+  ipcbuf_t *b = h->header_block;
+  if (nbufs) *nbufs = ipcbuf_get_nbufs(b);
+  if (bufsz) *bufsz = ipcbuf_get_bufsz(b);
+  return b->buffer;
+}
 
 /* ------------------------------------------------------------------ */
 /* ring pairs (the dada_db tool)                                        */

@@ -37,7 +37,7 @@ def dlib():
         L.dada_hdu_set_key.argtypes = [P, C.c_int]
         for n in ("dada_hdu_connect", "dada_hdu_disconnect", "dada_hdu_lock_write",
                   "dada_hdu_unlock_write", "dada_hdu_lock_read", "dada_hdu_unlock_read",
-                  "dada_hdu_open_read"):
+                  "dada_hdu_open_read", "dada_hdu_open_view", "dada_hdu_close_view"):
             getattr(L, n).argtypes = [P]
         L.dada_hdu_destroy.argtypes = [P]
         L.dada_hdu_destroy.restype = None
@@ -65,6 +65,17 @@ def dlib():
         L.ipcbuf_set_read_depth.argtypes = [P, C.c_int]
         L.ipcbuf_copy_in.argtypes = [P, P, P, C.c_uint64]
         L.ipcbuf_copy_out.argtypes = [P, P, P, C.c_uint64]
+        for n in ("ipcbuf_get_nfull", "ipcbuf_get_nclear", "ipcbuf_get_sodack", "ipcbuf_get_eodack"):
+            getattr(L, n).restype = C.c_uint64
+            getattr(L, n).argtypes = [P]
+            getattr(L, n + "_iread").restype = C.c_uint64
+            getattr(L, n + "_iread").argtypes = [P, C.c_int]
+        L.ipcbuf_get_reader_conn_iread.argtypes = [P, C.c_int]
+        L.ipcbuf_get_read_semaphore_count.argtypes = [P]
+        L.ipcio_read.restype = C.c_ssize_t
+        L.ipcio_read.argtypes = [P, P, C.c_size_t]
+        L.ipcio_write.restype = C.c_ssize_t
+        L.ipcio_write.argtypes = [P, P, C.c_size_t]
         L.dada_db_create_work.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint64,
                                           C.c_uint64, C.c_int]
         _dl = L
@@ -145,7 +156,8 @@ def destroy_ring(key: int) -> bool:
 
 
 class Hdu:
-    """A dada_hdu_t as writer ('W') or reader ('R')."""
+    """A dada_hdu_t as writer ('W'), reader ('R') or viewer of the data ring
+    ('r': follows the writer without taking blocks, dada_hdu_open_view)."""
 
     def __init__(self, key: int, mode: str):
         L = dlib()
@@ -156,7 +168,7 @@ class Hdu:
         if L.dada_hdu_connect(self.h) != 0:
             L.dada_hdu_destroy(self.h)
             raise OSError(f"no ring at key {key:x}")
-        lock = L.dada_hdu_lock_write if mode == "W" else L.dada_hdu_lock_read
+        lock = {"W": L.dada_hdu_lock_write, "R": L.dada_hdu_lock_read, "r": L.dada_hdu_open_view}[mode]
         if lock(self.h) != 0:
             L.dada_hdu_destroy(self.h)
             raise OSError(f"cannot lock ring {key:x} for {mode}")
@@ -273,10 +285,28 @@ class Hdu:
     def eod(self) -> bool:
         return bool(dlib().ipcbuf_eod(self.data))
 
+    def nfull(self, reader: int = -1) -> int:
+        """blocks filled and not yet taken by reader `reader` (ipcbuf_get_nfull)"""
+        return int(dlib().ipcbuf_get_nfull_iread(self.data, reader))
+
+    def write(self, data: bytes) -> None:
+        """stream bytes into the ring across blocks (ipcio_write)"""
+        if dlib().ipcio_write(self.data, bytes(data), len(data)) != len(data):
+            raise OSError("ipcio_write")
+
+    def read(self, nbytes: int) -> bytes:
+        """up to nbytes of the stream (fewer at end of data; ipcio_read)"""
+        buf = C.create_string_buffer(nbytes)
+        n = dlib().ipcio_read(self.data, buf, nbytes)
+        if n < 0:
+            raise OSError("ipcio_read")
+        return buf.raw[:n]
+
     def close(self) -> None:
         if self.h:
             L = dlib()
-            (L.dada_hdu_unlock_write if self.mode == "W" else L.dada_hdu_unlock_read)(self.h)
+            {"W": L.dada_hdu_unlock_write, "R": L.dada_hdu_unlock_read,
+             "r": L.dada_hdu_close_view}[self.mode](self.h)
             L.dada_hdu_destroy(self.h)
             self.h = None
 

@@ -143,7 +143,7 @@ def declarations(path: str):
     text = open(path).read()
     text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
     text = re.sub(r"^\s*#.*$", " ", text, flags=re.M)  # preprocessor lines
-    text = re.sub(r"__attribute__\s*\(\(.*?\)\)", " ", text)
+    text = re.sub(r"__attribute__\s*\(\((?:[^()]|\([^()]*\))*\)\)", " ", text)
     out = {}
     for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(\w+)\s*\(([^;{}()]*)\)\s*;", text):
         ret, name, params = m.group(1), m.group(2), m.group(3)
@@ -179,15 +179,17 @@ def test_standin_prototypes_match_dwarf():
     assert not bad, bad
 
 
-def test_libpafdada_exports_the_psrdada_subset():
-    """the writer and reader subset the reference's hosts use (SURVEY.md
-    Appendix A) is exported, with no symbol missing"""
+def test_libpafdada_exports_the_whole_psrdada_api():
+    """every function of the libpsrdada the reference links (all 113 its
+    debug info holds) is declared in include/b2p_dada.h and exported by
+    libpafdada -- not only the subset the reference's hosts call"""
     lib = os.path.join(REPO, "paf-baseband2power_amd", "lib", "libpafdada.so")
     out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True,
                          check=True).stdout
     have = {ln.split()[-1] for ln in out.splitlines()}
-    need = {n for n in decl_names() if n in ABI["functions"]}
-    assert need <= have, sorted(need - have)
+    assert len(ABI["functions"]) == 113
+    assert set(ABI["functions"]) <= have, sorted(set(ABI["functions"]) - have)
+    assert set(ABI["functions"]) <= decl_names(), sorted(set(ABI["functions"]) - decl_names())
 
 
 def decl_names():

@@ -10,7 +10,7 @@ import pytest
 from conftest import REPO
 
 SRC = [os.path.join(REPO, "paf-baseband2power_amd", "csrc", "dada", f)
-       for f in ("dada_ring.c", "dada_device.c", "ascii_header.c")]
+       for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c")]
 DRIVER = os.path.join(REPO, "tests", "c", "ring_stress.c")
 
 
@@ -53,7 +53,7 @@ def test_capture_receive_threads_under_tsan(tmp_path):
     stub = tmp_path / "stub.c"
     stub.write_text("".join(f"int {s}(void) {{ return -5; }}\n" for s in b2p))
     dsrc = [os.path.join(REPO, "paf-baseband2power_amd", "csrc", "dada", f)
-            for f in ("dada_ring.c", "dada_device.c", "ascii_header.c", "df_header.c")]
+            for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c", "df_header.c")]
     exe = tmp_path / "paf_capture_tsan"
     subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", "-fsanitize=thread", *inc,
                     str(obj), str(stub), *dsrc, "-o", str(exe), "-pthread", "-ldl", "-lm"], check=True)
