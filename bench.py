@@ -106,6 +106,10 @@ def parse(argv=None):
     ap.add_argument("--no-fuse", action="store_true",
                     help="use b2p_push + b2p_finish_async instead of b2p_integrate")
     ap.add_argument("--no-verify", action="store_true", help="skip the post-timing oracle check")
+    ap.add_argument("--blocks-per-launch", type=int, default=0, choices=range(0, 9), metavar="0..8",
+                    help="integrations per integrate launch (b2p_integrate_n: a consumer draining "
+                         "queued HBM-resident blocks); 1 = one b2p_integrate per block; 0 (default) = "
+                         "auto, as the stage batches queued blocks: floor(4 GiB / block), 1..8")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="seconds one multi-rank phase (rendezvous, first collective, a timed "
                          "region, verification) may take; past it the rank exits 4 naming it")
@@ -197,16 +201,23 @@ def parallelism_label(world: int, split: bool, dist_on: bool, rccl: bool) -> str
     return s
 
 
-def pmc_traffic(config: str):
+def pmc_traffic(config: str, bytes_per_launch: float):
     """HBM bytes per launch from the committed rocprofv3 PMC summary for this
     config (profiles/pmc_<config>.json, written by tools/pmc_summary.py from
-    separate --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
+    separate --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).
+    Measured on launches of another size (blocks per launch), it is scaled
+    by this run's algorithmic bytes per launch, and the source says so."""
     p = os.path.join(REPO, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
         return None, None
     try:
         d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(p, REPO)
+        hbm, alg = d.get("hbm_bytes_per_launch"), d.get("algorithmic_bytes_per_launch")
+        src = os.path.relpath(p, REPO)
+        if hbm and alg and bytes_per_launch and int(alg) != int(bytes_per_launch):
+            return (int(round(hbm / alg * bytes_per_launch)),
+                    f"{src} (measured on {alg}-B launches, scaled to {int(bytes_per_launch)} B)")
+        return hbm, src
     except (OSError, ValueError):
         return None, None
 
@@ -363,7 +374,8 @@ def main(argv=None) -> int:
         it.register_host(hb)
         blocks = [hb]
     else:
-        for b in range(NBLOCKS):
+        for b in range(max(NBLOCKS, a.blocks_per_launch or paf_b2p.blocks_per_launch(bb))):
+            # (distinct blocks within a launch)
             d = it.alloc(bb)
             it.fill_synthetic(d, SEED, subband, b, elem0=elem0)
             blocks.append(d)
@@ -382,6 +394,26 @@ def main(argv=None) -> int:
         else:  # b2p_integrate: one integrate launch per integration (its
             # finalize rides on the next launch)
             it.integrate(blk, dst, True)
+
+    # several queued blocks per integrate launch (b2p_integrate_n), for the
+    # HBM-resident fused path only; every integration still gets its spectrum
+    bpl = a.blocks_per_launch or paf_b2p.blocks_per_launch(bb)
+    if not a.blocks_per_launch:  # auto: every launch the same size (a divisor of K)
+        bpl = max(n for n in range(1, bpl + 1) if K % n == 0)
+    if split or host_mode or a.no_fuse:
+        bpl = 1
+
+    def steps(k0, row0, n):
+        """integrations k0 .. k0+n-1 into output rows row0 .."""
+        j = 0
+        while j < n:
+            m = min(bpl, n - j)
+            if m == 1:
+                step(k0 + j, row0 + j)
+            else:
+                it.integrate_n([blocks[(k0 + j + i) % len(blocks)] for i in range(m)],
+                               out_ptr + (row0 + j) * nout * 4, True)
+            j += m
 
     coll = {"op": "gather"}
 
@@ -419,8 +451,8 @@ def main(argv=None) -> int:
 
     kk = 0
     for _ in range(a.warmup):
-        step(kk, 0)
-        kk += 1
+        steps(kk, 0, 1 if bpl == 1 else min(bpl, K))
+        kk += 1 if bpl == 1 else min(bpl, K)
     it.sync()
     if dist_on:  # a communicator's first collective sets up its channels
         wd.arm(f"first {a.dist_backend} collective (communicator set-up)")
@@ -451,9 +483,8 @@ def main(argv=None) -> int:
         fence()
         t0 = time.perf_counter()
         it.set_timing(2)  # one event pair on the integrator's stream around the K launches
-        for k in range(K):
-            step(kk, k)
-            kk += 1
+        steps(kk, 0, K)
+        kk += K
         it.set_timing(0)  # records the closing event right behind the last launch (no wait)
         if not rccl:  # host-side exchange (gloo) reads what the integrator's stream wrote
             it.sync()
@@ -552,8 +583,7 @@ def main(argv=None) -> int:
     if not split and not host_mode and not a.no_fuse:
         it.reset_stats()
         it.set_timing(1)
-        for k in range(16):
-            it.integrate(blocks[k % len(blocks)], out_ptr, True)
+        steps(0, 0, min(16 * bpl, K))
         it.set_timing(0)
         it.sync()
         cs = it.stats()
@@ -563,7 +593,7 @@ def main(argv=None) -> int:
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
     achieved = bytes_per_launch / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(a.config)
+    traffic, traffic_src = pmc_traffic(a.config, bytes_per_launch)
 
     rc = 0
     if rank == 0:
@@ -609,12 +639,17 @@ def main(argv=None) -> int:
                 "nsamp_int": int(full_nsamp if split else geom.nsamp_int),
                 "bytes_per_integration": int(bb * (world if split else 1)),
                 "input": "pinned host buffer, H2D overlapped (PCIe-inclusive)" if host_mode
-                         else f"HBM-resident, {NBLOCKS} rotating blocks per GPU",
+                         else f"HBM-resident, {len(blocks)} rotating blocks per GPU",
                 "parallelism": parallelism_label(world, split, dist_on, rccl)
                 + ("" if coll["op"] == "gather" else " (all_gather: the backend refused gather)"),
                 "launcher": ("bench.py --gpus spawned torch.distributed.run"
                              if os.environ.get("BENCH_LAUNCHED_RANKS") else
                              ("torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")),
+                "blocks_per_launch": bpl,
+                "blocks_per_launch_rule": ("set by --blocks-per-launch" if a.blocks_per_launch else
+                                           "auto: floor(4 GiB / block), 1..8 -- the rule the stage "
+                                           "applies to blocks queued in its input ring -- lowered to "
+                                           "a divisor of --steps so every launch is the same size"),
                 "launch": {"threads": it.info.threads, "columns": it.info.columns,
                            "row_groups": it.info.row_groups, "replicas": it.info.replicas,
                            "unroll": it.info.unroll, "nt_loads": bool(it.info.nontemporal)},

@@ -234,6 +234,13 @@ int b2p_integrate(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device,
  * whose rows span several workgroups (frame-split: BMF, TFTFP) run one
  * launch per block, which measured as fast there. */
 #define B2P_MAX_BLOCKS 8
+/* How many queued blocks a consumer should hand one b2p_integrate_n: enough
+ * that a launch reads at least B2P_BATCH_BYTES (4 GiB), so its fixed ramp
+ * and tail (~2-3 us) cost under 0.5 %; 1..B2P_MAX_BLOCKS.  Measured on
+ * MI355X: 1 GiB blocks 0.890 -> 0.900 of 8 TB/s at 4 per launch, 4 GiB
+ * blocks gain nothing. */
+#define B2P_BATCH_BYTES (4ull << 30)
+uint32_t b2p_blocks_per_launch(uint64_t block_bytes);
 int b2p_integrate_n(b2p_ctx_t *ctx, const void *const *bufs, uint32_t nblk, float *out,
                     int out_is_device);
 /* Number of samples pushed into the current integration. */

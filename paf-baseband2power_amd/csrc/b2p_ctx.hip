@@ -879,6 +879,11 @@ int b2p_integrate_n(b2p_ctx_t *c, const void *const *bufs, uint32_t nblk, float 
   return B2P_OK;
 }
 
+uint32_t b2p_blocks_per_launch(uint64_t block_bytes) {
+  const uint64_t n = block_bytes ? B2P_BATCH_BYTES / block_bytes : 1;
+  return n < 1 ? 1 : n > kMaxBlk ? (uint32_t)kMaxBlk : (uint32_t)n;
+}
+
 int b2p_set_timing(b2p_ctx_t *c, int mode) {
   if (!c || mode < 0 || mode > 2) return B2P_EINVAL;
   LIVE(c);

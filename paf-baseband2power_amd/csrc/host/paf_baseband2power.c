@@ -386,69 +386,101 @@ static void *worker(void *arg) {
 }
 
 #if DEVICE_RINGS
-/* One sub-band on a GPU-resident ring: two blocks in flight.  Block k's
- * launch is enqueued before block k-1 is released, so the GPU never waits
- * on the host between integrations.  Block k-1 goes back to the ring once
- * its launch has finished (b2p_fence).  Its spectrum is finalized by launch
- * k and copied to the host behind it, so outputs trail by one block. */
+/* One sub-band on a GPU-resident ring, launches kept in flight.  Batch k's
+ * launch is enqueued before batch k-1's blocks are released, so the GPU
+ * never waits on the host between launches; batch k-1 goes back to the ring
+ * once its launch has finished (b2p_fence).  A batch is the next block plus
+ * every further full block already queued in the ring (ipcbuf_get_nfull:
+ * no wait), up to b2p_blocks_per_launch (a launch of >= 4 GiB), in ONE launch
+ * (b2p_integrate_n): a consumer that has fallen behind catches up without
+ * paying a launch per block.  Spectra are finalized by the next launch and
+ * copied home behind it, so outputs trail by one batch. */
+
+typedef struct {
+  uint64_t first; /* index of its first integration */
+  uint32_t n;     /* blocks (integrations) */
+  uint64_t ticket;
+} batch_t;
 
 static void run_device_pipelined(shared_t *sh) {
   sub_t *s = &sh->sub[0];
   ipcio_t *in = s->in->data_block;
-  const size_t sb = (sh->obytes + 4095) / 4096 * 4096;
-  float *spec = aligned_alloc(4096, 3 * sb); /* spectra k-2, k-1, k */
-  if (!spec || ipcbuf_set_read_depth(&in->buf, 2) < 0) {
+  const uint64_t nbufs = ipcbuf_get_nbufs(&in->buf);
+  /* blocks held: the batch in flight and the one being gathered */
+  const int depth = (int)(nbufs < 2 * B2P_MAX_BLOCKS ? nbufs : 2 * B2P_MAX_BLOCKS);
+  /* per launch: b2p_blocks_per_launch (>= 4 GiB read), within the depth */
+  const uint32_t want = b2p_blocks_per_launch(s->rbufsz);
+  const uint32_t bmax = depth > 1 ? ((uint32_t)depth - 1 < want ? (uint32_t)depth - 1 : want) : 1;
+  const size_t sb = (sh->obytes * bmax + 4095) / 4096 * 4096;
+  float *spec = aligned_alloc(4096, 3 * sb); /* spectra of batches k-2, k-1, k */
+  if (!spec || ipcbuf_set_read_depth(&in->buf, depth < 2 ? 2 : depth) < 0) {
     free(spec);
     sh->failed = 1;
     return;
   }
   b2p_register_host(s->ctx, spec, 3 * sb);
 #define SPEC(k) ((float *)((char *)spec + ((k) % 3) * sb))
-  uint64_t k = 0, written = 0, ticket[2] = {0, 0};
-  int open_prev = 0; /* block k-1 still held */
+  batch_t bat[3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+  uint64_t k = 0, next = 0; /* batches launched; integrations launched */
+  uint64_t written = 0;    /* batches whose spectra went out */
+  int held = 0;            /* blocks of batch k-1 still held */
   for (;;) {
+    const void *blks[B2P_MAX_BLOCKS];
     uint64_t bytes = 0, bid = 0;
     char *blk = g_stop ? NULL : ipcio_open_block_read(in, &bytes, &bid);
-    const int full = blk && bytes == s->rbufsz;
-    if (!full) { /* end of data or a partial block: drain the pipeline */
-      if (b2p_sync(s->ctx) != B2P_OK) sh->failed = 1;
-      if (open_prev) ipcio_close_block_read(in, 0);
-      open_prev = 0;
-      for (; !sh->failed && written < k; written++)
-        if (write_output(sh, SPEC(written)) < 0) sh->failed = 1;
-      if (blk) {
-        ipcio_close_block_read(in, bytes);
-        if (bytes) { /* a 0-byte block only carries the end of data */
-          sh->nskipped++;
-          multilog(sh->log, LOG_INFO, "partial integration skipped (a block held %" PRIu64 " of %" PRIu64
-                   " B)", bytes, s->rbufsz);
-        }
+    uint32_t n = 0;
+    while (blk && bytes == s->rbufsz) { /* gather this batch */
+      blks[n++] = blk;
+      blk = NULL;
+      if (n == bmax || held + (int)n >= depth || g_stop || ipcbuf_get_nfull_iread(&in->buf, in->buf.iread) == 0)
+        break;
+      blk = ipcio_open_block_read(in, &bytes, &bid); /* already queued: no wait */
+    }
+    batch_t *b = &bat[k % 3];
+    int rc = B2P_OK;
+    if (n) {
+      const double t0 = now_s();
+      if (sh->t_first == 0) sh->t_first = t0;
+      *b = (batch_t){next, n, 0};
+      rc = n == 1 ? b2p_integrate(s->ctx, blks[0], s->rbufsz, 1, SPEC(k), 0)
+                  : b2p_integrate_n(s->ctx, blks, n, SPEC(k), 0);
+      if (rc == B2P_OK) rc = b2p_fence(s->ctx, &b->ticket);
+      if (rc == B2P_OK && held) {
+        rc = b2p_fence_wait(s->ctx, bat[(k - 1) % 3].ticket); /* batch k-1 is done */
+        for (; rc == B2P_OK && held; held--) ipcio_close_block_read(in, 0); /* its blocks go back */
+        for (; rc == B2P_OK && written + 2 <= k; written++) /* batch k-2 is home */
+          for (uint32_t j = 0; rc == B2P_OK && j < bat[written % 3].n; j++)
+            if (write_output(sh, SPEC(written) + (size_t)j * (sh->obytes / 4)) < 0) rc = B2P_EHIP;
       }
-      if (!blk || sh->failed) break;
-      continue;
+      held += (int)n; /* this batch's blocks, launched or not */
+      if (rc == B2P_OK) {
+        next += n;
+        k++;
+        if (getenv("B2P_TRACE_PIPELINE") || k % 64 == 1)
+          multilog(sh->log, LOG_INFO, "launch %" PRIu64 ": %u integration(s) from %" PRIu64 ", %.3f ms in "
+                   "the loop body, %.3f ms since the first", k, n, b->first + 1, (now_s() - t0) * 1e3,
+                   (now_s() - sh->t_first) * 1e3);
+      } else {
+        multilog(sh->log, LOG_ERR, "integrate: %s (%s)", b2p_strerror(rc), b2p_last_error(s->ctx));
+        sh->failed = 1;
+      }
+      if (rc == B2P_OK && !blk && !g_stop) continue; /* the next block decides */
     }
-    const double t0 = now_s();
-    if (sh->t_first == 0) sh->t_first = t0;
-    int rc = b2p_integrate(s->ctx, blk, bytes, 1, SPEC(k), 0);
-    if (rc == B2P_OK) rc = b2p_fence(s->ctx, &ticket[k & 1]);
-    if (rc == B2P_OK && open_prev) {
-      rc = b2p_fence_wait(s->ctx, ticket[(k - 1) & 1]); /* launch k-1 is done */
-      ipcio_close_block_read(in, 0);                     /* releases block k-1 */
-      open_prev = 0;
-      for (; rc == B2P_OK && written + 2 <= k; written++) /* spectrum k-2 is home */
-        if (write_output(sh, SPEC(written)) < 0) rc = B2P_EHIP;
+    /* end of data, a partial block, a stop or a failure: drain the pipeline */
+    if (b2p_sync(s->ctx) != B2P_OK) sh->failed = 1;
+    for (; held; held--) ipcio_close_block_read(in, 0);
+    for (; !sh->failed && written < k; written++)
+      for (uint32_t j = 0; !sh->failed && j < bat[written % 3].n; j++)
+        if (write_output(sh, SPEC(written) + (size_t)j * (sh->obytes / 4)) < 0) sh->failed = 1;
+    if (blk) {
+      ipcio_close_block_read(in, bytes);
+      if (bytes) { /* a 0-byte block only carries the end of data */
+        sh->nskipped++;
+        multilog(sh->log, LOG_INFO, "partial integration skipped (a block held %" PRIu64 " of %" PRIu64
+                 " B)", bytes, s->rbufsz);
+      }
     }
-    if (rc != B2P_OK) {
-      multilog(sh->log, LOG_ERR, "integrate: %s (%s)", b2p_strerror(rc), b2p_last_error(s->ctx));
-      sh->failed = 1;
-      ipcio_close_block_read(in, 0);
-      break;
-    }
-    open_prev = 1;
-    k++;
-    if (getenv("B2P_TRACE_PIPELINE") || k % 64 == 1)
-      multilog(sh->log, LOG_INFO, "integration %" PRIu64 " enqueued, %.3f ms in the loop body, "
-               "%.3f ms since the first", k, (now_s() - t0) * 1e3, (now_s() - sh->t_first) * 1e3);
+    if (!blk || sh->failed) break;
   }
 #undef SPEC
   b2p_unregister_host(s->ctx, spec);
@@ -821,7 +853,8 @@ int main(int argc, char *argv[]) {
   {
 #if DEVICE_RINGS
     if (!split && nmem == 1 && sub[0].ondev && !getenv("B2P_NO_PIPELINE")) {
-      multilog(log, LOG_INFO, "GPU-resident input: two blocks in flight");
+      multilog(log, LOG_INFO, "GPU-resident input: two launches in flight, queued blocks integrated "
+               "together (up to %d per launch)", B2P_MAX_BLOCKS);
       run_device_pipelined(&sh);
       goto joined;
     }

@@ -110,6 +110,7 @@ PROTOTYPES = {
     "b2p_sync": (C.c_int, [_P]),
     "b2p_integrate": (C.c_int, [_P, _P, C.c_size_t, C.c_int, _P, C.c_int]),
     "b2p_integrate_n": (C.c_int, [_P, C.POINTER(_P), C.c_uint32, _P, C.c_int]),
+    "b2p_blocks_per_launch": (C.c_uint32, [C.c_uint64]),
     "b2p_samples_pending": (C.c_uint64, [_P]),
     "b2p_set_timing": (C.c_int, [_P, C.c_int]),
     "b2p_get_stats": (C.c_int, [_P, C.POINTER(Stats)]),

@@ -66,6 +66,16 @@ def block_bytes(g: L.Geom) -> int:
     return g.nsamp_int // g.nsamp_df * frame_bytes(g)
 
 
+BATCH_BYTES = 4 << 30  # include/b2p.h B2P_BATCH_BYTES
+MAX_BLOCKS = 8         # B2P_MAX_BLOCKS
+
+
+def blocks_per_launch(block_bytes: int) -> int:
+    """queued blocks per b2p_integrate_n launch (b2p_blocks_per_launch in
+    include/b2p.h): a launch reads >= 4 GiB, 1..8 blocks"""
+    return max(1, min(MAX_BLOCKS, BATCH_BYTES // block_bytes if block_bytes else 1))
+
+
 def nchan(g: L.Geom) -> int:
     return g.nchunk * g.nchan_chunk
 

@@ -103,6 +103,15 @@ def test_strerror_covers_codes():
     assert L.lib().b2p_strerror(-99).decode() == "unknown error"
 
 
+def test_blocks_per_launch_rule():
+    """queued blocks per b2p_integrate_n launch: a launch reads >= 4 GiB,
+    1..8 blocks; the Python mirror (bench.py's default) is the same rule"""
+    sizes = [0, 1, 1 << 24, 1 << 28, 512 << 20, 1 << 30, (1 << 30) + 1, 2 << 30, 2818572288, 4 << 30, 1 << 40]
+    got = [L.lib().b2p_blocks_per_launch(n) for n in sizes]
+    assert got == [1, 8, 8, 8, 8, 4, 3, 2, 1, 1, 1]
+    assert got == [paf_b2p.blocks_per_launch(n) for n in sizes]
+
+
 def test_open_without_gpu_fails_cleanly(have_gpu):
     if have_gpu:
         pytest.skip("a GPU is visible")

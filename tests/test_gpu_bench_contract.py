@@ -49,6 +49,23 @@ def test_bench_prints_one_contract_line(gpu):
     assert lo <= d["ms_per_step"] <= hi
 
 
+def test_bench_blocks_per_launch(gpu):
+    """--blocks-per-launch 4: queued HBM blocks in one b2p_integrate_n launch;
+    still one spectrum per step (10 steps: two launches of 4 and one of 2),
+    every one verified against the oracle; the roofline is per launch"""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "10", "--warmup", "1",
+                        "--cpu-seconds", "0", "--min-seconds", "0.05", "--blocks-per-launch", "4"],
+                       capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    assert d["verified"] is True and d["steps"] == 10
+    assert d["config"]["blocks_per_launch"] == 4
+    rf = d["roofline"]
+    per_block = d["config"]["bytes_per_integration"]
+    assert 3 * per_block < rf["algorithmic_bytes_per_launch"] < 4 * per_block  # (4+4+2)/3 blocks
+    assert rf["launches_timed"] % 3 == 0
+
+
 def test_bench_gpus2_gloo_spawns_two_ranks(gpu):
     """`bench.py --gpus 2` with no external launcher starts two ranks itself
     (gloo: both share the box's one GPU) and reports them"""

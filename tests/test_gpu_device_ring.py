@@ -8,7 +8,9 @@ a holder process (dada_db -g) and shared through HIP IPC handles.
 * paf_dfdb assembles a raw data-frame stream (paf_dfgen) on the GPU straight
   into the ring block, and the spectra match the oracle of the original
   blocks, with and without lost frames;
-* replay mode hands out re-used blocks, spectra match the oracle.
+* replay mode hands out re-used blocks, spectra match the oracle;
+* blocks already queued when the stage gets to them are integrated in one
+  launch (b2p_integrate_n), spectra bit-equal to the oracle.
 """
 import os
 import subprocess
@@ -94,7 +96,7 @@ def test_pipeline_with_device_input_ring(gpu, tmp_path):
         blk = payload[i * g.block_bytes:(i + 1) * g.block_bytes]
         assert np.array_equal(sp[i].view(np.uint32), co.power(g, blk, nthreads=8).view(np.uint32))
     log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
-    assert "GPU-resident" in log and "two blocks in flight" in log
+    assert "GPU-resident" in log and "two launches in flight" in log
     assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log
 
 
@@ -195,3 +197,37 @@ def test_gathered_subbands_on_device_rings(gpu, tmp_path):
             assert np.array_equal(sp[i, r].view(np.uint32), co.power(g, blk).view(np.uint32))
     log = open(str(tmp_path / "out" / "paf_baseband2power.log")).read()
     assert log.count("GPU-resident (device 0)") == 2
+
+
+def test_queued_blocks_are_integrated_in_one_launch(gpu, tmp_path):
+    """the input ring is filled (7 whole integrations + the end of data)
+    before the stage starts: it takes every queued block into one
+    b2p_integrate_n launch, and each spectrum equals the oracle's"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    nblk = 7
+    kin, kout = fresh_key(), fresh_key()
+    dada.create_ring(kin, nblk + 1, g.block_bytes, device=0)
+    dada.create_ring(kout, 4, g.nout * 4)
+    try:
+        payload = [co.fill_synthetic(g, g.block_bytes, SEED, 0, i) for i in range(nblk)]
+        with dada.Hdu(kin, "W") as w:
+            w.write_header(open(HDR).read())
+            for p in payload:
+                w.write_block(p.tobytes())
+        out = tmp_path / "power.dada"
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}",
+                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", "int8:256"],
+                                  stderr=subprocess.PIPE)]
+        _wait(procs)
+        _, data = dada.read_dada_file(str(out))
+        sp = data.view(np.float32).reshape(-1, g.nout)
+        assert sp.shape[0] == nblk
+        for i in range(nblk):
+            assert np.array_equal(sp[i].view(np.uint32), co.power(g, payload[i]).view(np.uint32))
+        log = open(str(tmp_path / "paf_baseband2power.log")).read()
+        assert "launch 1: 7 integration(s) from 1" in log
+    finally:
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)

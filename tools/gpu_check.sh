@@ -6,6 +6,7 @@
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
+#          benchbpl profbpl benchcmp
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -60,6 +61,18 @@ for s in $STEPS; do
             --cpu-seconds 0 --force-dist --split time &&
           run bench_split2gloo 600 python3 bench.py --gpus 2 --steps 10 --warmup 2 \
             --dist-backend gloo --split time ;;
+    benchbpl) for n in 2 4 8; do
+                run bench_bpl$n 600 python3 bench.py --steps 48 --warmup 4 --cpu-seconds 0 --blocks-per-launch $n &&
+                run bench_c5_bpl$n 600 python3 bench.py --config c5 --steps 24 --warmup 2 --cpu-seconds 0 \
+                  --blocks-per-launch $n || exit $?
+              done ;;
+    benchcmp) for r in 1 2; do  # the driver's command, and the same with one block per launch
+                run cmp_auto_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 &&
+                run cmp_bpl1_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 \
+                  --blocks-per-launch 1 || exit $?
+              done ;;
+    profbpl) run prof_bpl4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bpl4" -o run \
+            -- python3 bench.py --steps 48 --warmup 4 --cpu-seconds 0 --blocks-per-launch 4 ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
     asm) run bench_assemble 600 python3 tools/bench_assemble.py --steps 10 --warmup 2 ;;
     profasm) run prof_asm 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_asm" -o run \
@@ -115,10 +128,11 @@ for s in $STEPS; do
     tunebmf) run tune_bmf2 600 python3 tools/tune.py --config bmf --threads 168,256,336,448,512 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
             -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
-            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
+    pmc) # 12 steps: every launch carries bench.py's default 4 blocks (c2)
+         run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
-            -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
     pmc5) run pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run \
             -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run \

@@ -43,13 +43,15 @@ def main():
     ap.add_argument("--stats")
     ap.add_argument("--round", default="r01")
     ap.add_argument("--algorithmic-bytes", type=int, default=0)
+    ap.add_argument("--blocks-per-launch", type=int, default=1,
+                    help="integrations per integrate launch in the profiled run (bench.py's)")
     ap.add_argument("--kernel", default=KERNEL)
     a = ap.parse_args()
     f = counter(a.fetch, "FETCH_SIZE", a.kernel)
     w = counter(a.write, "WRITE_SIZE", a.kernel)
     fetch_kib, write_kib = statistics.median(f), statistics.median(w)
     hbm = int(fetch_kib * 1024 * 2 + write_kib * 1024)
-    alg = a.algorithmic_bytes or ALGORITHMIC.get(a.config, 0)
+    alg = a.algorithmic_bytes or ALGORITHMIC.get(a.config, 0) * a.blocks_per_launch
     fetch_dst = f"profiles/{a.round}_{a.config}_pmc_fetch.csv"
     write_dst = f"profiles/{a.round}_{a.config}_pmc_write.csv"
     out = {
@@ -61,6 +63,7 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 wide-stream under-count, MI355X_MICROARCH.md HBM)",
         "hbm_bytes_per_launch": hbm,
         "algorithmic_bytes_per_launch": alg or None,
+        "blocks_per_launch": a.blocks_per_launch,
         "traffic_over_algorithmic": round(hbm / alg, 4) if alg else None,
         "source": [fetch_dst, write_dst],
     }
