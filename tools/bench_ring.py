@@ -3,13 +3,16 @@
   paf_dfdb -R (replay producer) -> device ring (dada_db -g) ->
   paf_baseband2power (integrates the block in place) -> host ring -> paf_dbdisk
 
-on full-size BMF blocks (8192 frames x 48 chunks, 2.625 GiB).  The producer
+on full-size BMF blocks (8192 frames x 48 chunks, 2.625 GiB), or on
+configs[1]-shaped blocks (--layout int8:256, 1 GiB), where the replaying
+producer keeps blocks queued and the stage integrates them several per launch
+(b2p_integrate_n, b2p_blocks_per_launch).  The producer
 re-hands the ring's blocks without rewriting them, so the figure is what the
 consumer sustains through the ring: integrate launch + fences + semaphores +
 output block per integration.  "steady_*" leaves out the first 8 outputs
 (first-launch and producer start-up costs).  Prints one JSON line.
 
-  python tools/bench_ring.py [--blocks 200] [--ndf 8192]
+  python tools/bench_ring.py [--blocks 200] [--ndf 8192] [--layout int8:256 --nbufs 8]
 """
 from __future__ import annotations
 
@@ -36,11 +39,16 @@ def main():
     ap.add_argument("--blocks", type=int, default=200)
     ap.add_argument("--ndf", type=int, default=8192)
     ap.add_argument("--nbufs", type=int, default=4)
+    ap.add_argument("--layout", default="bmf", choices=["bmf", "int8:256"])
     ap.add_argument("--host", action="store_true",
                     help="host ring instead (the consumer copies every block H2D)")
     a = ap.parse_args()
-    bufsz = a.ndf * 48 * 7168
-    nout = 336
+    if a.layout == "bmf":
+        bufsz, nout = a.ndf * 48 * 7168, 336
+        samples = a.ndf * 128 * nout * 2  # channels x pols x time, as bench.py counts
+    else:  # 256 ch x 2 pol int8, 2^20 samples: configs[1]
+        bufsz, nout = 256 * 2 * 2 * (1 << 20), 256
+        samples = bufsz // 2
     kin, kout = 0x7e00, 0x7e10
     for k in (kin, kout):
         dada.destroy_ring(k)
@@ -53,10 +61,11 @@ def main():
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o",
                                    os.path.join(d, "power.dada")], stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
-                                   f"{kout:x}", "-c", d, "-d", "0", "-f", "bmf"],
+                                   f"{kout:x}", "-c", d, "-d", "0", "-f", a.layout],
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR,
-                                   "-R", str(a.blocks), "-f", "bmf"], stderr=subprocess.PIPE)]
+                                   "-R", str(a.blocks), "-f", a.layout] + (["-r", "20181105"] if a.layout != "bmf" else []),
+                                  stderr=subprocess.PIPE)]
         for p in procs:
             p.wait(timeout=600)
         wall = time.perf_counter() - t0
@@ -72,14 +81,17 @@ def main():
         m = re.search(r"FINISH PAF_PROCESS: (\d+) integrations.* ([0-9.]+) s from the first", log)
         steady = per[a.nbufs + 1:] or per
         med = statistics.median(steady) if steady else None  # the pipelined path logs no per-block time
-        samples = a.ndf * 128 * nout * 2  # channels x pols x time, as bench.py counts
+        launches = [int(x) for x in re.findall(r"launch \d+: (\d+) integration", log)]
         n_int, el = (int(m.group(1)), float(m.group(2))) if m else (0, 0.0)
         ms = re.search(r"([0-9.]+) s for the last (\d+)", log)
         el_s, n_s = (float(ms.group(1)), int(ms.group(2))) if ms else (0.0, 0)
         print(json.dumps({
             "path": ("host ring -> paf_baseband2power (pinned H2D, overlapped)" if a.host else
                      "device ring (dada_db -g) -> paf_baseband2power in place"),
+            "layout": a.layout, "nbufs": a.nbufs,
             "block_bytes": bufsz, "blocks": a.blocks, "integrations_logged": len(per),
+            "launches_logged": len(launches),
+            "max_blocks_per_launch_logged": max(launches) if launches else None,
             "consumer_ms_per_block_median": round(med, 3) if med else None,
             "ms_per_block": round(el / n_int * 1e3, 4) if n_int else None,
             "consumer_elapsed_s": el,

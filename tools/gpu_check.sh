@@ -6,7 +6,7 @@
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp
+#          benchbpl profbpl benchcmp ringq
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -71,6 +71,11 @@ for s in $STEPS; do
                 run cmp_bpl1_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 \
                   --blocks-per-launch 1 || exit $?
               done ;;
+    ringq) # configs[1] blocks through the device ring: 2 blocks (one per launch) vs 8 (batched)
+           run ring_q2 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 2 --blocks 400 &&
+           run ring_q8 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 400 &&
+           run ring_q2b 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 2 --blocks 400 &&
+           run ring_q8b 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 400 ;;
     profbpl) run prof_bpl4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bpl4" -o run \
             -- python3 bench.py --steps 48 --warmup 4 --cpu-seconds 0 --blocks-per-launch 4 ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
