@@ -231,3 +231,41 @@ def test_queued_blocks_are_integrated_in_one_launch(gpu, tmp_path):
     finally:
         dada.destroy_ring(kin)
         dada.destroy_ring(kout)
+
+
+def test_replaying_producer_keeps_the_stage_batching(gpu, tmp_path):
+    """paf_dfdb -R re-hands ring blocks faster than one launch per block
+    drains them: with every launch logged (B2P_TRACE_PIPELINE) the launches
+    add up to every block, several took more than one, none more than
+    b2p_blocks_per_launch allows within the ring (6 blocks: 5), and every
+    spectrum equals the oracle's of the block it read"""
+    import re
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    nbufs, nrep = 6, 60
+    kin, kout = fresh_key(), fresh_key()
+    dada.create_ring(kin, nbufs, g.block_bytes, device=0)
+    dada.create_ring(kout, 4, g.nout * 4)
+    try:
+        out = tmp_path / "power.dada"
+        env = dict(os.environ, B2P_TRACE_PIPELINE="1")
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}",
+                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", "int8:256"],
+                                  stderr=subprocess.PIPE, env=env),
+                 subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-R", str(nrep),
+                                   "-f", "int8:256", "-r", str(SEED)], stderr=subprocess.PIPE)]
+        _wait(procs)
+        _, data = dada.read_dada_file(str(out))
+        sp = data.view(np.float32).reshape(-1, g.nout)
+        assert sp.shape[0] == nrep
+        want = [co.power(g, co.fill_synthetic(g, g.block_bytes, SEED, 0, i)) for i in range(nbufs)]
+        for i in range(nrep):
+            assert np.array_equal(sp[i].view(np.uint32), want[i % nbufs].view(np.uint32))
+        log = open(str(tmp_path / "paf_baseband2power.log")).read()
+        launches = [int(n) for n in re.findall(r"launch \d+: (\d+) integration", log)]
+        assert sum(launches) == nrep and max(launches) <= nbufs - 1, launches
+        assert sum(n > 1 for n in launches) >= 2, launches
+    finally:
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
