@@ -127,6 +127,44 @@ PROTOCOL = {
                      ["ipcbuf_mark_cleared", "0x404c11"], ["ipcbuf_reset", "0x404df8"],
                      ["ipcbuf_unlock_read", "0x404616"], ["ipcbuf_unlock_read", "0x404639"]],
     },
+    "view_protocol": {
+        "open": "ipcio_open 'r': no lock, rdwrt = 'r'; ipcio_read / open_block_read accept "
+                "(rdwrt & ~0x20) == 'R'; only 'R' calls mark_cleared",
+        "first_view": "VIEWER -> VIEWING: xfer = r_xfers[0] % 8, viewbuf = s_buf[xfer]; "
+                      "w_buf > s_buf + 1 ? viewbuf = w_buf - 1 (the newest block), start 0 : "
+                      "start = s_byte[xfer]",
+        "next": "while w_buf <= viewbuf: eod[xfer] && r_bufs[0] && r_bufs[0] == e_buf[xfer] "
+                "-> VSTOP, else float_sleep(0.1); viewbuf + nbufs < w_buf -> viewbuf = "
+                "w_buf - nbufs + 1 (lapped); block = viewbuf++",
+        "evidence": [["ipcio_open", "0x405a48"], ["ipcbuf_get_next_read_work", "0x404880"],
+                     ["ipcbuf_get_next_read_work", "0x4048f4"],
+                     ["ipcbuf_get_next_read_work", "0x4048c0"],
+                     ["ipcbuf_get_next_read_work", "0x40479d"],
+                     ["ipcbuf_get_next_read_work", "0x404820"], ["ipcio_read", "0x406776"]],
+    },
+    "deferred_start": {
+        "open": "ipcio_open 'w': lock_write + disable_sod (WRITER: mark_filled only w_buf++)",
+        "start": "ipcio_start(byte) needs rdwrt 'w': sod_pending = 1, rdwrt = 'W', sod_buf = "
+                 "byte / bufsz, sod_byte = byte % bufsz, then check_pending_sod",
+        "check_pending_sod": "sod_pending && w_buf > sod_buf -> enable_sod(sod_buf, sod_byte), "
+                             "sod_pending = 0",
+        "stop_close": "'W' writing: enable_eod, mark_filled(bytes), check_pending_sod, "
+                      "marked_filled = 1, curbuf = 0 if bytes == bufsz; rdwrt = 'w'; unlock: "
+                      "w_xfer ? w_buf = e_buf[(w_xfer-1) % 8] + 1, unlock_write",
+        "evidence": [["ipcio_open", "0x405a19"], ["ipcio_start", "0x405bb8"],
+                     ["ipcio_check_pending_sod", "0x405b5a"], ["ipcio_stop_close", "0x405c81"],
+                     ["ipcio_stop", "0x405ddb"], ["ipcio_close", "0x405e10"]],
+    },
+    "resets": {
+        "reset_writer": "writer with w_buf > 0: CLEAR -1 per reader for every count[], SODACK and "
+                        "EODACK -8 then +8 per reader, r_bufs = r_xfers = 0, w_buf = w_xfer = 0, "
+                        "eod[] = 1",
+        "hard_reset": "w_buf = w_xfer = 0, eod[] = 1, per reader r_bufs = r_xfers = 0 and "
+                      "semctl SETVAL 0 of FULL and CLEAR (count[] untouched)",
+        "evidence": [["ipcbuf_reset", "0x404d60"], ["ipcbuf_reset", "0x404e43"],
+                     ["ipcbuf_reset", "0x404d98"], ["ipcbuf_hard_reset", "0x40501f"],
+                     ["ipcbuf_hard_reset", "0x404fdd"]],
+    },
     "device_blocks": {
         "what": "on_device_id >= 0: block ibuf's segment at shmkey[ibuf] holds a 64-B IPC memory "
                 "handle (ipc_alloc_cuda: shmget(key, 64); creator allocates and publishes the "
