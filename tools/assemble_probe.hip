@@ -76,8 +76,7 @@ __global__ void __launch_bounds__(512) copy_kernel(const unsigned char *dfs, uns
 #pragma unroll
       for (int k = 0; k < 7; ++k) store16<POL>(dst + k * 64 + lane, v[k]);
       if (dn >= ndf) break;
-#pragma unroll
-      for (int k = 0; k < 7; ++k) v[k] = w[k];
+      for (int k = 0; k < 7; ++k) v[k] = w[k];  // register moves: no unroll pragma needed
       d = dn;
     }
     return;
