@@ -280,6 +280,8 @@ typedef struct shared_t {
   int have[MAX_SUB]; /* this round: 1 whole block, 0 partial, -1 end of data */
   int failed;
   uint64_t nblocks, nskipped;
+  uint64_t nlaunches; /* device ring: integrate launches, several queued blocks each at most */
+  uint32_t max_batch;
   double t_first, t_last; /* first integration started, last output written */
   double t_warm;          /* output kWarm written: start of the steady-state span */
   /* time split (-t): the block every member takes its share of */
@@ -456,6 +458,8 @@ static void run_device_pipelined(shared_t *sh) {
       if (rc == B2P_OK) {
         next += n;
         k++;
+        sh->nlaunches = k;
+        if (n > sh->max_batch) sh->max_batch = n;
         if (getenv("B2P_TRACE_PIPELINE") || k % 64 == 1)
           multilog(sh->log, LOG_INFO, "launch %" PRIu64 ": %u integration(s) from %" PRIu64 ", %.3f ms in "
                    "the loop body, %.3f ms since the first", k, n, b->first + 1, (now_s() - t0) * 1e3,
@@ -908,6 +912,9 @@ done:
   free(sh.spec_host);
   dada_hdu_destroy(out);
   if (g_stop) multilog(log, LOG_INFO, "stopped by a signal between blocks; output transfer ended");
+  if (sh.nlaunches)
+    multilog(log, LOG_INFO, "%" PRIu64 " integrate launches for %" PRIu64 " integrations, up to %u queued "
+             "blocks per launch", sh.nlaunches, sh.nblocks, sh.max_batch);
   multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s, "
            "%.6f s from the first integration to the last output, %.6f s for the last %" PRIu64,
            sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED",

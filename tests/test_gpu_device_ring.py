@@ -228,6 +228,7 @@ def test_queued_blocks_are_integrated_in_one_launch(gpu, tmp_path):
             assert np.array_equal(sp[i].view(np.uint32), co.power(g, payload[i]).view(np.uint32))
         log = open(str(tmp_path / "paf_baseband2power.log")).read()
         assert "launch 1: 7 integration(s) from 1" in log
+        assert "1 integrate launches for 7 integrations, up to 7 queued blocks per launch" in log
     finally:
         dada.destroy_ring(kin)
         dada.destroy_ring(kout)
