@@ -269,6 +269,10 @@ int b2p_group_open(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode);
  * B2P_EHIP instead of hanging.  b2p_group_open uses 60 000 ms. */
 int b2p_group_open_timed(b2p_group_t **grp, b2p_ctx_t *const *ctxs, int n, int mode, int timeout_ms);
 int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);
+/* nspec consecutive spectra per member (e.g. one b2p_integrate_n batch) in
+ * one collective; root_out is member-major: member r's nspec x nout floats
+ * at r * nspec * nout.  b2p_group_gather is nspec = 1. */
+int b2p_group_gather_n(b2p_group_t *grp, float *const *spectra, uint32_t nspec, float *root_out);
 /* Time-split mode (second mode): member r integrated its share
  * of ONE sub-band's samples and emitted exact sums with
  * b2p_finish_partial_async; sums[r] holds `count` uint64 on member r's

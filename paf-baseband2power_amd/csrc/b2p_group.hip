@@ -215,19 +215,25 @@ int b2p_group_open_timed(b2p_group_t **out, b2p_ctx_t *const *ctxs, int n, int m
 }
 
 int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
-  if (!g || !spectra || !root_out) return B2P_EINVAL;
+  return b2p_group_gather_n(g, spectra, 1, root_out);
+}
+
+// nspec consecutive spectra per member in one collective: root_out holds
+// member r's nspec x nout floats at r * nspec * nout (member-major)
+int b2p_group_gather_n(b2p_group_t *g, float *const *spectra, uint32_t nspec, float *root_out) {
+  if (!g || !spectra || !root_out || nspec < 1) return B2P_EINVAL;
   if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_gather", "group aborted earlier; close it");
   // every member's deferred finalize must be enqueued before the gather
   for (int r = 0; r < g->n; ++r) {
     int rc = b2p_internal_flush(g->ctx[r]);
     if (rc != B2P_OK) return gerr(g, rc, "flush", b2p_last_error(g->ctx[r]));
   }
-  const size_t bytes = (size_t)g->nout * sizeof(float);
+  const size_t count = (size_t)g->nout * nspec, bytes = count * sizeof(float);
   if (g->mode == 0) {
     ncclResult_t nr = ncclGroupStart();
     for (int r = 0; r < g->n && nr == ncclSuccess; ++r) {
       (void)hipSetDevice(g->dev[r]);
-      nr = ncclGather(spectra[r], r == 0 ? root_out : nullptr, g->nout, ncclFloat32, 0, g->comm[r],
+      nr = ncclGather(spectra[r], r == 0 ? root_out : nullptr, count, ncclFloat32, 0, g->comm[r],
                       g->stream[r]);
     }
     ncclResult_t ne = ncclGroupEnd();
@@ -243,7 +249,7 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
   (void)hipSetDevice(g->dev[0]);
   for (int r = 0; r < g->n; ++r) {
     if (hipStreamWaitEvent(g->stream[0], g->done[r], 0) != hipSuccess ||
-        hipMemcpyPeerAsync(root_out + (size_t)r * g->nout, g->dev[0], spectra[r], g->dev[r], bytes,
+        hipMemcpyPeerAsync(root_out + (size_t)r * count, g->dev[0], spectra[r], g->dev[r], bytes,
                            g->stream[0]) != hipSuccess)
       return gerr(g, B2P_EHIP, "hipMemcpyPeerAsync", "");
   }

@@ -273,11 +273,17 @@ typedef struct shared_t {
   multilog_t *log;
   dada_hdu_t *out;
   b2p_group_t *grp;
-  float *root_dev;  /* nsub*nout on sub[0]'s device */
-  float *spec_host; /* nsub*nout, pinned */
+  float *root_dev;  /* nsub*nout on sub[0]'s device (x bmax when gathering batches) */
+  float *spec_host; /* nsub*nout, pinned (x bmax when gathering batches) */
+  float *stage;     /* gathered batches: one output block reordered member by member */
   uint64_t nout, obytes;
   pthread_barrier_t bar;
   int have[MAX_SUB]; /* this round: 1 whole block, 0 partial, -1 end of data */
+  /* gathered batches (device rings): blocks each member has queued, whole
+   * blocks it took, and whether its batch ended at a partial block */
+  int avail[MAX_SUB], got[MAX_SUB], partial[MAX_SUB];
+  uint32_t bmax;
+  int gather_dev; /* every sub-band on a GPU-resident ring: worker_gather_dev */
   int failed;
   uint64_t nblocks, nskipped;
   uint64_t nlaunches; /* device ring: integrate launches, several queued blocks each at most */
@@ -388,6 +394,121 @@ static void *worker(void *arg) {
 }
 
 #if DEVICE_RINGS
+/* nsub > 1 sub-bands on GPU-resident rings, gathered.  Each round every
+ * member integrates the same number m of its blocks in one launch --
+ * m = the fewest whole blocks any member has queued, up to sh->bmax
+ * (b2p_blocks_per_launch) -- and the root gathers the m spectra of every
+ * member in one collective (b2p_group_gather_n) and writes m output
+ * blocks.  With one block per round the round's fixed cost (syncs, two
+ * barriers, the gather, the output) held two sub-bands sharing one GPU to
+ * 4.4 TB/s when the producers ran ahead (tools/bench_ring.py --nsub 2);
+ * now it is paid once per m integrations.  A real-time stream gives m = 1,
+ * the rounds of the unbatched worker.  A member whose transfer ends (a
+ * partial block) ends the round at the blocks every member has whole; the
+ * rest are released unintegrated and counted as one skipped integration. */
+static void *worker_gather_dev(void *arg) {
+  worker_t *w = (worker_t *)arg;
+  shared_t *sh = w->sh;
+  const int r = w->r;
+  sub_t *s = &sh->sub[r];
+  ipcio_t *in = s->in->data_block;
+  const size_t nfl = sh->obytes / sizeof(float) / (size_t)sh->nsub; /* floats per member spectrum */
+  if (sh->bmax > 1 && ipcbuf_set_read_depth(&in->buf, (int)sh->bmax) < 0) {
+    multilog(sh->log, LOG_ERR, "sub-band %d: read depth %u refused", r, sh->bmax);
+    sh->failed = 1;
+  }
+  for (;;) {
+    const void *blks[B2P_MAX_BLOCKS];
+    uint64_t bytes = 0, bid = 0;
+    char *blk = g_stop || sh->failed ? NULL : next_block(s->in, &bytes);
+    int taken = blk ? 1 : 0, avail = 0;
+    sh->have[r] = !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
+    if (sh->have[r] == 1) {
+      blks[0] = blk;
+      const uint64_t q = ipcbuf_get_nfull_iread(&in->buf, in->buf.iread);
+      avail = 1 + (int)(q < sh->bmax - 1 ? q : sh->bmax - 1);
+    }
+    sh->avail[r] = avail;
+    pthread_barrier_wait(&sh->bar); /* every member knows what it holds */
+    int stop = sh->failed, skip = 0, n = (int)sh->bmax;
+    for (int q = 0; q < sh->nsub; q++) {
+      if (sh->have[q] < 0) stop = 1;
+      if (sh->have[q] == 0) skip = 1;
+      if (sh->avail[q] < n) n = sh->avail[q];
+    }
+    int m = stop || skip ? 0 : 1, part = 0;
+    for (int j = 1; !stop && !skip && j < n; j++) { /* queued: no wait */
+      uint64_t b = 0;
+      char *p = ipcio_open_block_read(in, &b, &bid);
+      if (!p) break;
+      taken++;
+      if (b != s->rbufsz) { /* this sub-band's transfer ends here */
+        part = b != 0;
+        break;
+      }
+      blks[m++] = p;
+    }
+    sh->got[r] = m;
+    sh->partial[r] = part;
+    pthread_barrier_wait(&sh->bar); /* every member's batch is known */
+    int mm = m;
+    for (int q = 0; q < sh->nsub; q++)
+      if (sh->got[q] < mm) mm = sh->got[q];
+    const double t0 = now_s();
+    if (r == 0 && mm && sh->t_first == 0) sh->t_first = t0;
+    int rc = B2P_OK;
+    if (mm) {
+      rc = mm == 1 ? b2p_integrate(s->ctx, blks[0], s->rbufsz, 1, s->spec_dev, 1)
+                   : b2p_integrate_n(s->ctx, blks, (uint32_t)mm, s->spec_dev, 1);
+      if (rc == B2P_OK) rc = b2p_sync(s->ctx); /* done with the blocks */
+      if (rc != B2P_OK) {
+        multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", r, b2p_strerror(rc), b2p_last_error(s->ctx));
+        sh->failed = 1;
+      }
+    }
+    for (int j = 0; j < taken; j++) ipcio_close_block_read(in, 0); /* oldest first */
+    pthread_barrier_wait(&sh->bar); /* every spectrum of this round is on its device */
+    if (r == 0) {
+      int lost = skip && !stop;
+      for (int q = 0; q < sh->nsub; q++) lost |= sh->got[q] > mm || sh->partial[q];
+      if (lost) {
+        sh->nskipped++;
+        multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
+      }
+      if (!sh->failed && mm) {
+        float *specs[MAX_SUB];
+        for (int q = 0; q < sh->nsub; q++) specs[q] = sh->sub[q].spec_dev;
+        rc = b2p_group_gather_n(sh->grp, specs, (uint32_t)mm, sh->root_dev);
+        if (rc == B2P_OK) rc = b2p_group_sync(sh->grp);
+        if (rc == B2P_OK) rc = b2p_memcpy(s->ctx, sh->spec_host, sh->root_dev, (size_t)mm * sh->obytes, 2);
+        if (rc != B2P_OK) {
+          multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
+          sh->failed = 1;
+        }
+        for (int j = 0; !sh->failed && j < mm; j++) { /* member-major -> one block per integration */
+          for (int q = 0; q < sh->nsub; q++)
+            memcpy(sh->stage + (size_t)q * nfl, sh->spec_host + ((size_t)q * (size_t)mm + (size_t)j) * nfl,
+                   nfl * sizeof(float));
+          if (write_output(sh, sh->stage) < 0) sh->failed = 1;
+        }
+        if (!sh->failed) {
+          sh->nlaunches++;
+          if ((uint32_t)mm > sh->max_batch) sh->max_batch = (uint32_t)mm;
+          const double dt = sh->t_last - t0;
+          if (getenv("B2P_TRACE_PIPELINE") || sh->nlaunches % 64 == 1)
+            multilog(sh->log, LOG_INFO, "round %" PRIu64 ": %d integration(s) per sub-band in %.3f ms, "
+                     "%.1f Msamples/s in all", sh->nlaunches, mm, dt * 1e3,
+                     (double)mm * sh->nsub * (double)(nfl / s->g.npol_out) * s->g.npol *
+                         (double)s->g.nsamp_int / dt / 1e6);
+        }
+      }
+    }
+    pthread_barrier_wait(&sh->bar);
+    if (sh->failed || stop) break;
+  }
+  return NULL;
+}
+
 /* One sub-band on a GPU-resident ring, launches kept in flight.  Batch k's
  * launch is enqueued before batch k-1's blocks are released, so the GPU
  * never waits on the host between launches; batch k-1 goes back to the ring
@@ -810,10 +931,27 @@ int main(int argc, char *argv[]) {
     if (ipcbuf_mark_filled(out->header_block, ohsz) < 0) goto done;
   }
 
+  sh.bmax = 1;
+#if DEVICE_RINGS
+  if (!split && conf.nsub > 1 && !getenv("B2P_NO_PIPELINE")) { /* gathered batches (worker_gather_dev) */
+    int all_dev = 1;
+    uint64_t nb = UINT64_MAX;
+    for (int r = 0; r < conf.nsub; r++) {
+      all_dev &= sub[r].ondev;
+      const uint64_t x = ipcbuf_get_nbufs(&sub[r].in->data_block->buf);
+      if (x < nb) nb = x;
+    }
+    const uint32_t want = b2p_blocks_per_launch(sub[0].rbufsz);
+    sh.gather_dev = all_dev;
+    if (all_dev) sh.bmax = nb < want ? (uint32_t)nb : want;
+    if (!sh.bmax) sh.bmax = 1;
+  }
+#endif
   {
-    const size_t hb = (sh.obytes + 4095) / 4096 * 4096;
+    const size_t hb = (sh.bmax * sh.obytes + 4095) / 4096 * 4096;
     sh.spec_host = aligned_alloc(4096, hb);
-    if (!sh.spec_host) goto done;
+    sh.stage = malloc(sh.obytes);
+    if (!sh.spec_host || !sh.stage) goto done;
     b2p_register_host(sub[0].ctx, sh.spec_host, hb);
   }
   if (split) {
@@ -837,9 +975,9 @@ int main(int argc, char *argv[]) {
              mode ? "peer copies (shared device)" : "RCCL ncclReduce");
   } else if (conf.nsub > 1) {
     for (int r = 0; r < conf.nsub; r++)
-      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, info.nout * sizeof(float)) != B2P_OK)
+      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, sh.bmax * info.nout * sizeof(float)) != B2P_OK)
         goto done;
-    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, sh.obytes) != B2P_OK) goto done;
+    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, sh.bmax * sh.obytes) != B2P_OK) goto done;
     b2p_ctx_t *ctxs[MAX_SUB];
     for (int r = 0; r < conf.nsub; r++) ctxs[r] = sub[r].ctx;
     const int mode = group_mode(&conf, dup_dev, log);
@@ -850,8 +988,9 @@ int main(int argc, char *argv[]) {
               b2p_group_last_error(NULL));
       goto done;
     }
-    multilog(log, LOG_INFO, "gather of %d sub-bands to GPU %d via %s", conf.nsub, sub[0].device,
-             mode ? "peer copies (shared device)" : "RCCL ncclGather");
+    multilog(log, LOG_INFO, "gather of %d sub-bands to GPU %d via %s%s", conf.nsub, sub[0].device,
+             mode ? "peer copies (shared device)" : "RCCL ncclGather",
+             sh.gather_dev ? ", queued blocks in rounds of up to b2p_blocks_per_launch" : "");
   }
 
   {
@@ -869,7 +1008,12 @@ int main(int argc, char *argv[]) {
     for (int r = 0; r < nmem; r++) {
       wk[r].sh = &sh;
       wk[r].r = r;
-      pthread_create(&th[r], NULL, split ? worker_split : worker, &wk[r]);
+#if DEVICE_RINGS
+      void *(*fn)(void *) = split ? worker_split : sh.gather_dev ? worker_gather_dev : worker;
+#else
+      void *(*fn)(void *) = split ? worker_split : worker;
+#endif
+      pthread_create(&th[r], NULL, fn, &wk[r]);
     }
     /* join by polling, so a stop request can wake workers that wait on a ring */
     int joined[MAX_SUB] = {0}, left = nmem;
@@ -910,11 +1054,13 @@ done:
     free(s->hdr);
   }
   free(sh.spec_host);
+  free(sh.stage);
   dada_hdu_destroy(out);
   if (g_stop) multilog(log, LOG_INFO, "stopped by a signal between blocks; output transfer ended");
   if (sh.nlaunches)
-    multilog(log, LOG_INFO, "%" PRIu64 " integrate launches for %" PRIu64 " integrations, up to %u queued "
-             "blocks per launch", sh.nlaunches, sh.nblocks, sh.max_batch);
+    multilog(log, LOG_INFO, "%" PRIu64 " integrate %s for %" PRIu64 " integrations%s, up to %u queued "
+             "blocks per launch", sh.nlaunches, sh.gather_dev ? "rounds" : "launches", sh.nblocks,
+             sh.gather_dev ? " per sub-band" : "", sh.max_batch);
   multilog(log, LOG_INFO, "FINISH PAF_PROCESS: %" PRIu64 " integrations, %" PRIu64 " skipped, %s, "
            "%.6f s from the first integration to the last output, %.6f s for the last %" PRIu64,
            sh.nblocks, sh.nskipped, status == EXIT_SUCCESS ? "ok" : "FAILED",

@@ -270,3 +270,47 @@ def test_replaying_producer_keeps_the_stage_batching(gpu, tmp_path):
     finally:
         dada.destroy_ring(kin)
         dada.destroy_ring(kout)
+
+
+def test_gathered_replays_in_batches(gpu, tmp_path):
+    """paf_baseband2power -n 2 on two GPU-resident rings fed by replaying
+    producers: every round integrates the same number of queued blocks per
+    sub-band in one launch each and gathers them in one collective
+    (b2p_group_gather_n); rounds add up to every block, several took more
+    than one, and every output block holds both sub-bands' spectra of the
+    blocks they read, equal to the oracle's"""
+    import re
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    nbufs, nrep, nsub = 6, 40, 2
+    base, kout = fresh_key(), fresh_key()
+    kins = [base + 0x10 * q for q in range(nsub)]
+    for k in kins:
+        dada.destroy_ring(k)
+        dada.create_ring(k, nbufs, g.block_bytes, device=0)
+    dada.create_ring(kout, 4, nsub * g.nout * 4)
+    try:
+        out = tmp_path / "power.dada"
+        env = dict(os.environ, B2P_TRACE_PIPELINE="1")
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{base:x}", "-b", f"{kout:x}",
+                                   "-c", str(tmp_path), "-d", "0", "-f", "int8:256", "-n", str(nsub)],
+                                  stderr=subprocess.PIPE, env=env)]
+        procs += [subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{k:x}", "-b", HDR, "-R", str(nrep),
+                                    "-f", "int8:256", "-r", str(SEED + q)], stderr=subprocess.PIPE)
+                  for q, k in enumerate(kins)]
+        _wait(procs)
+        _, data = dada.read_dada_file(str(out))
+        sp = data.view(np.float32).reshape(-1, nsub, g.nout)
+        assert sp.shape[0] == nrep
+        want = [[co.power(g, co.fill_synthetic(g, g.block_bytes, SEED + q, 0, i)) for i in range(nbufs)]
+                for q in range(nsub)]
+        for i in range(nrep):
+            for q in range(nsub):
+                assert np.array_equal(sp[i, q].view(np.uint32), want[q][i % nbufs].view(np.uint32)), (i, q)
+        log = open(str(tmp_path / "paf_baseband2power.log")).read()
+        rounds = [int(n) for n in re.findall(r"round \d+: (\d+) integration", log)]
+        assert sum(rounds) == nrep and max(rounds) > 1, rounds
+    finally:
+        for k in kins + [kout]:
+            dada.destroy_ring(k)

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--ndf", type=int, default=8192)
     ap.add_argument("--nbufs", type=int, default=4)
     ap.add_argument("--layout", default="bmf", choices=["bmf", "int8:256"])
+    ap.add_argument("--nsub", type=int, default=1,
+                    help="sub-bands served by one stage (-n N: rings key + 0x10*r, spectra gathered)")
     ap.add_argument("--host", action="store_true",
                     help="host ring instead (the consumer copies every block H2D)")
     a = ap.parse_args()
@@ -49,23 +51,27 @@ def main():
     else:  # 256 ch x 2 pol int8, 2^20 samples: configs[1]
         bufsz, nout = 256 * 2 * 2 * (1 << 20), 256
         samples = bufsz // 2
-    kin, kout = 0x7e00, 0x7e10
-    for k in (kin, kout):
+    kin, kout = 0x7e00, 0x7f00
+    kins = [kin + 0x10 * r for r in range(a.nsub)]
+    for k in kins + [kout]:
         dada.destroy_ring(k)
     d = tempfile.mkdtemp(prefix="bench_ring_")
-    dada.create_ring(kin, a.nbufs, bufsz, device=-1 if a.host else 0)
-    dada.create_ring(kout, 8, nout * 4)
+    for k in kins:
+        dada.create_ring(k, a.nbufs, bufsz, device=-1 if a.host else 0)
+    dada.create_ring(kout, 8, a.nsub * nout * 4)
     procs = []
     try:
         t0 = time.perf_counter()
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o",
                                    os.path.join(d, "power.dada")], stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
-                                   f"{kout:x}", "-c", d, "-d", "0", "-f", a.layout],
-                                  stderr=subprocess.PIPE),
-                 subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR,
-                                   "-R", str(a.blocks), "-f", a.layout] + (["-r", "20181105"] if a.layout != "bmf" else []),
+                                   f"{kout:x}", "-c", d, "-d", "0", "-f", a.layout]
+                                  + (["-n", str(a.nsub)] if a.nsub > 1 else []),
                                   stderr=subprocess.PIPE)]
+        procs += [subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{k:x}", "-b", HDR,
+                                    "-R", str(a.blocks), "-f", a.layout]
+                                   + (["-r", "20181105"] if a.layout != "bmf" else []), stderr=subprocess.PIPE)
+                  for k in kins]
         for p in procs:
             p.wait(timeout=600)
         wall = time.perf_counter() - t0
@@ -88,19 +94,19 @@ def main():
         print(json.dumps({
             "path": ("host ring -> paf_baseband2power (pinned H2D, overlapped)" if a.host else
                      "device ring (dada_db -g) -> paf_baseband2power in place"),
-            "layout": a.layout, "nbufs": a.nbufs,
+            "layout": a.layout, "nbufs": a.nbufs, "nsub": a.nsub,
             "block_bytes": bufsz, "blocks": a.blocks, "integrations_logged": len(per),
             "launches_logged": len(launches),
             "max_blocks_per_launch_logged": max(launches) if launches else None,
             "consumer_ms_per_block_median": round(med, 3) if med else None,
             "ms_per_block": round(el / n_int * 1e3, 4) if n_int else None,
             "consumer_elapsed_s": el,
-            "ring_Msamples_s": round(n_int * samples / el / 1e6, 1) if el else None,
-            "ring_GBps": round(n_int * bufsz / el / 1e9, 1) if el else None,
+            "ring_Msamples_s": round(a.nsub * n_int * samples / el / 1e6, 1) if el else None,
+            "ring_GBps": round(a.nsub * n_int * bufsz / el / 1e9, 1) if el else None,
             "steady_blocks": n_s,
             "steady_ms_per_block": round(el_s / n_s * 1e3, 4) if n_s else None,
-            "steady_Msamples_s": round(n_s * samples / el_s / 1e6, 1) if n_s else None,
-            "steady_GBps": round(n_s * bufsz / el_s / 1e9, 1) if n_s else None,
+            "steady_Msamples_s": round(a.nsub * n_s * samples / el_s / 1e6, 1) if n_s else None,
+            "steady_GBps": round(a.nsub * n_s * bufsz / el_s / 1e9, 1) if n_s else None,
             "wall_s_incl_startup": round(wall, 2),
         }), flush=True)
         return 0
@@ -109,8 +115,8 @@ def main():
             if p.poll() is None:
                 p.kill()
                 p.wait()
-        dada.destroy_ring(kin)
-        dada.destroy_ring(kout)
+        for k in kins + [kout]:
+            dada.destroy_ring(k)
 
 
 if __name__ == "__main__":

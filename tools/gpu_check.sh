@@ -6,7 +6,7 @@
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq
+#          benchbpl profbpl benchcmp ringq ringn
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -76,6 +76,9 @@ for s in $STEPS; do
            run ring_q8 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 400 &&
            run ring_q2b 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 2 --blocks 400 &&
            run ring_q8b 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 400 ;;
+    ringn) # one stage serving 2 sub-bands (-n 2, gathered) vs one, configs[1] blocks, one GPU
+           run ring_n1 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 200 &&
+           run ring_n2 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 200 --nsub 2 ;;
     profbpl) run prof_bpl4 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_bpl4" -o run \
             -- python3 bench.py --steps 48 --warmup 4 --cpu-seconds 0 --blocks-per-launch 4 ;;
     bench3) run bench_c3 600 python3 bench.py --config c3 --steps 4 --warmup 1 --cpu-seconds 0 ;;
