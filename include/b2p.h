@@ -273,6 +273,18 @@ int b2p_group_gather(b2p_group_t *grp, float *const *spectra, float *root_out);
  * one collective; root_out is member-major: member r's nspec x nout floats
  * at r * nspec * nout.  b2p_group_gather is nspec = 1. */
 int b2p_group_gather_n(b2p_group_t *grp, float *const *spectra, uint32_t nspec, float *root_out);
+/* The same gather for consumers that keep launches in flight: member r's
+ * spectra are read once its fence ticket tickets[r] has passed (b2p_fence
+ * after the launch that finalizes them -- with b2p_integrate[_n] that is
+ * the NEXT launch, or b2p_sync), on streams of the group's own, so neither
+ * the members' streams nor their pending finalizes are touched.  host_out
+ * (pinned, optional) receives root_out (nspec x nout x members floats)
+ * behind the gather.  *gticket is for b2p_group_wait; up to 8 gathers may be
+ * outstanding.  Call from one thread; the members' threads may keep
+ * launching meanwhile. */
+int b2p_group_gather_async(b2p_group_t *grp, float *const *spectra, uint32_t nspec, float *root_out,
+                           const uint64_t *tickets, float *host_out, uint64_t *gticket);
+int b2p_group_wait(b2p_group_t *grp, uint64_t gticket); /* bounded by the group's time limit */
 /* Time-split mode (second mode): member r integrated its share
  * of ONE sub-band's samples and emitted exact sums with
  * b2p_finish_partial_async; sums[r] holds `count` uint64 on member r's

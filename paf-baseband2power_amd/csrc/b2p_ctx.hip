@@ -701,6 +701,11 @@ uint64_t b2p_samples_pending(const b2p_ctx_t *c) { return c ? c->samples : 0; }
 
 void *b2p_internal_stream(b2p_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
 
+void *b2p_internal_fence_event(b2p_ctx_t *c, uint64_t ticket) {
+  if (!c || ticket >= c->fence_next || c->fence_next - ticket > 8) return nullptr;
+  return (void *)c->fence_ev[ticket % 8];
+}
+
 int b2p_internal_flush(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
   LIVE(c);  // a group collective over a failed member reports it

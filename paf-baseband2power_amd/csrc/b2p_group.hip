@@ -31,6 +31,11 @@ struct b2p_group {
   std::vector<hipStream_t> stream;
   std::vector<ncclComm_t> comm;
   std::vector<hipEvent_t> done;  // mode 1: member r's spectrum is final
+  // b2p_group_gather_async: the group's own streams (not the members'), and
+  // one event per issued gather (ring of 8), waited on by b2p_group_wait
+  std::vector<hipStream_t> gstream;
+  hipEvent_t gev[8] = {};
+  uint64_t gnext = 0;
   unsigned long long *scratch = nullptr;  // mode 1 reduce: rows gathered on the root
   uint64_t scratch_count = 0;
   uint32_t nout = 0;
@@ -256,6 +261,104 @@ int b2p_group_gather_n(b2p_group_t *g, float *const *spectra, uint32_t nspec, fl
   return B2P_OK;
 }
 
+// Gather behind the members' fences, on streams of the group's own: the
+// members' next launches are not held behind the collective, and their
+// pending finalizes are left to ride those launches.
+int b2p_group_gather_async(b2p_group_t *g, float *const *spectra, uint32_t nspec, float *root_out,
+                           const uint64_t *tickets, float *host_out, uint64_t *gticket) {
+  if (!g || !spectra || !root_out || !tickets || !gticket || nspec < 1) return B2P_EINVAL;
+  if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_gather_async", "group aborted earlier; close it");
+  if (g->gnext >= 8) {  // the event of gather gnext - 8 is recorded again: it must have completed
+    (void)hipSetDevice(g->dev[0]);
+    if (hipEventSynchronize(g->gev[g->gnext % 8]) != hipSuccess)
+      return gerr(g, B2P_EHIP, "hipEventSynchronize", "");
+  }
+  if (g->gstream.empty()) {
+    g->gstream.assign(g->n, nullptr);
+    for (int r = 0; r < g->n; ++r) {
+      (void)hipSetDevice(g->dev[r]);
+      if (hipStreamCreateWithFlags(&g->gstream[r], hipStreamNonBlocking) != hipSuccess)
+        return gerr(g, B2P_EHIP, "hipStreamCreate", "");
+    }
+  }
+  for (int r = 0; r < g->n; ++r) {
+    hipEvent_t e = (hipEvent_t)b2p_internal_fence_event(g->ctx[r], tickets[r]);
+    if (!e) return gerr(g, B2P_EINVAL, "b2p_group_gather_async", "a member's ticket is not one of its last 8");
+    (void)hipSetDevice(g->dev[r]);
+    // mode 1 copies on the root's group stream: it waits for every member
+    if (hipStreamWaitEvent(g->gstream[g->mode == 0 ? r : 0], e, 0) != hipSuccess)
+      return gerr(g, B2P_EHIP, "hipStreamWaitEvent", "");
+  }
+  const size_t count = (size_t)g->nout * nspec, bytes = count * sizeof(float);
+  if (g->mode == 0) {
+    ncclResult_t nr = ncclGroupStart();
+    for (int r = 0; r < g->n && nr == ncclSuccess; ++r) {
+      (void)hipSetDevice(g->dev[r]);
+      nr = ncclGather(spectra[r], r == 0 ? root_out : nullptr, count, ncclFloat32, 0, g->comm[r],
+                      g->gstream[r]);
+    }
+    ncclResult_t ne = ncclGroupEnd();
+    if ((nr != ncclSuccess && nr != ncclInProgress) || (ne != ncclSuccess && ne != ncclInProgress))
+      return gerr(g, B2P_EHIP, "ncclGather", ncclGetErrorString(nr != ncclSuccess ? nr : ne));
+    int rc = settle_comms(g, now_s() + 1e-3 * g->timeout_ms, "ncclGather enqueue");
+    if (rc != B2P_OK) return rc;
+  } else {
+    (void)hipSetDevice(g->dev[0]);
+    for (int r = 0; r < g->n; ++r)
+      if (hipMemcpyPeerAsync(root_out + (size_t)r * count, g->dev[0], spectra[r], g->dev[r], bytes,
+                             g->gstream[0]) != hipSuccess)
+        return gerr(g, B2P_EHIP, "hipMemcpyPeerAsync", "");
+  }
+  (void)hipSetDevice(g->dev[0]);
+  if (host_out && hipMemcpyAsync(host_out, root_out, bytes * g->n, hipMemcpyDeviceToHost, g->gstream[0]) !=
+                      hipSuccess)
+    return gerr(g, B2P_EHIP, "hipMemcpyAsync", "");
+  const int slot = (int)(g->gnext % 8);
+  if (!g->gev[slot] && hipEventCreateWithFlags(&g->gev[slot], hipEventDisableTiming) != hipSuccess)
+    return gerr(g, B2P_EHIP, "hipEventCreate", "");
+  if (hipEventRecord(g->gev[slot], g->gstream[0]) != hipSuccess) return gerr(g, B2P_EHIP, "hipEventRecord", "");
+  *gticket = g->gnext++;
+  return B2P_OK;
+}
+
+// Wait for one b2p_group_gather_async (polled against the group's limit)
+int b2p_group_wait(b2p_group_t *g, uint64_t gticket) {
+  if (!g || gticket >= g->gnext) return B2P_EINVAL;
+  if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_wait", "group aborted earlier; close it");
+  if (g->gnext - gticket > 8) return B2P_OK;  // a later gather's event has been waited on since
+  (void)hipSetDevice(g->dev[0]);
+  const double deadline = now_s() + 1e-3 * g->timeout_ms;
+  for (;;) {
+    hipError_t e = hipEventQuery(g->gev[gticket % 8]);
+    if (e == hipSuccess) return B2P_OK;
+    if (e != hipErrorNotReady) {
+      if (!g->comm.empty()) abort_comms(g);
+      g->dead = 1;
+      return gerr(g, B2P_EHIP, "b2p_group_wait", hipGetErrorString(e));
+    }
+    if (!g->comm.empty()) {
+      ncclResult_t st = ncclSuccess;
+      for (int r = 0; r < (int)g->comm.size() && st == ncclSuccess; ++r) {
+        ncclResult_t q = ncclCommGetAsyncError(g->comm[r], &st);
+        if (q != ncclSuccess) st = q;
+        if (st == ncclInProgress) st = ncclSuccess;
+      }
+      if (st != ncclSuccess) {
+        abort_comms(g);
+        return gerr(g, B2P_EHIP, "b2p_group_wait", ncclGetErrorString(st));
+      }
+    }
+    if (now_s() > deadline) {
+      char d[96];
+      snprintf(d, sizeof d, "gather not complete after %d ms; communicators aborted", g->timeout_ms);
+      if (!g->comm.empty()) abort_comms(g);
+      g->dead = 1;
+      return gerr(g, B2P_ETIMEDOUT, "b2p_group_wait", d);
+    }
+    usleep(20);
+  }
+}
+
 int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint64_t *root_sum) {
   if (!g || !sums || !root_sum || !count) return B2P_EINVAL;
   if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_reduce", "group aborted earlier; close it");
@@ -342,6 +445,15 @@ int b2p_group_close(b2p_group_t *g) {
       (void)hipSetDevice(g->dev[r]);
       (void)hipEventDestroy(g->done[r]);
     }
+  for (size_t r = 0; r < g->gstream.size(); ++r)
+    if (g->gstream[r]) {
+      (void)hipSetDevice(g->dev[r]);
+      (void)hipStreamSynchronize(g->gstream[r]);
+      (void)hipStreamDestroy(g->gstream[r]);
+    }
+  (void)hipSetDevice(g->dev[0]);
+  for (auto e : g->gev)
+    if (e) (void)hipEventDestroy(e);
   delete g;
   return B2P_OK;
 }

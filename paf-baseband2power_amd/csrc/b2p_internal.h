@@ -137,3 +137,5 @@ uint64_t splitmix64_host(uint64_t x);
 struct b2p_ctx;
 void *b2p_internal_stream(struct b2p_ctx *ctx);  // the context's current stream
 int b2p_internal_flush(struct b2p_ctx *ctx);     // enqueue a deferred finalize
+// the event b2p_fence recorded for `ticket` (one of the last 8), or null
+void *b2p_internal_fence_event(struct b2p_ctx *ctx, uint64_t ticket);

@@ -283,7 +283,9 @@ typedef struct shared_t {
    * blocks it took, and whether its batch ended at a partial block */
   int avail[MAX_SUB], got[MAX_SUB], partial[MAX_SUB];
   uint32_t bmax;
+  int depth;      /* read depth: two batches held */
   int gather_dev; /* every sub-band on a GPU-resident ring: worker_gather_dev */
+  uint64_t tick[MAX_SUB]; /* each member's fence after its latest launch */
   int failed;
   uint64_t nblocks, nskipped;
   uint64_t nlaunches; /* device ring: integrate launches, several queued blocks each at most */
@@ -394,18 +396,55 @@ static void *worker(void *arg) {
 }
 
 #if DEVICE_RINGS
-/* nsub > 1 sub-bands on GPU-resident rings, gathered.  Each round every
- * member integrates the same number m of its blocks in one launch --
- * m = the fewest whole blocks any member has queued, up to sh->bmax
- * (b2p_blocks_per_launch) -- and the root gathers the m spectra of every
- * member in one collective (b2p_group_gather_n) and writes m output
- * blocks.  With one block per round the round's fixed cost (syncs, two
- * barriers, the gather, the output) held two sub-bands sharing one GPU to
- * 4.4 TB/s when the producers ran ahead (tools/bench_ring.py --nsub 2);
- * now it is paid once per m integrations.  A real-time stream gives m = 1,
- * the rounds of the unbatched worker.  A member whose transfer ends (a
- * partial block) ends the round at the blocks every member has whole; the
- * rest are released unintegrated and counted as one skipped integration. */
+/* nsub > 1 sub-bands on GPU-resident rings, gathered, launches kept in
+ * flight.  Round k: every member takes the same number m_k of whole blocks
+ * -- the next block plus what it has queued, the fewest any member has, up
+ * to sh->bmax (b2p_blocks_per_launch) -- and integrates them in one launch,
+ * which also finalizes its batch k-1 (carried).  Only then does it wait for
+ * batch k-1's kernel and release those blocks, so its GPU never waits on the
+ * host between rounds.  The root gathers batch k-1 of every member in one
+ * collective on the group's own streams behind the members' fences
+ * (b2p_group_gather_async) and writes batch k-2's output blocks.  Outputs
+ * trail by two rounds; a real-time stream gives m = 1.  One block per round
+ * with a sync, a gather and the outputs inside it held two sub-bands
+ * sharing one GPU to 4.45 TB/s (tools/bench_ring.py --nsub 2).  A member
+ * whose transfer ends (a partial block) ends the batch at the blocks every
+ * member has whole; the rest are released unintegrated and counted as one
+ * skipped integration. */
+typedef struct {
+  uint64_t slot;   /* batch index */
+  uint32_t m;      /* integrations per member */
+  uint64_t gticket;
+} gathered_t;
+
+static int root_write_batch(shared_t *sh, const gathered_t *b, size_t nfl) {
+  int rc = b2p_group_wait(sh->grp, b->gticket);
+  if (rc != B2P_OK) {
+    multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
+    return -1;
+  }
+  const float *host = sh->spec_host + (b->slot % 3) * (size_t)sh->bmax * (sh->obytes / sizeof(float));
+  for (uint32_t j = 0; j < b->m; j++) { /* member-major -> one output block per integration */
+    for (int q = 0; q < sh->nsub; q++)
+      memcpy(sh->stage + (size_t)q * nfl, host + ((size_t)q * b->m + j) * nfl, nfl * sizeof(float));
+    if (write_output(sh, sh->stage) < 0) return -1;
+  }
+  return 0;
+}
+
+static int root_gather_batch(shared_t *sh, uint64_t slot, uint32_t m, size_t nfl, gathered_t *out) {
+  float *specs[MAX_SUB];
+  const size_t per = (size_t)sh->bmax * nfl;
+  for (int q = 0; q < sh->nsub; q++) specs[q] = sh->sub[q].spec_dev + (slot % 3) * per;
+  const size_t rs = (size_t)sh->bmax * (sh->obytes / sizeof(float));
+  out->slot = slot;
+  out->m = m;
+  int rc = b2p_group_gather_async(sh->grp, specs, m, sh->root_dev + (slot % 3) * rs, sh->tick,
+                                  sh->spec_host + (slot % 3) * rs, &out->gticket);
+  if (rc != B2P_OK) multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
+  return rc == B2P_OK ? 0 : -1;
+}
+
 static void *worker_gather_dev(void *arg) {
   worker_t *w = (worker_t *)arg;
   shared_t *sh = w->sh;
@@ -413,11 +452,18 @@ static void *worker_gather_dev(void *arg) {
   sub_t *s = &sh->sub[r];
   ipcio_t *in = s->in->data_block;
   const size_t nfl = sh->obytes / sizeof(float) / (size_t)sh->nsub; /* floats per member spectrum */
-  if (sh->bmax > 1 && ipcbuf_set_read_depth(&in->buf, (int)sh->bmax) < 0) {
-    multilog(sh->log, LOG_ERR, "sub-band %d: read depth %u refused", r, sh->bmax);
+  const uint32_t B = sh->bmax;
+  const int depth = sh->depth;
+  if (ipcbuf_set_read_depth(&in->buf, depth) < 0) {
+    multilog(sh->log, LOG_ERR, "sub-band %d: read depth %d refused", r, depth);
     sh->failed = 1;
   }
-  for (;;) {
+  uint64_t t_prev = 0;
+  int held = 0;      /* blocks of the previous batch, still held */
+  uint32_t m_prev = 0; /* its integrations (same on every member) */
+  gathered_t gq[2];  /* root: gathers issued, not yet written (oldest first) */
+  int ngq = 0;
+  for (uint64_t k = 0;; k++) {
     const void *blks[B2P_MAX_BLOCKS];
     uint64_t bytes = 0, bid = 0;
     char *blk = g_stop || sh->failed ? NULL : next_block(s->in, &bytes);
@@ -426,18 +472,19 @@ static void *worker_gather_dev(void *arg) {
     if (sh->have[r] == 1) {
       blks[0] = blk;
       const uint64_t q = ipcbuf_get_nfull_iread(&in->buf, in->buf.iread);
-      avail = 1 + (int)(q < sh->bmax - 1 ? q : sh->bmax - 1);
+      uint64_t cap = B < (uint32_t)(depth - held) ? B : (uint32_t)(depth - held);
+      avail = (int)(1 + q < cap ? 1 + q : cap);
     }
     sh->avail[r] = avail;
-    pthread_barrier_wait(&sh->bar); /* every member knows what it holds */
-    int stop = sh->failed, skip = 0, n = (int)sh->bmax;
+    pthread_barrier_wait(&sh->bar); /* B1: every member knows what it holds */
+    int stop = sh->failed, skip = 0, n = (int)B;
     for (int q = 0; q < sh->nsub; q++) {
       if (sh->have[q] < 0) stop = 1;
       if (sh->have[q] == 0) skip = 1;
       if (sh->avail[q] < n) n = sh->avail[q];
     }
     int m = stop || skip ? 0 : 1, part = 0;
-    for (int j = 1; !stop && !skip && j < n; j++) { /* queued: no wait */
+    for (int j = 1; m && j < n; j++) { /* queued: no wait */
       uint64_t b = 0;
       char *p = ipcio_open_block_read(in, &b, &bid);
       if (!p) break;
@@ -450,62 +497,67 @@ static void *worker_gather_dev(void *arg) {
     }
     sh->got[r] = m;
     sh->partial[r] = part;
-    pthread_barrier_wait(&sh->bar); /* every member's batch is known */
-    int mm = m;
+    pthread_barrier_wait(&sh->bar); /* B2: every member's batch is known */
+    uint32_t mm = (uint32_t)m;
     for (int q = 0; q < sh->nsub; q++)
-      if (sh->got[q] < mm) mm = sh->got[q];
-    const double t0 = now_s();
-    if (r == 0 && mm && sh->t_first == 0) sh->t_first = t0;
+      if ((uint32_t)sh->got[q] < mm) mm = (uint32_t)sh->got[q];
+    if (r == 0 && mm && sh->t_first == 0) sh->t_first = now_s();
     int rc = B2P_OK;
-    if (mm) {
-      rc = mm == 1 ? b2p_integrate(s->ctx, blks[0], s->rbufsz, 1, s->spec_dev, 1)
-                   : b2p_integrate_n(s->ctx, blks, (uint32_t)mm, s->spec_dev, 1);
-      if (rc == B2P_OK) rc = b2p_sync(s->ctx); /* done with the blocks */
-      if (rc != B2P_OK) {
-        multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", r, b2p_strerror(rc), b2p_last_error(s->ctx));
-        sh->failed = 1;
-      }
+    uint64_t t = 0;
+    float *slot = s->spec_dev + (k % 3) * (size_t)B * nfl;
+    if (mm) { /* batch k; its launch also finalizes batch k-1 */
+      rc = mm == 1 ? b2p_integrate(s->ctx, blks[0], s->rbufsz, 1, slot, 1)
+                   : b2p_integrate_n(s->ctx, blks, mm, slot, 1);
+      if (rc == B2P_OK) rc = b2p_fence(s->ctx, &t);
+    } else if (m_prev) { /* no launch to carry batch k-1's finalize: enqueue it */
+      rc = b2p_sync(s->ctx);
+      if (rc == B2P_OK) rc = b2p_fence(s->ctx, &t);
     }
-    for (int j = 0; j < taken; j++) ipcio_close_block_read(in, 0); /* oldest first */
-    pthread_barrier_wait(&sh->bar); /* every spectrum of this round is on its device */
+    if (rc == B2P_OK && m_prev) rc = b2p_fence_wait(s->ctx, t_prev); /* batch k-1's kernel is done */
+    for (; held; held--) ipcio_close_block_read(in, 0); /* its blocks go back, oldest first */
+    held = taken;
+    if (!mm)
+      for (; held; held--) ipcio_close_block_read(in, 0); /* nothing launched on these */
+    if (rc != B2P_OK) {
+      multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", r, b2p_strerror(rc), b2p_last_error(s->ctx));
+      sh->failed = 1;
+    }
+    sh->tick[r] = t;
+    pthread_barrier_wait(&sh->bar); /* B3: every member launched batch k, tickets published */
     if (r == 0) {
       int lost = skip && !stop;
-      for (int q = 0; q < sh->nsub; q++) lost |= sh->got[q] > mm || sh->partial[q];
+      for (int q = 0; q < sh->nsub; q++) lost |= (uint32_t)sh->got[q] > mm || sh->partial[q];
       if (lost) {
         sh->nskipped++;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
       }
-      if (!sh->failed && mm) {
-        float *specs[MAX_SUB];
-        for (int q = 0; q < sh->nsub; q++) specs[q] = sh->sub[q].spec_dev;
-        rc = b2p_group_gather_n(sh->grp, specs, (uint32_t)mm, sh->root_dev);
-        if (rc == B2P_OK) rc = b2p_group_sync(sh->grp);
-        if (rc == B2P_OK) rc = b2p_memcpy(s->ctx, sh->spec_host, sh->root_dev, (size_t)mm * sh->obytes, 2);
-        if (rc != B2P_OK) {
-          multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
-          sh->failed = 1;
-        }
-        for (int j = 0; !sh->failed && j < mm; j++) { /* member-major -> one block per integration */
-          for (int q = 0; q < sh->nsub; q++)
-            memcpy(sh->stage + (size_t)q * nfl, sh->spec_host + ((size_t)q * (size_t)mm + (size_t)j) * nfl,
-                   nfl * sizeof(float));
-          if (write_output(sh, sh->stage) < 0) sh->failed = 1;
-        }
-        if (!sh->failed) {
-          sh->nlaunches++;
-          if ((uint32_t)mm > sh->max_batch) sh->max_batch = (uint32_t)mm;
-          const double dt = sh->t_last - t0;
-          if (getenv("B2P_TRACE_PIPELINE") || sh->nlaunches % 64 == 1)
-            multilog(sh->log, LOG_INFO, "round %" PRIu64 ": %d integration(s) per sub-band in %.3f ms, "
-                     "%.1f Msamples/s in all", sh->nlaunches, mm, dt * 1e3,
-                     (double)mm * sh->nsub * (double)(nfl / s->g.npol_out) * s->g.npol *
-                         (double)s->g.nsamp_int / dt / 1e6);
-        }
+      if (!sh->failed && m_prev && root_gather_batch(sh, k - 1, m_prev, nfl, &gq[ngq++]) < 0) sh->failed = 1;
+      if (mm) {
+        sh->nlaunches++;
+        if (mm > sh->max_batch) sh->max_batch = mm;
+        if (getenv("B2P_TRACE_PIPELINE") || sh->nlaunches % 64 == 1)
+          multilog(sh->log, LOG_INFO, "round %" PRIu64 ": %u integration(s) per sub-band, %.3f ms since the "
+                   "first", sh->nlaunches, mm, (now_s() - sh->t_first) * 1e3);
       }
     }
-    pthread_barrier_wait(&sh->bar);
-    if (sh->failed || stop) break;
+    /* every member breaks on the same round: stop was decided at B1 (a
+     * failure raised after B3 stops the next round, at its B1) */
+    if (stop) break;
+    if (r == 0) /* batch k-2 is home: its gather waited for launch k-1 */
+      while (ngq > 1 && !sh->failed) {
+        if (root_write_batch(sh, &gq[0], nfl) < 0) sh->failed = 1;
+        gq[0] = gq[1];
+        ngq--;
+      }
+    t_prev = t;
+    m_prev = mm;
   }
+  /* stopped: batch k-1 was finalized and gathered above (m = 0 in a stop
+   * round); release what is held, write what is gathered */
+  for (; held; held--) ipcio_close_block_read(in, 0);
+  if (r == 0)
+    for (int i = 0; i < ngq && !sh->failed; i++)
+      if (root_write_batch(sh, &gq[i], nfl) < 0) sh->failed = 1;
   return NULL;
 }
 
@@ -942,13 +994,17 @@ int main(int argc, char *argv[]) {
       if (x < nb) nb = x;
     }
     const uint32_t want = b2p_blocks_per_launch(sub[0].rbufsz);
-    sh.gather_dev = all_dev;
-    if (all_dev) sh.bmax = nb < want ? (uint32_t)nb : want;
-    if (!sh.bmax) sh.bmax = 1;
+    /* two batches held: B <= nbufs - 1, depth = min(nbufs, 2B) */
+    sh.gather_dev = all_dev && nb >= 2;
+    if (sh.gather_dev) {
+      sh.bmax = nb - 1 < want ? (uint32_t)(nb - 1) : want;
+      sh.depth = (int)(nb < 2 * sh.bmax ? nb : 2 * sh.bmax);
+      if (sh.depth < 2) sh.depth = 2;
+    }
   }
 #endif
   {
-    const size_t hb = (sh.bmax * sh.obytes + 4095) / 4096 * 4096;
+    const size_t hb = ((sh.gather_dev ? 3 : 1) * sh.bmax * sh.obytes + 4095) / 4096 * 4096;
     sh.spec_host = aligned_alloc(4096, hb);
     sh.stage = malloc(sh.obytes);
     if (!sh.spec_host || !sh.stage) goto done;
@@ -975,9 +1031,9 @@ int main(int argc, char *argv[]) {
              mode ? "peer copies (shared device)" : "RCCL ncclReduce");
   } else if (conf.nsub > 1) {
     for (int r = 0; r < conf.nsub; r++)
-      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, sh.bmax * info.nout * sizeof(float)) != B2P_OK)
+      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, 3 * sh.bmax * info.nout * sizeof(float)) != B2P_OK)
         goto done;
-    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, sh.bmax * sh.obytes) != B2P_OK) goto done;
+    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, 3 * sh.bmax * sh.obytes) != B2P_OK) goto done;
     b2p_ctx_t *ctxs[MAX_SUB];
     for (int r = 0; r < conf.nsub; r++) ctxs[r] = sub[r].ctx;
     const int mode = group_mode(&conf, dup_dev, log);

@@ -132,6 +132,9 @@ PROTOTYPES = {
     "b2p_group_open_timed": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int, C.c_int]),
     "b2p_group_gather": (C.c_int, [_P, C.POINTER(_P), _P]),
     "b2p_group_gather_n": (C.c_int, [_P, C.POINTER(_P), C.c_uint32, _P]),
+    "b2p_group_gather_async": (C.c_int, [_P, C.POINTER(_P), C.c_uint32, _P, C.POINTER(C.c_uint64), _P,
+                                         C.POINTER(C.c_uint64)]),
+    "b2p_group_wait": (C.c_int, [_P, C.c_uint64]),
     "b2p_group_sync": (C.c_int, [_P]),
     "b2p_group_last_error": (C.c_char_p, [_P]),
     "b2p_group_close": (C.c_int, [_P]),
