@@ -14,17 +14,21 @@
  * samples).  A short final block (EOD) is skipped and logged.
  *
  * -n N (extension): N sub-bands in one process, sub-band r on
- * ring key_in + 0x10*r and GPU d + r, one host thread + one stream each; after
- * every integration the N spectra are gathered to GPU d over RCCL
- * (b2p_group_gather) and written as one N*NCHAN block to key_out.
+ * ring key_in + 0x10*r and GPU d + r, one host thread + one stream each; the
+ * N spectra of every integration are gathered to GPU d over RCCL
+ * (b2p_group_gather) and written as one N*NCHAN block to key_out.  On
+ * GPU-resident rings the members integrate their queued blocks in rounds of
+ * one launch each, launches kept in flight, gathered on the group's own
+ * streams (worker_gather_dev).
  *
  * DADA library: built by default against libpafdada (include/b2p_dada.h).
  * With -DB2P_PSRDADA it includes PSRDADA's own headers and calls only the
  * PSRDADA subset the reference's hosts use, touching
  * no DADA struct but dada_hdu_t's data_block / header_block, so it links
- * against the real libpsrdada; GPU-resident rings, two
- * blocks in flight and pinning every ring block up front (libpafdada
- * extensions) are then off, and blocks are pinned when first seen.
+ * against the real libpsrdada; GPU-resident rings, launches
+ * in flight over held blocks and pinning every ring block up front
+ * (libpafdada extensions) are then off, and blocks are pinned when first
+ * seen.
  */
 #include <getopt.h>
 #include <inttypes.h>
