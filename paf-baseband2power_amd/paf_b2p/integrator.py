@@ -268,6 +268,25 @@ class Group:
             raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
         self.sync()
 
+    def gather_async(self, spectra_ptrs: list[int], nspec: int, root_out_ptr: int, tickets: list[int],
+                     host_out_ptr: int | None = None) -> int:
+        """b2p_group_gather_async: nspec spectra per member, read once member
+        r's fence ticket tickets[r] has passed, on the group's own streams;
+        returns the ticket for wait()"""
+        arr = (C.c_void_p * len(spectra_ptrs))(*spectra_ptrs)
+        tk = (C.c_uint64 * len(tickets))(*tickets)
+        gt = C.c_uint64()
+        rc = L.lib().b2p_group_gather_async(self._g, arr, nspec, C.c_void_p(root_out_ptr), tk,
+                                            C.c_void_p(host_out_ptr) if host_out_ptr else None, C.byref(gt))
+        if rc != L.B2P_OK:
+            raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
+        return gt.value
+
+    def wait(self, gticket: int) -> None:
+        rc = L.lib().b2p_group_wait(self._g, gticket)
+        if rc != L.B2P_OK:
+            raise L.B2PError(rc, L.lib().b2p_group_last_error(self._g).decode(errors="replace"))
+
     def sync(self) -> None:
         rc = L.lib().b2p_group_sync(self._g)
         if rc != L.B2P_OK:

@@ -46,6 +46,49 @@ def test_group_gather(gpu, n, mode):
         it.close()
 
 
+@pytest.mark.parametrize("n,mode", [(1, 0), (2, 1)])
+def test_group_gather_async_behind_fences(gpu, n, mode):
+    """b2p_group_gather_async: each member integrates 3 blocks in one launch
+    (finalize left pending), then a second batch whose launch finalizes the
+    first; the gather of batch 1 waits on the tickets fenced after that
+    second launch, runs on the group's streams, lands member-major on the
+    root and in pinned host memory; every spectrum equals the oracle's"""
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 14)
+    nb = 3
+    its = [paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) for _ in range(n)]
+    blocks = [[its[r].alloc(g.block_bytes) for _ in range(2 * nb)] for r in range(n)]
+    for r in range(n):
+        for i, b in enumerate(blocks[r]):
+            its[r].fill_synthetic(b, SEED, r, i)
+    slots = [[its[r].alloc(nb * g.nout * 4) for _ in range(2)] for r in range(n)]
+    root = its[0].alloc(n * nb * g.nout * 4)
+    host = np.zeros(n * nb * g.nout, np.float32)
+    with paf_b2p.Group(its, mode=mode) as grp:
+        for r in range(n):
+            its[r].integrate_n(blocks[r][:nb], slots[r][0].ptr, True)   # batch 1, finalize pending
+        tickets = []
+        for r in range(n):
+            its[r].integrate_n(blocks[r][nb:], slots[r][1].ptr, True)   # finalizes batch 1
+            tickets.append(its[r].fence())
+        gt = grp.gather_async([slots[r][0].ptr for r in range(n)], nb, root.ptr, tickets,
+                              host.ctypes.data)
+        grp.wait(gt)
+        got_root = its[0].download(root).view(np.float32).reshape(n, nb, g.nout)
+        for r in range(n):
+            for i in range(nb):
+                want = co.power(g, its[r].download(blocks[r][i]))
+                assert np.array_equal(got_root[r, i].view(np.uint32), want.view(np.uint32)), (r, i)
+                assert np.array_equal(host.reshape(n, nb, g.nout)[r, i].view(np.uint32), want.view(np.uint32))
+        for it in its:
+            it.sync()
+    for r in range(n):
+        for b in blocks[r] + slots[r]:
+            b.free()
+    root.free()
+    for it in its:
+        it.close()
+
+
 def test_multi_subband_c_host_gathered(gpu, tmp_path):
     from test_gpu_pipeline import write_conf
     g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 15)
