@@ -314,3 +314,47 @@ def test_gathered_replays_in_batches(gpu, tmp_path):
     finally:
         for k in kins + [kout]:
             dada.destroy_ring(k)
+
+
+def test_gathered_rounds_stop_at_the_shorter_transfer(gpu, tmp_path):
+    """two GPU-resident rings filled before the stage starts, 5 and 7 whole
+    blocks: the gathered stage takes them in rounds of queued blocks, ends
+    at the shorter transfer (5 output blocks, both sub-bands' spectra equal
+    to the oracle's), counts the unmatched blocks as a skipped integration
+    and exits cleanly"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    counts = [5, 7]
+    base, kout = fresh_key(), fresh_key()
+    kins = [base + 0x10 * q for q in range(2)]
+    for k in kins:
+        dada.destroy_ring(k)
+        dada.create_ring(k, 8, g.block_bytes, device=0)
+    dada.create_ring(kout, 8, 2 * g.nout * 4)
+    try:
+        payload = [[co.fill_synthetic(g, g.block_bytes, SEED + 7, q, i) for i in range(counts[q])]
+                   for q in range(2)]
+        for q, k in enumerate(kins):
+            with dada.Hdu(k, "W") as w:
+                w.write_header(open(HDR).read())
+                for p in payload[q]:
+                    w.write_block(p.tobytes())
+        out = tmp_path / "power.dada"
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{base:x}", "-b", f"{kout:x}",
+                                   "-c", str(tmp_path), "-d", "0", "-f", "int8:256", "-n", "2"],
+                                  stderr=subprocess.PIPE)]
+        _wait(procs)
+        _, data = dada.read_dada_file(str(out))
+        sp = data.view(np.float32).reshape(-1, 2, g.nout)
+        assert sp.shape[0] == 5
+        for i in range(5):
+            for q in range(2):
+                want = co.power(g, payload[q][i])
+                assert np.array_equal(sp[i, q].view(np.uint32), want.view(np.uint32)), (i, q)
+        log = open(str(tmp_path / "paf_baseband2power.log")).read()
+        assert "partial integration skipped (a sub-band's transfer ended)" in log
+        assert "FINISH PAF_PROCESS: 5 integrations, 1 skipped, ok" in log
+    finally:
+        for k in kins + [kout]:
+            dada.destroy_ring(k)
