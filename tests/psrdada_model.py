@@ -169,6 +169,9 @@ class Ring:
 
     def mark_filled(self, nbytes: int):  # @0x404170
         s = self.s
+        if self.state == "writer":  # start of data disabled: invisible to readers
+            s.set("w_buf", s.get("w_buf") + 1)
+            return
         if self.state == "wchange" or nbytes < self.bufsz:
             for r in range(self.n_readers):
                 semop(self.semid_data[r], EODACK, -1)
@@ -188,6 +191,21 @@ class Ring:
     def write_block(self, data: bytes):
         p = self.get_next_write()
         C.memmove(p, data, len(data))
+        self.mark_filled(len(data))
+
+    def disable_sod(self):  # @0x403c60 (ipcio_open 'w')
+        assert self.state == "wchange"
+        self.state = "writer"
+
+    def write_invisible(self, data: bytes):
+        """a block written while the start of data is disabled (WRITER):
+        get_next_write's slot wait, then mark_filled only counts w_buf"""
+        b = self.s.get("w_buf") % self.nbufs
+        while self.count(b):
+            for r in range(self.n_readers):
+                semop(self.semid_data[r], CLEAR, -1)
+            self.set_count(b, self.count(b) - 1)
+        C.memmove(self.blocks[b], data, len(data))
         self.mark_filled(len(data))
 
     def end_transfer(self):

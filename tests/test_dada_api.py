@@ -244,6 +244,48 @@ def test_deferred_start_and_stop_read_by_psrdada(ring):
     L.dada_hdu_destroy(h)
 
 
+def test_deferred_start_read_by_libpafdada(ring):
+    """the same deferred start, libpafdada on both sides: the reader's first
+    block starts at the transfer's start byte (s_byte)"""
+    k = ring(8, 64)
+    stream = bytes(np.random.default_rng(9).integers(0, 256, 5 * 64, dtype=np.uint8))
+    h = L.dada_hdu_create(None)
+    L.dada_hdu_set_key(h, k)
+    assert L.dada_hdu_connect(h) == 0 and L.dada_hdu_lock_write_spec(h, b"w") == 0
+    d = dada.HduStruct.from_address(h).data_block
+    assert L.ipcio_write(d, stream[:200], 200) == 200
+    assert L.ipcio_start(d, 70) == 0                      # block 1, byte 6
+    assert L.ipcio_write(d, stream[200:], len(stream) - 200) == len(stream) - 200
+    assert L.ipcio_close(d) == 0
+    with dada.Hdu(k, "R") as r:
+        assert r.read(1000) == stream[70:]
+        assert r.eod()
+    L.dada_hdu_unlock_write(h)
+    L.dada_hdu_destroy(h)
+
+
+def test_psrdada_deferred_writer_read_by_libpafdada(ring):
+    """the PSRDADA model writes blocks with the start of data disabled, then
+    enables it at block 2 byte 10 (enable_sod, as ipcio_start does) and ends
+    the transfer; paf's reader gets exactly the stream from there"""
+    k = ring(8, 64)
+    blocks = [bytes(np.random.default_rng(10 + i).integers(0, 256, 64, dtype=np.uint8)) for i in range(5)]
+    m = pm.Ring(k)
+    m.lock_write()
+    m.disable_sod()
+    for b in blocks[:3]:
+        m.write_invisible(b)
+    m.enable_sod(2, 10)                                   # w_buf 3 > 2: blocks 2.. become visible
+    for b in blocks[3:]:
+        m.write_block(b)
+    m.end_transfer()
+    m.unlock_write()
+    m.close()
+    with dada.Hdu(k, "R") as r:
+        assert r.read(1000) == b"".join(blocks)[2 * 64 + 10:]
+        assert r.eod()
+
+
 def test_start_refused_unless_deferred(ring):
     k = ring(2, 64)
     with dada.Hdu(k, "W") as w:
