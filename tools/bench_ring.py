@@ -87,7 +87,7 @@ def main():
         m = re.search(r"FINISH PAF_PROCESS: (\d+) integrations.* ([0-9.]+) s from the first", log)
         steady = per[a.nbufs + 1:] or per
         med = statistics.median(steady) if steady else None  # the pipelined path logs no per-block time
-        launches = [int(x) for x in re.findall(r"launch \d+: (\d+) integration", log)]
+        launches = [int(x) for x in re.findall(r"(?:launch|round) \d+: (\d+) integration", log)]
         n_int, el = (int(m.group(1)), float(m.group(2))) if m else (0, 0.0)
         ms = re.search(r"([0-9.]+) s for the last (\d+)", log)
         el_s, n_s = (float(ms.group(1)), int(ms.group(2))) if ms else (0.0, 0)
