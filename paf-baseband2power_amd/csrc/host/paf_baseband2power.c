@@ -71,6 +71,8 @@ typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
   int nsplit; /* > 1: one ring's integration split by time over nsplit GPUs */
   int gather;  /* -G: 0 auto (RCCL unless members share a GPU), 1 RCCL, 2 copies */
   int coll_timeout_s; /* -T: RCCL set-up / collective time limit */
+  int sync;  /* -S: one block per launch, waited for (the unpipelined baseline) */
+  int trace; /* -V: log every launch / round */
 } conf_t;
 
 typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
@@ -112,6 +114,9 @@ static void usage(void) {
           " -G  Transport for -n / -t: rccl | copy (default: RCCL unless members share a GPU)\n"
           " -T  Time limit in s for the RCCL set-up and each collective (default 60); past it\n"
           "     the communicators are aborted and the stage exits with an error\n"
+          " -S  GPU-resident rings: one block per launch, each waited for before the next\n"
+          "     (no launches in flight, no batching of queued blocks; a diagnostic baseline)\n"
+          " -V  Log every integrate launch / gathered round\n"
           " -h  show help\n");
 }
 
@@ -539,7 +544,7 @@ static void *worker_gather_dev(void *arg) {
       if (mm) {
         sh->nlaunches++;
         if (mm > sh->max_batch) sh->max_batch = mm;
-        if (getenv("B2P_TRACE_PIPELINE") || sh->nlaunches % 64 == 1)
+        if (sh->conf->trace || sh->nlaunches % 64 == 1)
           multilog(sh->log, LOG_INFO, "round %" PRIu64 ": %u integration(s) per sub-band, %.3f ms since the "
                    "first", sh->nlaunches, mm, (now_s() - sh->t_first) * 1e3);
       }
@@ -637,7 +642,7 @@ static void run_device_pipelined(shared_t *sh) {
         k++;
         sh->nlaunches = k;
         if (n > sh->max_batch) sh->max_batch = n;
-        if (getenv("B2P_TRACE_PIPELINE") || k % 64 == 1)
+        if (sh->conf->trace || k % 64 == 1)
           multilog(sh->log, LOG_INFO, "launch %" PRIu64 ": %u integration(s) from %" PRIu64 ", %.3f ms in "
                    "the loop body, %.3f ms since the first", k, n, b->first + 1, (now_s() - t0) * 1e3,
                    (now_s() - sh->t_first) * 1e3);
@@ -762,7 +767,7 @@ int main(int argc, char *argv[]) {
   strcpy(conf.dir, ".");
   int have_in = 0, have_out = 0;
 
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:G:T:mh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:G:T:mSVh")) != -1) {
     switch (arg) {
       case 'h':
         usage();
@@ -788,6 +793,8 @@ int main(int argc, char *argv[]) {
       case 'n': conf.nsub = atoi(optarg); break;
       case 't': conf.nsplit = atoi(optarg); break;
       case 'm': conf.mean = 1; break;
+      case 'S': conf.sync = 1; break;
+      case 'V': conf.trace = 1; break;
       case 'G':
         if (!strcmp(optarg, "rccl")) conf.gather = 1;
         else if (!strcmp(optarg, "copy")) conf.gather = 2;
@@ -989,7 +996,7 @@ int main(int argc, char *argv[]) {
 
   sh.bmax = 1;
 #if DEVICE_RINGS
-  if (!split && conf.nsub > 1 && !getenv("B2P_NO_PIPELINE")) { /* gathered batches (worker_gather_dev) */
+  if (!split && conf.nsub > 1 && !conf.sync) { /* gathered batches (worker_gather_dev) */
     int all_dev = 1;
     uint64_t nb = UINT64_MAX;
     for (int r = 0; r < conf.nsub; r++) {
@@ -1055,7 +1062,7 @@ int main(int argc, char *argv[]) {
 
   {
 #if DEVICE_RINGS
-    if (!split && nmem == 1 && sub[0].ondev && !getenv("B2P_NO_PIPELINE")) {
+    if (!split && nmem == 1 && sub[0].ondev && !conf.sync) {
       multilog(log, LOG_INFO, "GPU-resident input: two launches in flight, queued blocks integrated "
                "together (up to %d per launch)", B2P_MAX_BLOCKS);
       run_device_pipelined(&sh);

@@ -236,7 +236,7 @@ def test_queued_blocks_are_integrated_in_one_launch(gpu, tmp_path):
 
 def test_replaying_producer_keeps_the_stage_batching(gpu, tmp_path):
     """paf_dfdb -R re-hands ring blocks faster than one launch per block
-    drains them: with every launch logged (B2P_TRACE_PIPELINE) the launches
+    drains them: with every launch logged (-V) the launches
     add up to every block, several took more than one, none more than
     b2p_blocks_per_launch allows within the ring (6 blocks: 5), and every
     spectrum equals the oracle's of the block it read"""
@@ -248,12 +248,11 @@ def test_replaying_producer_keeps_the_stage_batching(gpu, tmp_path):
     dada.create_ring(kout, 4, g.nout * 4)
     try:
         out = tmp_path / "power.dada"
-        env = dict(os.environ, B2P_TRACE_PIPELINE="1")
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}",
-                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", "int8:256"],
-                                  stderr=subprocess.PIPE, env=env),
+                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", "int8:256", "-V"],
+                                  stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-R", str(nrep),
                                    "-f", "int8:256", "-r", str(SEED)], stderr=subprocess.PIPE)]
         _wait(procs)
@@ -290,12 +289,11 @@ def test_gathered_replays_in_batches(gpu, tmp_path):
     dada.create_ring(kout, 4, nsub * g.nout * 4)
     try:
         out = tmp_path / "power.dada"
-        env = dict(os.environ, B2P_TRACE_PIPELINE="1")
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{base:x}", "-b", f"{kout:x}",
-                                   "-c", str(tmp_path), "-d", "0", "-f", "int8:256", "-n", str(nsub)],
-                                  stderr=subprocess.PIPE, env=env)]
+                                   "-c", str(tmp_path), "-d", "0", "-f", "int8:256", "-n", str(nsub), "-V"],
+                                  stderr=subprocess.PIPE)]
         procs += [subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{k:x}", "-b", HDR, "-R", str(nrep),
                                     "-f", "int8:256", "-r", str(SEED + q)], stderr=subprocess.PIPE)
                   for q, k in enumerate(kins)]

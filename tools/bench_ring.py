@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--layout", default="bmf", choices=["bmf", "int8:256"])
     ap.add_argument("--nsub", type=int, default=1,
                     help="sub-bands served by one stage (-n N: rings key + 0x10*r, spectra gathered)")
+    ap.add_argument("--sync", action="store_true",
+                    help="paf_baseband2power -S: one block per launch, waited for (the unpipelined baseline)")
+    ap.add_argument("--trace", action="store_true", help="paf_baseband2power -V: log every launch / round")
     ap.add_argument("--host", action="store_true",
                     help="host ring instead (the consumer copies every block H2D)")
     a = ap.parse_args()
@@ -66,7 +69,8 @@ def main():
                                    os.path.join(d, "power.dada")], stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
                                    f"{kout:x}", "-c", d, "-d", "0", "-f", a.layout]
-                                  + (["-n", str(a.nsub)] if a.nsub > 1 else []),
+                                  + (["-n", str(a.nsub)] if a.nsub > 1 else [])
+                                  + (["-S"] if a.sync else []) + (["-V"] if a.trace else []),
                                   stderr=subprocess.PIPE)]
         procs += [subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{k:x}", "-b", HDR,
                                     "-R", str(a.blocks), "-f", a.layout]

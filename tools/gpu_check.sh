@@ -90,7 +90,7 @@ for s in $STEPS; do
                   --steps 10 --warmup 2 --order tm || exit $?
               done ;;
     ring) run bench_ring 600 python3 tools/bench_ring.py --blocks 200 &&
-          run bench_ring_sync 600 env B2P_NO_PIPELINE=1 python3 tools/bench_ring.py --blocks 200 &&
+          run bench_ring_sync 600 python3 tools/bench_ring.py --blocks 200 --sync &&
           run bench_ring_host 600 python3 tools/bench_ring.py --blocks 20 --host ;;
     pmcasm) run pmc_fetch_asm 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm &&
