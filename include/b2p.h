@@ -214,6 +214,12 @@ int b2p_finalize_sums(b2p_ctx_t *ctx, const uint64_t *sums, uint64_t nspec, uint
  * waits for the whole stream. */
 int b2p_fence(b2p_ctx_t *ctx, uint64_t *ticket);
 int b2p_fence_wait(b2p_ctx_t *ctx, uint64_t ticket);
+/* 1 once the work behind `ticket` has finished, 0 while it runs (no wait) */
+int b2p_fence_done(b2p_ctx_t *ctx, uint64_t ticket);
+/* Enqueue a deferred finalize now (b2p_finish_async / b2p_integrate leave
+ * it to ride the next launch) without waiting: for a consumer that has no
+ * next block yet and wants the spectrum out as soon as its kernel ends. */
+int b2p_flush(b2p_ctx_t *ctx);
 int b2p_sync(b2p_ctx_t *ctx);
 /* One whole integration in one call: push exactly block_bytes and emit it,
  * enqueued (out valid after b2p_sync()).  For a device span this is ONE
@@ -285,6 +291,7 @@ int b2p_group_gather_n(b2p_group_t *grp, float *const *spectra, uint32_t nspec, 
 int b2p_group_gather_async(b2p_group_t *grp, float *const *spectra, uint32_t nspec, float *root_out,
                            const uint64_t *tickets, float *host_out, uint64_t *gticket);
 int b2p_group_wait(b2p_group_t *grp, uint64_t gticket); /* bounded by the group's time limit */
+int b2p_group_done(b2p_group_t *grp, uint64_t gticket); /* 1 once finished, 0 while running */
 /* Time-split mode (second mode): member r integrated its share
  * of ONE sub-band's samples and emitted exact sums with
  * b2p_finish_partial_async; sums[r] holds `count` uint64 on member r's

@@ -785,6 +785,29 @@ int b2p_fence_wait(b2p_ctx_t *c, uint64_t ticket) {
   return B2P_OK;
 }
 
+int b2p_fence_done(b2p_ctx_t *c, uint64_t ticket) {
+  if (!c || ticket >= c->fence_next) return B2P_EINVAL;
+  LIVE(c);
+  CK(c, hipSetDevice(c->device));
+  if (c->fence_next - ticket > 8) {  // its event was recorded again since: ask the stream
+    const hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipErrorNotReady) return 0;
+    CK(c, e);
+    return 1;
+  }
+  const hipError_t e = hipEventQuery(c->fence_ev[ticket % 8]);
+  if (e == hipErrorNotReady) return 0;
+  CK(c, e);
+  return 1;
+}
+
+int b2p_flush(b2p_ctx_t *c) {
+  if (!c) return B2P_EINVAL;
+  LIVE(c);
+  CK(c, hipSetDevice(c->device));
+  return flush_pending(c);
+}
+
 int b2p_sync(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
   LIVE(c);

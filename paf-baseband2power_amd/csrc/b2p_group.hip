@@ -321,6 +321,18 @@ int b2p_group_gather_async(b2p_group_t *g, float *const *spectra, uint32_t nspec
   return B2P_OK;
 }
 
+// Has one b2p_group_gather_async finished?  1 / 0, no wait
+int b2p_group_done(b2p_group_t *g, uint64_t gticket) {
+  if (!g || gticket >= g->gnext) return B2P_EINVAL;
+  if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_done", "group aborted earlier; close it");
+  if (g->gnext - gticket > 8) return 1;
+  (void)hipSetDevice(g->dev[0]);
+  const hipError_t e = hipEventQuery(g->gev[gticket % 8]);
+  if (e == hipErrorNotReady) return 0;
+  if (e != hipSuccess) return gerr(g, B2P_EHIP, "b2p_group_done", hipGetErrorString(e));
+  return 1;
+}
+
 // Wait for one b2p_group_gather_async (polled against the group's limit)
 int b2p_group_wait(b2p_group_t *g, uint64_t gticket) {
   if (!g || gticket >= g->gnext) return B2P_EINVAL;

@@ -295,6 +295,8 @@ typedef struct shared_t {
   int depth;      /* read depth: two batches held */
   int gather_dev; /* every sub-band on a GPU-resident ring: worker_gather_dev */
   uint64_t tick[MAX_SUB]; /* each member's fence after its latest launch */
+  uint64_t tick2[MAX_SUB]; /* ... after finishing its batch at once (nothing queued) */
+  int idle[MAX_SUB];       /* nothing queued behind this round's batch */
   int failed;
   uint64_t nblocks, nskipped;
   uint64_t nlaunches; /* device ring: integrate launches, several queued blocks each at most */
@@ -414,7 +416,9 @@ static void *worker(void *arg) {
  * host between rounds.  The root gathers batch k-1 of every member in one
  * collective on the group's own streams behind the members' fences
  * (b2p_group_gather_async) and writes batch k-2's output blocks.  Outputs
- * trail by two rounds; a real-time stream gives m = 1.  One block per round
+ * trail by two rounds while blocks are queued; when no member has one
+ * queued behind its batch (a real-time stream between blocks, m = 1) the
+ * round finishes at once and its spectra go out a kernel after the blocks.  One block per round
  * with a sync, a gather and the outputs inside it held two sub-bands
  * sharing one GPU to 4.45 TB/s (tools/bench_ring.py --nsub 2).  A member
  * whose transfer ends (a partial block) ends the batch at the blocks every
@@ -441,14 +445,15 @@ static int root_write_batch(shared_t *sh, const gathered_t *b, size_t nfl) {
   return 0;
 }
 
-static int root_gather_batch(shared_t *sh, uint64_t slot, uint32_t m, size_t nfl, gathered_t *out) {
+static int root_gather_batch(shared_t *sh, uint64_t slot, uint32_t m, size_t nfl, const uint64_t *tickets,
+                             gathered_t *out) {
   float *specs[MAX_SUB];
   const size_t per = (size_t)sh->bmax * nfl;
   for (int q = 0; q < sh->nsub; q++) specs[q] = sh->sub[q].spec_dev + (slot % 3) * per;
   const size_t rs = (size_t)sh->bmax * (sh->obytes / sizeof(float));
   out->slot = slot;
   out->m = m;
-  int rc = b2p_group_gather_async(sh->grp, specs, m, sh->root_dev + (slot % 3) * rs, sh->tick,
+  int rc = b2p_group_gather_async(sh->grp, specs, m, sh->root_dev + (slot % 3) * rs, tickets,
                                   sh->spec_host + (slot % 3) * rs, &out->gticket);
   if (rc != B2P_OK) multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
   return rc == B2P_OK ? 0 : -1;
@@ -467,10 +472,10 @@ static void *worker_gather_dev(void *arg) {
     multilog(sh->log, LOG_ERR, "sub-band %d: read depth %d refused", r, depth);
     sh->failed = 1;
   }
-  uint64_t t_prev = 0;
-  int held = 0;      /* blocks of the previous batch, still held */
-  uint32_t m_prev = 0; /* its integrations (same on every member) */
-  gathered_t gq[2];  /* root: gathers issued, not yet written (oldest first) */
+  uint64_t t_held = 0; /* fence after the launch that reads the held blocks */
+  int held = 0;        /* blocks of the previous batch, still held */
+  uint32_t m_prev = 0; /* batch k-1's integrations, if its gather is still to come */
+  gathered_t gq[3];  /* root: gathers issued, not yet written (oldest first) */
   int ngq = 0;
   for (uint64_t k = 0;; k++) {
     const void *blks[B2P_MAX_BLOCKS];
@@ -522,9 +527,10 @@ static void *worker_gather_dev(void *arg) {
       rc = b2p_sync(s->ctx);
       if (rc == B2P_OK) rc = b2p_fence(s->ctx, &t);
     }
-    if (rc == B2P_OK && m_prev) rc = b2p_fence_wait(s->ctx, t_prev); /* batch k-1's kernel is done */
+    if (rc == B2P_OK && held) rc = b2p_fence_wait(s->ctx, t_held); /* batch k-1's kernel is done */
     for (; held; held--) ipcio_close_block_read(in, 0); /* its blocks go back, oldest first */
     held = taken;
+    if (mm) t_held = t;
     if (!mm)
       for (; held; held--) ipcio_close_block_read(in, 0); /* nothing launched on these */
     if (rc != B2P_OK) {
@@ -532,7 +538,10 @@ static void *worker_gather_dev(void *arg) {
       sh->failed = 1;
     }
     sh->tick[r] = t;
+    sh->idle[r] = mm && !g_stop && ipcbuf_get_nfull_iread(&in->buf, in->buf.iread) == 0;
     pthread_barrier_wait(&sh->bar); /* B3: every member launched batch k, tickets published */
+    int drain = mm && !stop; /* nobody has a block queued: finish batch k now */
+    for (int q = 0; q < sh->nsub; q++) drain &= sh->idle[q];
     if (r == 0) {
       int lost = skip && !stop;
       for (int q = 0; q < sh->nsub; q++) lost |= (uint32_t)sh->got[q] > mm || sh->partial[q];
@@ -540,7 +549,8 @@ static void *worker_gather_dev(void *arg) {
         sh->nskipped++;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
       }
-      if (!sh->failed && m_prev && root_gather_batch(sh, k - 1, m_prev, nfl, &gq[ngq++]) < 0) sh->failed = 1;
+      if (!sh->failed && m_prev && root_gather_batch(sh, k - 1, m_prev, nfl, sh->tick, &gq[ngq++]) < 0)
+        sh->failed = 1;
       if (mm) {
         sh->nlaunches++;
         if (mm > sh->max_batch) sh->max_batch = mm;
@@ -552,13 +562,58 @@ static void *worker_gather_dev(void *arg) {
     /* every member breaks on the same round: stop was decided at B1 (a
      * failure raised after B3 stops the next round, at its B1) */
     if (stop) break;
+    if (drain) { /* a real-time stream between blocks: batch k's spectra go out as soon as they can */
+      uint64_t t2 = 0;
+      rc = b2p_flush(s->ctx); /* its finalize now, as a kernel of its own (no wait) */
+      if (rc == B2P_OK) rc = b2p_fence(s->ctx, &t2);
+      if (rc != B2P_OK) {
+        multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", r, b2p_strerror(rc), b2p_last_error(s->ctx));
+        sh->failed = 1;
+      }
+      sh->tick2[r] = t2;
+      pthread_barrier_wait(&sh->bar); /* B3b: every member's batch k is finalized on its stream */
+      if (r == 0 && !sh->failed) {
+        const int i0 = ngq;
+        if (root_gather_batch(sh, k, mm, nfl, sh->tick2, &gq[ngq++]) < 0) sh->failed = 1;
+        /* write everything once batch k's gather is done, unless every
+         * member's next block arrives first (then the rounds go on in flight) */
+        while (!sh->failed && !g_stop) {
+          int queued = 1;
+          for (int q = 0; q < sh->nsub && queued; q++) {
+            ipcbuf_t *qb = &sh->sub[q].in->data_block->buf;
+            queued = ipcbuf_get_nfull_iread(qb, qb->iread) > 0;
+          }
+          if (queued) break;
+          const int d = b2p_group_done(sh->grp, gq[i0].gticket);
+          if (d < 0) {
+            multilog(sh->log, LOG_ERR, "gather: %s", b2p_group_last_error(sh->grp));
+            sh->failed = 1;
+          } else if (d) {
+            for (int i = 0; i < ngq && !sh->failed; i++)
+              if (root_write_batch(sh, &gq[i], nfl) < 0) sh->failed = 1;
+            ngq = 0;
+            break;
+          } else {
+            nanosleep(&(struct timespec){0, 20000}, NULL);
+          }
+        }
+      }
+      m_prev = 0; /* batch k is gathered; its blocks are released next round, after t_held */
+      if (r == 0)
+        while (ngq > 2 && !sh->failed) { /* keep at most the two newest gathers pending */
+          if (root_write_batch(sh, &gq[0], nfl) < 0) sh->failed = 1;
+          gq[0] = gq[1];
+          gq[1] = gq[2];
+          ngq--;
+        }
+      continue;
+    }
     if (r == 0) /* batch k-2 is home: its gather waited for launch k-1 */
       while (ngq > 1 && !sh->failed) {
         if (root_write_batch(sh, &gq[0], nfl) < 0) sh->failed = 1;
         gq[0] = gq[1];
         ngq--;
       }
-    t_prev = t;
     m_prev = mm;
   }
   /* stopped: batch k-1 was finalized and gathered above (m = 0 in a stop
@@ -578,7 +633,9 @@ static void *worker_gather_dev(void *arg) {
  * no wait), up to b2p_blocks_per_launch (a launch of >= 4 GiB), in ONE launch
  * (b2p_integrate_n): a consumer that has fallen behind catches up without
  * paying a launch per block.  Spectra are finalized by the next launch and
- * copied home behind it, so outputs trail by one batch. */
+ * copied home behind it, so outputs trail by one batch -- unless nothing is
+ * queued behind a batch (a real-time stream between blocks): then the batch
+ * is finished at once and its spectra go out a kernel after their block. */
 
 typedef struct {
   uint64_t first; /* index of its first integration */
@@ -649,6 +706,40 @@ static void run_device_pipelined(shared_t *sh) {
       } else {
         multilog(sh->log, LOG_ERR, "integrate: %s (%s)", b2p_strerror(rc), b2p_last_error(s->ctx));
         sh->failed = 1;
+      }
+      /* nothing queued behind this batch 0.2 ms after its launch (a
+       * real-time stream between blocks): its finalize is enqueued now, as
+       * a kernel of its own, and
+       * the batch is finished as soon as its kernel ends -- its spectra go
+       * out then, not a block later -- unless a block arrives first, which
+       * keeps the launches in flight */
+      if (rc == B2P_OK && !blk && !g_stop) { /* a producer ahead refills the slot just released */
+        const double t_idle = now_s();
+        while (!g_stop && ipcbuf_get_nfull_iread(&in->buf, in->buf.iread) == 0 && now_s() - t_idle < 2e-4)
+          nanosleep(&(struct timespec){0, 10000}, NULL);
+      }
+      if (rc == B2P_OK && !blk && !g_stop && ipcbuf_get_nfull_iread(&in->buf, in->buf.iread) == 0) {
+        uint64_t tf = 0;
+        rc = b2p_flush(s->ctx);
+        if (rc == B2P_OK) rc = b2p_fence(s->ctx, &tf);
+        while (rc == B2P_OK && !g_stop && ipcbuf_get_nfull_iread(&in->buf, in->buf.iread) == 0) {
+          const int d = b2p_fence_done(s->ctx, tf);
+          if (d < 0) {
+            rc = d;
+          } else if (d) { /* batch k done: its blocks go back, every spectrum out */
+            for (; held; held--) ipcio_close_block_read(in, 0);
+            for (; rc == B2P_OK && written < k; written++)
+              for (uint32_t j = 0; rc == B2P_OK && j < bat[written % 3].n; j++)
+                if (write_output(sh, SPEC(written) + (size_t)j * (sh->obytes / 4)) < 0) rc = B2P_EHIP;
+            break;
+          } else {
+            nanosleep(&(struct timespec){0, 20000}, NULL);
+          }
+        }
+        if (rc != B2P_OK) {
+          multilog(sh->log, LOG_ERR, "integrate: %s (%s)", b2p_strerror(rc), b2p_last_error(s->ctx));
+          sh->failed = 1;
+        }
       }
       if (rc == B2P_OK && !blk && !g_stop) continue; /* the next block decides */
     }

@@ -126,6 +126,8 @@ PROTOTYPES = {
     "b2p_finish_partial_async": (C.c_int, [_P, _P, C.c_int]),
     "b2p_fence": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "b2p_fence_wait": (C.c_int, [_P, C.c_uint64]),
+    "b2p_fence_done": (C.c_int, [_P, C.c_uint64]),
+    "b2p_flush": (C.c_int, [_P]),
     "b2p_finalize_sums": (C.c_int, [_P, _P, C.c_uint64, C.c_uint64, _P]),
     "b2p_group_reduce": (C.c_int, [_P, _P, C.c_uint64, _P]),
     "b2p_group_open": (C.c_int, [C.POINTER(_P), C.POINTER(_P), C.c_int, C.c_int]),
@@ -135,6 +137,7 @@ PROTOTYPES = {
     "b2p_group_gather_async": (C.c_int, [_P, C.POINTER(_P), C.c_uint32, _P, C.POINTER(C.c_uint64), _P,
                                          C.POINTER(C.c_uint64)]),
     "b2p_group_wait": (C.c_int, [_P, C.c_uint64]),
+    "b2p_group_done": (C.c_int, [_P, C.c_uint64]),
     "b2p_group_sync": (C.c_int, [_P]),
     "b2p_group_last_error": (C.c_char_p, [_P]),
     "b2p_group_close": (C.c_int, [_P]),

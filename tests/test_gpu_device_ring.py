@@ -356,3 +356,60 @@ def test_gathered_rounds_stop_at_the_shorter_transfer(gpu, tmp_path):
     finally:
         for k in kins + [kout]:
             dada.destroy_ring(k)
+
+
+def _read_with_timeout(hdu, seconds=30):
+    import threading
+    got = []
+    t = threading.Thread(target=lambda: got.append(hdu.read_block()), daemon=True)
+    t.start()
+    t.join(seconds)
+    return got[0] if got else "TIMEOUT"
+
+
+@pytest.mark.parametrize("nsub", [1, 2])
+def test_real_time_spectra_do_not_wait_for_the_next_block(gpu, tmp_path, nsub):
+    """a real-time producer: one block at a time, the next only after the
+    previous block's spectrum has come out -- which it must, since nothing
+    is queued behind it (outputs do not trail by a block / two rounds);
+    spectra equal the oracle's"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    base, kout = fresh_key(), fresh_key()
+    kins = [base + 0x10 * q for q in range(nsub)]
+    for k in kins:
+        dada.destroy_ring(k)
+        dada.create_ring(k, 4, g.block_bytes, device=0)
+    dada.create_ring(kout, 4, nsub * g.nout * 4)
+    proc = None
+    ws = []
+    try:
+        ws = [dada.Hdu(k, "W") for k in kins]
+        for w in ws:
+            w.write_header(open(HDR).read())
+        proc = subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{base:x}", "-b", f"{kout:x}",
+                                 "-c", str(tmp_path), "-d", "0", "-f", "int8:256"]
+                                + (["-n", str(nsub)] if nsub > 1 else []), stderr=subprocess.PIPE)
+        with dada.Hdu(kout, "R") as r:
+            r.read_header()
+            for i in range(4):
+                blocks = [co.fill_synthetic(g, g.block_bytes, SEED + 11, q, i) for q in range(nsub)]
+                for w, b in zip(ws, blocks):
+                    w.write_block(b.tobytes())
+                got = _read_with_timeout(r)
+                assert got != "TIMEOUT", f"spectrum {i} did not come out before block {i + 1}"
+                sp = np.frombuffer(got, np.float32).reshape(nsub, g.nout)
+                for q in range(nsub):
+                    assert np.array_equal(sp[q].view(np.uint32), co.power(g, blocks[q]).view(np.uint32))
+            for w in ws:
+                w.close()
+            ws = []
+            assert _read_with_timeout(r) is None
+        assert proc.wait(timeout=60) == 0, proc.stderr.read().decode(errors="replace")[-800:]
+    finally:
+        for w in ws:
+            w.close()
+        if proc and proc.poll() is None:
+            proc.kill()
+            proc.wait()
+        for k in kins + [kout]:
+            dada.destroy_ring(k)
