@@ -313,6 +313,9 @@ int b2p_group_close(b2p_group_t *grp);
  *   between set_timing(ctx, 2) and set_timing(ctx, 0); kernel_ms is the
  *   region's elapsed time (inter-launch gaps and finalizes included), i.e.
  *   an upper bound of the summed launch durations, with no per-launch cost.
+ *   The opening event goes on the stream with the region's first piece of
+ *   work (launch, staging copy or finalize), so the caller's own time
+ *   between set_timing(ctx, 2) and that call is not counted.
  * mode 0: off.  Closing a mode-2 region records its end event and returns
  *   without waiting; b2p_get_stats waits for it and adds the region. */
 int b2p_set_timing(b2p_ctx_t *ctx, int mode);

@@ -86,6 +86,10 @@ struct b2p_ctx {
   hipEvent_t region_a = nullptr, region_b = nullptr;
   uint64_t region_launches = 0, region_bytes = 0, region_finalizes = 0;
   int region_closed = 0;  // closing event recorded, not read yet (read by drain_timing)
+  // region opened, its first event not recorded yet: it is recorded by the
+  // region's first enqueue, so the caller's own time between opening the
+  // region and its first call is not GPU time (region_mark)
+  int region_open = 0;
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> ev_pool;
   b2p_stats_t stats{};
@@ -521,6 +525,16 @@ static hipEvent_t pool_event(b2p_ctx_t *c) {
   return e;
 }
 
+// The opening event of a timing region, recorded in front of the region's
+// first piece of GPU work.
+static int region_mark(b2p_ctx_t *c) {
+  if (c->region_open) {
+    CK(c, hipEventRecord(c->region_a, c->stream));
+    c->region_open = 0;
+  }
+  return B2P_OK;
+}
+
 static size_t pend_bytes(const b2p_ctx_t *c) {
   return (size_t)c->pend.nblk * c->nout * (c->pend.raw ? sizeof(unsigned long long) : sizeof(float));
 }
@@ -573,6 +587,7 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   EvPair p{nullptr, nullptr, nbytes, 0};
   p.bytes = nbytes * a.nblk;
   if (c->timing == 2) {
+    if (int rm = region_mark(c)) return rm;
     c->region_launches++;
     c->region_bytes += nbytes * a.nblk;
   } else if (c->timing) {
@@ -606,6 +621,7 @@ static int flush_pending(b2p_ctx_t *c) {
   f.raw = (uint32_t)c->pend.raw;
   EvPair p{nullptr, nullptr, 0, 1};
   if (c->timing == 2) {
+    if (int rm = region_mark(c)) return rm;
     c->region_finalizes++;
   } else if (c->timing) {
     if (c->pending.size() >= kTimingRing) drain_timing(c);
@@ -643,6 +659,7 @@ static int ensure_staging(b2p_ctx_t *c) {
 // landed (the caller may release the span).  A failure after the first
 // chunk leaves part of the span summed.
 static int push_host(b2p_ctx_t *c, const uint8_t *h, uint64_t nbytes) {
+  if (int rm = region_mark(c)) return rm;  // the region holds the copies as well
   int last = -1;
   long k = 0;
   for (uint64_t off = 0; off < nbytes; off += c->stage_bytes, ++k) {
@@ -758,6 +775,7 @@ int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64
   a.n = nspec * c->nout;
   a.mean = c->g.mean;
   a.nsamp = (double)(nsamp_total ? nsamp_total : c->g.nsamp_int);
+  if ((rc = region_mark(c)) != B2P_OK) return rc;
   CK(c, launch_convert(a, c->stream));
   return B2P_OK;
 }
@@ -918,6 +936,7 @@ int b2p_set_timing(b2p_ctx_t *c, int mode) {
   CK(c, hipSetDevice(c->device));
   if (c->timing == 2 && mode != 2) {  // close the region, last finalize included
     int rc = flush_pending(c);
+    if (rc == B2P_OK) rc = region_mark(c);  // an empty region
     if (rc != B2P_OK) return rc;
     // no host wait: work enqueued next (a collective) follows the region on
     // the stream at once; b2p_get_stats reads the time
@@ -928,7 +947,7 @@ int b2p_set_timing(b2p_ctx_t *c, int mode) {
     drain_timing(c);  // an earlier region still unread
     if (!c->region_a) CK(c, hipEventCreate(&c->region_a));
     if (!c->region_b) CK(c, hipEventCreate(&c->region_b));
-    CK(c, hipEventRecord(c->region_a, c->stream));
+    c->region_open = 1;  // region_a goes in front of the region's first launch
   }
   c->timing = mode;
   return B2P_OK;

@@ -6,7 +6,7 @@
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq ringn
+#          benchbpl profbpl benchcmp ringq ringn drvx3
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -71,6 +71,9 @@ for s in $STEPS; do
                 run cmp_bpl1_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 \
                   --blocks-per-launch 1 || exit $?
               done ;;
+    drvx3) for r in 1 2 3; do  # the driver's command three times (no CPU leg)
+             run drv_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 || exit $?
+           done ;;
     ringq) # configs[1] blocks through the device ring: 2 blocks (one per launch) vs 8 (batched)
            run ring_q2 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 2 --blocks 400 &&
            run ring_q8 600 python3 tools/bench_ring.py --layout int8:256 --nbufs 8 --blocks 400 &&
