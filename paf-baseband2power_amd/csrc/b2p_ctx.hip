@@ -257,6 +257,11 @@ static int plan_launch(b2p_ctx_t *c, int ncu) {
     uint32_t best = 0;
     for (uint32_t b = maxT / 64 * 64; b >= 64; b -= 64)
       if (c->CP % b == 0) { best = b; break; }
+    // a power-of-two frame (TFTFP 8x8 int16: 4096 vectors) divides into 256
+    // under the int16 cap; 512-thread columns, one per CU, measured 2-4 %
+    // faster there (8 KiB contiguous per row and workgroup), while BMF keeps
+    // 448 (512 measured 2.7 % slower; profiles/r03_tune_frame_split.jsonl)
+    if (!t.max_threads && best && best <= 256 && maxT < 512 && c->CP % 512 == 0) best = 512;
     if (t.threads) {  // tuning: an exact whole-wave divisor of the frame
       if (c->CP % (uint32_t)t.threads)
         return set_err(c, B2P_EINVAL, "tuning threads %d does not divide the %u-vector frame",
@@ -885,18 +890,6 @@ int b2p_integrate_n(b2p_ctx_t *c, const void *const *bufs, uint32_t nblk, float 
     if ((uintptr_t)bufs[b] % 16) return set_err(c, B2P_EALIGN, "block %u not 16-B aligned", b);
   }
   CK(c, hipSetDevice(c->device));
-  if (c->NC > 1) {
-    // rows split into several workgroup columns (frame-split layouts: BMF,
-    // TFTFP 8x8): one launch per block measured as fast or faster there
-    // (TFTFP 8x8: 6.5 TB/s per block vs 5.8-6.2 in one launch; BMF equal),
-    // so those run as nblk ordinary integrations -- same bits either way
-    for (uint32_t b = 0; b < nblk; ++b) {
-      int rc = b2p_push(c, bufs[b], c->block_bytes, 1);
-      if (rc == B2P_OK) rc = b2p_finish_async(c, out + (size_t)b * c->nout, out_is_device);
-      if (rc != B2P_OK) return rc;
-    }
-    return B2P_OK;
-  }
   if (!c->d_mrep) {
     const size_t words = 2 * (size_t)kMaxBlk * c->nrep * c->nout;
     if (hipMalloc(&c->d_mrep, words * sizeof(unsigned long long)) != hipSuccess)

@@ -17,6 +17,10 @@ LAYOUTS = {
     "int8_256_p2": dict(nbit=8, nchan_chunk=256, nsamp_int=1 << 13, npol_out=2, mean=1),
     "bmf_small": dict(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7, nsamp_int=128 * 16),
     "tftfp_8x8": dict(nbit=16, big_endian=1, nchunk=8, nsamp_df=128, nchan_chunk=8, nsamp_int=128 * 32),
+    # the planner's other branches: a period split into whole-wave columns,
+    # and a frame with no whole-wave divisor (rows of lcm(frame, 64))
+    "int8_336": dict(nbit=8, nchan_chunk=336, nsamp_int=1 << 12),
+    "int8_odd": dict(nbit=8, nchunk=11, nsamp_df=4, nchan_chunk=99, nsamp_int=4 * 64),
 }
 
 

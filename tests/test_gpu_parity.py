@@ -92,6 +92,8 @@ GEOMS = {
     "int8_3ch": npo.Geom(nbit=8, nchunk=1, nsamp_df=4, nchan_chunk=3, nsamp_int=4 * 999),
     "int16be_5x3": npo.Geom(nbit=16, big_endian=1, nchunk=5, nsamp_df=16, nchan_chunk=3,
                             nsamp_int=16 * 77),
+    "tftfp_8x8": npo.Geom(nbit=16, big_endian=1, nchunk=8, nsamp_df=128, nchan_chunk=8,
+                          nsamp_int=128 * 12),                                 # B = 512, NC = 8
 }
 
 
@@ -200,6 +202,20 @@ def test_full_bmf_block_vs_c_oracle(gpu):
         host = it.download(d)
         d.free()
     assert out.shape == (336,)
+    assert same_bits(out, co.power(g, host, nthreads=16))
+
+
+def test_full_tftfp_8x8_block_vs_c_oracle(gpu):
+    """int16 BE TFTFP, 8 chunks x 8 channels, a full 2^20-sample integration
+    (512 MiB): the power-of-two frame runs as 8 columns of 512 threads"""
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=8, nsamp_df=128, nchan_chunk=8)
+    with paf_b2p.Integrator(to_b2p(g)) as it:
+        assert (it.info.threads, it.info.columns) == (512, 8)
+        d = it.alloc(g.block_bytes)
+        it.fill_synthetic(d, SEED, 2, 3)
+        out = it.integrate(d)
+        host = it.download(d)
+        d.free()
     assert same_bits(out, co.power(g, host, nthreads=16))
 
 

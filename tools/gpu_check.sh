@@ -6,7 +6,7 @@
 #   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq ringn drvx3
+#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -71,6 +71,12 @@ for s in $STEPS; do
                 run cmp_bpl1_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 \
                   --blocks-per-launch 1 || exit $?
               done ;;
+    tunelay) # the two slowest layouts of the perf matrix
+             run tune_i8_336 600 python3 tools/tune.py --case "int8 336ch" --quick &&
+             run tune_tftfp88 600 python3 tools/tune.py --case "int16 BE TFTFP 8x8" --threads 128,256,512,1024 ;;
+    tunefs) # frame-split workgroup sizes: TFTFP 8x8 and BMF, 5 rounds
+             run tune_fs_tftfp88 600 python3 tools/tune.py --case "int16 BE TFTFP 8x8" --threads 256,512 --rounds 5 &&
+             run tune_fs_bmf 600 python3 tools/tune.py --config bmf --threads 448,512 --rounds 5 ;;
     drvx3) for r in 1 2 3; do  # the driver's command three times (no CPU leg)
              run drv_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 || exit $?
            done ;;

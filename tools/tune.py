@@ -47,12 +47,18 @@ def open_variant(geom, v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--case", default="", help="a tools/perf_matrix.py layout by name (e.g. 'int8 336ch') instead of --config")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--launches", type=int, default=12)
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--threads", default="", help="comma list of exact workgroup sizes (b2p_tuning_t.threads, BMF)")
     a = ap.parse_args()
-    geom = CONFIGS[a.config]["geom"]()
+    if a.case:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from perf_matrix import CASES
+        geom = dict(CASES)[a.case]()
+    else:
+        geom = CONFIGS[a.config]["geom"]()
     base = paf_b2p.Integrator(geom)
     bb = base.block_bytes
     blocks = []
@@ -100,7 +106,7 @@ def main():
         rows.append({**v, **info[i], "median_us": round(ms * 1e3, 2),
                      "min_us": round(min(res[i]) * 1e3, 2), "GBps": round(bb / (ms * 1e-3) / 1e9, 1)})
     rows.sort(key=lambda r: r["median_us"])
-    print(json.dumps({"config": a.config, "block_bytes": bb, "rounds": a.rounds, "variants": rows},
+    print(json.dumps({"config": a.case or a.config, "block_bytes": bb, "rounds": a.rounds, "variants": rows},
                      indent=1))
     for d in blocks:
         d.free()
