@@ -369,10 +369,10 @@ int b2p_open_tuned(b2p_ctx_t **out, const b2p_geom_t *g, int device, const b2p_t
   // measured defaults (tools/tune.py, DESIGN.md "launch shape"): 28-32 KiB
   // of loads in flight per CU -- 4 rows per lane; int8 512 threads with
   // contiguous row slices, int16 (BMF) 448 threads with interleaved rows --
-  // one workgroup per CU, non-temporal loads
+  // one workgroup per CU, non-temporal loads (the row order is chosen after
+  // the launch shape, below)
   c->kc.unroll = t.unroll ? t.unroll : 4;
   c->kc.nt = t.nontemporal != 0;
-  c->interleave = t.interleave >= 0 ? (uint32_t)t.interleave : (g->nbit == 16 ? 1u : 0u);
   c->fuse = t.fuse > 0;
   c->block_bytes = b2p_block_bytes(g);
   int rc;
@@ -388,6 +388,11 @@ int b2p_open_tuned(b2p_ctx_t **out, const b2p_geom_t *g, int device, const b2p_t
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0)
     ncu = 256;
   if ((rc = plan_launch(c, ncu)) != B2P_OK) return fail(rc);
+  // rows: contiguous slices for a one-column int8 row (configs[1..4]);
+  // interleaved for int16 and for rows over several workgroup columns, whose
+  // columns then walk the same rows together (int8 TFTFP 32x8: 6.51 -> 6.95
+  // TB/s, int8 336 ch 6.80 -> 6.96; profiles/r03_tune_interleave.jsonl)
+  c->interleave = t.interleave >= 0 ? (uint32_t)t.interleave : (g->nbit == 16 || c->NC > 1 ? 1u : 0u);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "hipStreamCreate"));
   c->stream = c->own_stream;

@@ -77,6 +77,9 @@ for s in $STEPS; do
     tunefs) # frame-split workgroup sizes: TFTFP 8x8 and BMF, 5 rounds
              run tune_fs_tftfp88 600 python3 tools/tune.py --case "int16 BE TFTFP 8x8" --threads 256,512 --rounds 5 &&
              run tune_fs_bmf 600 python3 tools/tune.py --config bmf --threads 448,512 --rounds 5 ;;
+    tuneil) # row interleave for multi-column int8 layouts
+             run tune_il_336 600 python3 tools/tune.py --case "int8 336ch" --quick --rounds 5 &&
+             run tune_il_tftfp32x8 600 python3 tools/tune.py --case "int8 TFTFP 32x8" --threads 256,512 --rounds 5 ;;
     drvx3) for r in 1 2 3; do  # the driver's command three times (no CPU leg)
              run drv_r$r 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 || exit $?
            done ;;

@@ -29,6 +29,7 @@ CASES = [
     ("int16 LE 256ch", lambda **k: generic_geom(256, nbit=16, **k)),
     ("int16 LE 48ch", lambda **k: generic_geom(48, nbit=16, **k)),
     ("int16 BE BMF 48x7", lambda **k: bmf_geom(**k)),
+    ("int8 TFTFP 32x8", lambda **k: make_geom(nbit=8, nchunk=32, nsamp_df=128, nchan_chunk=8, **k)),
     ("int16 BE TFTFP 8x8", lambda **k: make_geom(nbit=16, big_endian=1, nchunk=8, nsamp_df=128,
                                                  nchan_chunk=8, **k)),
 ]
