@@ -118,6 +118,20 @@ def test_bad_counts_rejected():
         assert r.returncode == 2 and "must be >= 1" in r.stderr
 
 
+def test_pmc_traffic_follows_the_launch_size():
+    """the committed PMC summary (profiles/pmc_c2.json) scales to this run's
+    bytes per launch; the measured launch size itself is taken as is"""
+    import json
+    d = json.load(open(os.path.join(REPO, "profiles", "pmc_c2.json")))
+    alg, hbm = d["algorithmic_bytes_per_launch"], d["hbm_bytes_per_launch"]
+    t, src = bench.pmc_traffic("c2", alg)
+    assert t == hbm and src == "profiles/pmc_c2.json"
+    t1, src1 = bench.pmc_traffic("c2", 1 << 30)
+    assert abs(t1 / (1 << 30) - hbm / alg) < 1e-6 and "scaled to 1073741824 B" in src1
+    assert 1.0 <= hbm / alg < 1.01          # no wasted re-reads
+    assert bench.pmc_traffic("no_such_config", 1 << 30) == (None, None)
+
+
 def test_baseline_config_names():
     assert bench.baseline_config("c2", 1, False) == "configs[1]"
     assert bench.baseline_config("c2", 4, False) == "configs[3]"
