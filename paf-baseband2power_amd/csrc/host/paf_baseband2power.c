@@ -332,7 +332,9 @@ static void *worker(void *arg) {
   sub_t *s = &sh->sub[w->r];
   for (;;) {
     uint64_t bytes = 0;
+    const double t_ask = now_s();
     char *blk = g_stop ? NULL : next_block(s->in, &bytes);
+    const double t_got = now_s();
     /* a 0-byte block only carries the end of data (PSRDADA's ipcio_close
      * after a full block): it ends the loop like a NULL one */
     sh->have[w->r] = !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
@@ -355,6 +357,7 @@ static void *worker(void *arg) {
     }
     const double t0 = now_s();
     if (w->r == 0 && sh->t_first == 0) sh->t_first = t0;
+    double t_copied = 0;
     int rc;
     if (s->ondev) {
       /* the block is already in HBM: one integrate launch reads it in place;
@@ -366,6 +369,7 @@ static void *worker(void *arg) {
     } else {
       pin_block(s, blk, sh->log);
       rc = b2p_push(s->ctx, blk, bytes, 0); /* returns once the block is copied */
+      t_copied = now_s();
       ipcio_close_block_read(s->in->data_block, bytes);
       if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
                                               sh->nsub == 1 ? 0 : 1);
@@ -394,9 +398,12 @@ static void *worker(void *arg) {
         } else {
           const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s per sub-band, "
-                   "%.1f Msamples/s in all", sh->nblocks, dt * 1e3, (double)bytes / dt / 1e9,
+                   "%.1f Msamples/s in all (block waited for %.3f ms%s%.3f ms)", sh->nblocks, dt * 1e3,
+                   (double)bytes / dt / 1e9,
                    (double)sh->nsub * (double)(sh->nout / s->g.npol_out) * s->g.npol *
-                       (double)s->g.nsamp_int / dt / 1e6);
+                       (double)s->g.nsamp_int / dt / 1e6,
+                   (t_got - t_ask) * 1e3, t_copied > 0 ? ", copied in " : ", integrated in ",
+                   ((t_copied > 0 ? t_copied : sh->t_last) - t0) * 1e3);
         }
       }
     }
