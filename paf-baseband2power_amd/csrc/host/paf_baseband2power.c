@@ -330,6 +330,7 @@ static void *worker(void *arg) {
   worker_t *w = (worker_t *)arg;
   shared_t *sh = w->sh;
   sub_t *s = &sh->sub[w->r];
+  double t_prev = 0; /* the previous output's time */
   for (;;) {
     uint64_t bytes = 0;
     const double t_ask = now_s();
@@ -398,15 +399,18 @@ static void *worker(void *arg) {
         } else {
           const double dt = sh->t_last - t0;
           multilog(sh->log, LOG_INFO, "integration %" PRIu64 ": %.3f ms, %.2f GB/s per sub-band, "
-                   "%.1f Msamples/s in all (block waited for %.3f ms%s%.3f ms)", sh->nblocks, dt * 1e3,
+                   "%.1f Msamples/s in all (asked for the block %.3f ms after the previous output, "
+                   "waited for it %.3f ms, integrating from %.3f ms after it%s%.3f ms)", sh->nblocks, dt * 1e3,
                    (double)bytes / dt / 1e9,
                    (double)sh->nsub * (double)(sh->nout / s->g.npol_out) * s->g.npol *
                        (double)s->g.nsamp_int / dt / 1e6,
-                   (t_got - t_ask) * 1e3, t_copied > 0 ? ", copied in " : ", integrated in ",
+                   t_prev > 0 ? (t_ask - t_prev) * 1e3 : 0.0, (t_got - t_ask) * 1e3,
+                   t_prev > 0 ? (t0 - t_prev) * 1e3 : 0.0, t_copied > 0 ? ", copied in " : ", integrated in ",
                    ((t_copied > 0 ? t_copied : sh->t_last) - t0) * 1e3);
         }
       }
     }
+    t_prev = sh->t_last;
     pthread_barrier_wait(&sh->bar);
     if (sh->failed) break;
   }

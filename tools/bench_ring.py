@@ -103,6 +103,10 @@ def main():
             "launches_logged": len(launches),
             "max_blocks_per_launch_logged": max(launches) if launches else None,
             "consumer_ms_per_block_median": round(med, 3) if med else None,
+            # host ring: the stage logs every block (asked -> output, ~5 us
+            # between blocks); the median leaves out the last blocks, which
+            # overlap the replaying producer's exit and copy 15-20 % slower
+            "consumer_GBps_median": round(a.nsub * bufsz / (med * 1e-3) / 1e9, 1) if med else None,
             "ms_per_block": round(el / n_int * 1e3, 4) if n_int else None,
             "consumer_elapsed_s": el,
             "ring_Msamples_s": round(a.nsub * n_int * samples / el / 1e6, 1) if el else None,
