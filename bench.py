@@ -38,10 +38,23 @@ against the C oracle (outside the timed region; the oracle is the checker,
 never the measured path); rank 0 also checks that the gathered spectra equal
 what each rank holds.  `verified` is in the JSON line and a mismatch exits 3.
 
+Launch shape.  The headline integrates bench.py's HBM-resident blocks as the
+stage integrates blocks queued in its ring: floor(4 GiB / block) per launch
+(b2p_integrate_n), e.g. 4 for configs[1].  A real-time ring never queues, so
+the stage then launches one block at a time: that shape is timed in the same
+run after the headline (`one_per_launch`, --bpl1-seconds) and verified too.
+
+Roofline.  `roofline.frac` is from HIP events around each region's launches,
+`frac_of_value` from the host-timed median region `value` comes from (the two
+differ by the region's host bracketing), `frac_kernel_only` from per-launch
+packet events.  `traffic` is the committed PMC summary's, marked STALE when
+the kernel's sources changed after it was measured (`provenance`).
+
 Prints ONE JSON line on rank 0.  Options beyond the driver contract:
   --config c2|c5|bmf|c3   workload (c3 = pinned host buffer, H2D overlapped;
                           its value is PCIe-bound and is never the default)
   --cpu-seconds S         bounded CPU-baseline sample (0 disables)
+  --blocks N              distinct input blocks per rank (default 4)
 """
 from __future__ import annotations
 
@@ -93,9 +106,10 @@ def parse(argv=None):
     ap.add_argument("--min-seconds", type=float, default=5.0,
                     help="repeat the K-step region until this much timed work has run")
     ap.add_argument("--config", default="c2", choices=["c2", "c5", "bmf", "c3"])
-    ap.add_argument("--cpu-seconds", type=float, default=4.0,
-                    help="CPU-baseline budget (tuned port, 1 thread, oracle), run after the GPU "
-                         "leg; the every-logical-CPU leg adds a quarter of it")
+    ap.add_argument("--cpu-seconds", type=float, default=9.0,
+                    help="CPU-baseline budget, run after the GPU legs: 60 %% for the tuned port at "
+                         "every CPU the job may use (>= 5 s by default), 25 %% at 1 thread, 15 %% "
+                         "for the oracle beside it; the every-logical-CPU leg adds 15 %%")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse N ranks on fewer GPUs (spectra gathered on the host)")
     ap.add_argument("--force-dist", action="store_true",
@@ -110,12 +124,20 @@ def parse(argv=None):
                     help="integrations per integrate launch (b2p_integrate_n: a consumer draining "
                          "queued HBM-resident blocks); 1 = one b2p_integrate per block; 0 (default) = "
                          "auto, as the stage batches queued blocks: floor(4 GiB / block), 1..8")
+    ap.add_argument("--blocks", type=int, default=0,
+                    help="distinct HBM-resident input blocks per rank (0 = auto: 4, or the blocks "
+                         "per launch if more); fewer than 4 lets the 256 MiB Infinity Cache serve "
+                         "repeats of small blocks, so use it only to fit many ranks on one GPU")
+    ap.add_argument("--bpl1-seconds", type=float, default=2.0,
+                    help="when the headline batches queued blocks, also time this long of regions "
+                         "with ONE block per launch (the real-time stage's launch shape) and report "
+                         "it beside the headline (0 disables)")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="seconds one multi-rank phase (rendezvous, first collective, a timed "
                          "region, verification) may take; past it the rank exits 4 naming it")
     a = ap.parse_args(argv)
-    if a.gpus < 1 or a.steps < 1 or a.warmup < 0:
-        ap.error("--gpus and --steps must be >= 1, --warmup >= 0")
+    if a.gpus < 1 or a.steps < 1 or a.warmup < 0 or a.blocks < 0:
+        ap.error("--gpus and --steps must be >= 1, --warmup and --blocks >= 0")
     return a
 
 
@@ -201,25 +223,53 @@ def parallelism_label(world: int, split: bool, dist_on: bool, rccl: bool) -> str
     return s
 
 
+# the sources that decide what the integrate kernel reads (its code and its
+# launch planner): a PMC summary measured on other sources is stale
+KERNEL_SOURCES = ("paf-baseband2power_amd/csrc/b2p_kernels.hip", "paf-baseband2power_amd/csrc/b2p_ctx.hip",
+                  "paf-baseband2power_amd/csrc/b2p_internal.h")
+
+
+def kernel_sources_sha() -> str:
+    """sha256 over KERNEL_SOURCES' bytes, in order (no git needed: the GPU
+    box's snapshot has no .git); tools/pmc_summary.py stamps it into
+    profiles/pmc_<config>.json"""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
 def pmc_traffic(config: str, bytes_per_launch: float):
     """HBM bytes per launch from the committed rocprofv3 PMC summary for this
     config (profiles/pmc_<config>.json, written by tools/pmc_summary.py from
     separate --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).
     Measured on launches of another size (blocks per launch), it is scaled
-    by this run's algorithmic bytes per launch, and the source says so."""
+    by this run's algorithmic bytes per launch, and the source says so.
+    Returns (bytes, source, provenance): provenance names the commit the
+    summary was measured on and whether the kernel sources changed since
+    (`stale`: then the traffic belongs to other code)."""
     p = os.path.join(REPO, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
-        return None, None
+        return None, None, None
     try:
         d = json.load(open(p))
         hbm, alg = d.get("hbm_bytes_per_launch"), d.get("algorithmic_bytes_per_launch")
         src = os.path.relpath(p, REPO)
+        sha = d.get("kernel_sources_sha256")
+        prov = {"measured_commit": d.get("commit"), "kernel_sources_commit": d.get("kernel_sources_commit"),
+                "stale": sha != kernel_sources_sha() if sha else None}
+        if prov["stale"] is None:
+            prov["note"] = "summary predates source stamping: freshness unknown"
+        if prov["stale"]:
+            src += " (STALE: the kernel sources changed after it was measured)"
         if hbm and alg and bytes_per_launch and int(alg) != int(bytes_per_launch):
             return (int(round(hbm / alg * bytes_per_launch)),
-                    f"{src} (measured on {alg}-B launches, scaled to {int(bytes_per_launch)} B)")
-        return hbm, src
+                    f"{src} (measured on {alg}-B launches, scaled to {int(bytes_per_launch)} B)", prov)
+        return hbm, src, prov
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
 
 
 # --------------------------------------------------------------------------
@@ -241,6 +291,7 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
     sys.path.insert(0, ORACLE)
     import cpu_baseline as cb
     threads = cb.effective_cpus()
+    picked = cb.pick_cpus(threads)
 
     def child(env, budget, *extra):
         r = subprocess.run([sys.executable, os.path.join(ORACLE, "cpu_baseline.py"),
@@ -251,11 +302,14 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
             return None
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    res = child(cb.child_env(threads), seconds)
+    res = child(cb.child_env(threads, cpus=picked["cpus"]), seconds)
+    if res is not None:
+        res["cpus_picked"] = {**picked, "rule": "one logical CPU per physical core, the idlest allowed "
+                                                "cores of one NUMA node over the sample before the legs"}
     ncpu = os.cpu_count() or threads
     if res is not None and ncpu > threads:
         res["all_cpus"] = child(cb.child_env(ncpu, places="threads", wait="passive"),
-                                max(1.0, seconds * 0.25), "only")
+                                max(1.0, seconds * 0.15), "only")
     return res
 
 
@@ -364,6 +418,16 @@ def main(argv=None) -> int:
         out_buf = it.alloc(K * nout * 4)
         out_ptr = out_buf.ptr
 
+    # several queued blocks per integrate launch (b2p_integrate_n), for the
+    # HBM-resident fused path only; every integration still gets its spectrum
+    bpl_auto = paf_b2p.blocks_per_launch(bb)
+    bpl = a.blocks_per_launch or bpl_auto
+    if not a.blocks_per_launch:  # auto: every launch the same size (a divisor of K)
+        bpl = max(n for n in range(1, bpl + 1) if K % n == 0)
+    if split or host_mode or a.no_fuse:
+        bpl = 1
+    nblocks = a.blocks or max(NBLOCKS, a.blocks_per_launch or bpl_auto)
+
     blocks = []
     if host_mode:
         hb = np.empty(bb, dtype=np.uint8)
@@ -374,8 +438,7 @@ def main(argv=None) -> int:
         it.register_host(hb)
         blocks = [hb]
     else:
-        for b in range(max(NBLOCKS, a.blocks_per_launch or paf_b2p.blocks_per_launch(bb))):
-            # (distinct blocks within a launch)
+        for b in range(nblocks):  # distinct blocks (within a launch too, when they suffice)
             d = it.alloc(bb)
             it.fill_synthetic(d, SEED, subband, b, elem0=elem0)
             blocks.append(d)
@@ -395,19 +458,13 @@ def main(argv=None) -> int:
             # finalize rides on the next launch)
             it.integrate(blk, dst, True)
 
-    # several queued blocks per integrate launch (b2p_integrate_n), for the
-    # HBM-resident fused path only; every integration still gets its spectrum
-    bpl = a.blocks_per_launch or paf_b2p.blocks_per_launch(bb)
-    if not a.blocks_per_launch:  # auto: every launch the same size (a divisor of K)
-        bpl = max(n for n in range(1, bpl + 1) if K % n == 0)
-    if split or host_mode or a.no_fuse:
-        bpl = 1
+    cur = {"bpl": bpl}  # the launch shape of the regions being timed
 
     def steps(k0, row0, n):
         """integrations k0 .. k0+n-1 into output rows row0 .."""
         j = 0
         while j < n:
-            m = min(bpl, n - j)
+            m = min(cur["bpl"], n - j)
             if m == 1:
                 step(k0 + j, row0 + j)
             else:
@@ -493,40 +550,49 @@ def main(argv=None) -> int:
         wd.disarm()
         return time.perf_counter() - t0, got
 
-    it.reset_stats()
-    el0, gathered = region()
-    el0_max = D.max_over_ranks(el0, "cuda" if rccl else "cpu") if dist_on else el0
-    repeats = max(1, min(100000, math.ceil(a.min_seconds / max(el0_max, 1e-9))))
-    els = [el0]
-    for _ in range(repeats - 1):
-        el, gathered = region()
-        els.append(el)
-    last_k0 = kk - K  # first step of the last region
+    def timed_leg(min_seconds):
+        """repeat the K-step region until min_seconds of timed work: every
+        repeat's time max-reduced over the ranks; returns those times, this
+        rank's per-step median, what rank 0 gathered last, the first step of
+        the last region, and the integrator's event stats of the leg"""
+        it.reset_stats()
+        el0, got = region()
+        el0_max = D.max_over_ranks(el0, "cuda" if rccl else "cpu") if dist_on else el0
+        repeats = max(1, min(100000, math.ceil(min_seconds / max(el0_max, 1e-9))))
+        els = [el0]
+        for _ in range(repeats - 1):
+            el, got = region()
+            els.append(el)
+        if dist_on:
+            t = torch.tensor(els, dtype=torch.float64, device="cuda" if rccl else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            els_max = t.cpu().tolist()
+        else:
+            els_max = els
+        return els_max, els, got, kk - K, it.stats()
+
+    els_max, els, gathered, last_k0, st = timed_leg(a.min_seconds)
     if dist_on:
-        t = torch.tensor(els, dtype=torch.float64, device="cuda" if rccl else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        els_max = t.cpu().tolist()
         mine = torch.tensor([statistics.median(els)], dtype=torch.float64,
                             device="cuda" if rccl else "cpu")
         per_rank = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(per_rank, mine)
         per_rank_ms = [round(float(x.item()) / K * 1e3, 4) for x in per_rank]
     else:
-        els_max, per_rank_ms = els, [round(statistics.median(els) / K * 1e3, 4)]
+        per_rank_ms = [round(statistics.median(els) / K * 1e3, 4)]
     el_med = statistics.median(els_max)
-    st = it.stats()
 
     # ---- verification (outside timing) ------------------------------------
-    verified = None
-    vinfo = {}
-    if dist_on:
-        wd.arm("verification against the oracle", max(a.dist_timeout, 900.0))
-    if not a.no_verify:
+    def verify(k0, gathered):
+        """every spectrum of the region that started at step k0 against the C
+        oracle of its input block, bit for bit; rank 0 also checks the
+        gathered spectra.  Returns (ok on every rank, info)"""
+        vinfo = {}
         vthreads = max(1, cpu_threads() // world)
         rows_ok = True
         blocks_of_rows = {}
         for j in range(K):
-            blocks_of_rows.setdefault((last_k0 + j) % len(blocks), []).append(j)
+            blocks_of_rows.setdefault((k0 + j) % len(blocks), []).append(j)
         if split:
             if rank == 0:
                 spec = spec_t.cpu().numpy()
@@ -567,23 +633,61 @@ def main(argv=None) -> int:
         ok_t = torch.tensor([1 if rows_ok else 0], dtype=torch.int64, device="cuda" if rccl else "cpu")
         if dist_on:
             dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-        verified = bool(ok_t.item())
         vinfo.update(what=(f"every spectrum of the last timed region ({K}) against the C oracle of "
                            f"its input block ({len(blocks_of_rows)} distinct block(s)"
                            + (", regenerated on the host" if split else ", downloaded from HBM")
                            + f"), bit for bit, {'rank 0' if split else 'every rank'}"),
                      threads=vthreads)
+        return bool(ok_t.item()), vinfo
+
+    verified = None
+    vinfo = {}
+    if dist_on:
+        wd.arm("verification against the oracle", max(a.dist_timeout, 900.0))
+    if not a.no_verify:
+        verified, vinfo = verify(last_k0, gathered)
     wd.disarm()
+
+    # the real-time launch shape beside the batched headline: the stage
+    # launches one block at a time unless blocks are queued in its ring
+    # (paf_baseband2power.c, run_device_pipelined), so time that too
+    one = None
+    if bpl > 1 and a.bpl1_seconds > 0:
+        cur["bpl"] = 1
+        steps(kk, 0, 1)  # warm the one-block launch shape
+        kk += 1
+        els1_max, _, gathered1, last1_k0, st1 = timed_leg(a.bpl1_seconds)
+        el1 = statistics.median(els1_max)
+        if dist_on:
+            wd.arm("verification against the oracle (one block per launch)", max(a.dist_timeout, 900.0))
+        ok1 = None if a.no_verify else verify(last1_k0, gathered1)[0]
+        wd.disarm()
+        if ok1 is False:
+            verified = False
+        k1 = st1["kernel_ms"] / max(st1["launches"], 1) / 1e3
+        one = {"blocks_per_launch": 1, "ms_per_step": round(el1 / K * 1e3, 4),
+               "value": round(D.aggregate_rate(world, K, spb, el1), 1),
+               "frac_of_value": round(bb / (el1 / K) / 1e9 / HBM_PEAK_GBS, 4),
+               "frac_events": round(st1["bytes"] / max(st1["launches"], 1) / k1 / 1e9 / HBM_PEAK_GBS, 4)
+               if k1 > 0 else None,
+               "timed_regions": len(els1_max), "timed_seconds": round(sum(els1_max), 4),
+               "verified": ok1}
+        cur["bpl"] = bpl
 
     # cross-check, outside every timed region: the integrate kernel alone,
     # timed by start/stop events on each launch's own dispatch packet (no
     # inter-launch gap, no finalize) -- the quantity rocprofv3 --kernel-trace
-    # reports as the kernel's duration
+    # reports as the kernel's duration; at least 16 launches of the headline
+    # shape, after one untimed launch (the GPU sat idle during verification)
     calib_us = None
     if not split and not host_mode and not a.no_fuse:
+        n_c = (K // bpl) * bpl or K  # whole launches of the headline shape, rows < K
+        steps(0, 0, n_c)
+        it.sync()
         it.reset_stats()
         it.set_timing(1)
-        steps(0, 0, min(16 * bpl, K))
+        while it.stats()["launches"] < 16:
+            steps(0, 0, n_c)
         it.set_timing(0)
         it.sync()
         cs = it.stats()
@@ -593,7 +697,7 @@ def main(argv=None) -> int:
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
     achieved = bytes_per_launch / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(a.config, bytes_per_launch)
+    traffic, traffic_src, traffic_prov = pmc_traffic(a.config, bytes_per_launch)
 
     rc = 0
     if rank == 0:
@@ -661,8 +765,13 @@ def main(argv=None) -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # the same quantity from the line's own headline numbers: one
+                # integration's algorithmic bytes per ms_per_step, per GPU
+                # (each rank reads bb bytes per step; a time-split rank its share)
+                "frac_of_value": round(bb / (el_med / K) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_provenance": traffic_prov,
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "avg_launch_us": round(kern_avg_s * 1e6, 2),
                 # per-launch dispatch-packet events over 16 launches after the
@@ -671,12 +780,23 @@ def main(argv=None) -> int:
                 "frac_kernel_only": (round(bytes_per_launch / (calib_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
                                      if calib_us else None),
                 "launches_timed": int(st["launches"]),
-                "timing": "HIP events on the integrator stream bracketing each timed region's "
-                          "launches (region / launches: gaps and finalizes included, an upper bound)",
+                "timing": ("frac: HIP events on the integrator stream bracketing each timed region's "
+                           "launches, summed over the regions (region / launches: gaps and finalizes "
+                           "included, the region's host bracketing not); frac_of_value: the host-timed "
+                           "median region (barrier + device sync on both sides) that `value` and "
+                           "`ms_per_step` come from -- the fraction that goes with `value`; "
+                           "frac_kernel_only: per-launch dispatch-packet events (kernel only)"),
                 "finalizes": ("carried by the next integrate launch; "
                               f"{st['finalizes']} standalone finalize launch(es) inside the regions"),
             },
+            # the real-time stage launches one block at a time (blocks only
+            # queue when it has fallen behind): that launch shape, timed in
+            # the same run after the headline's regions, verified the same way
+            "one_per_launch": one if one else (
+                {"same_as_headline": True, "blocks_per_launch": 1} if bpl == 1 else None),
             "cpu_baseline": None,
+            "provenance": {"kernel_sources_sha256": kernel_sources_sha(),
+                           "kernel_sources": list(KERNEL_SOURCES)},
         }
         if world == 1 and a.cpu_seconds > 0 and not host_mode:
             res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)

@@ -286,7 +286,8 @@ int b2p_group_gather_n(b2p_group_t *grp, float *const *spectra, uint32_t nspec, 
  * the members' streams nor their pending finalizes are touched.  host_out
  * (pinned, optional) receives root_out (nspec x nout x members floats)
  * behind the gather.  *gticket is for b2p_group_wait; up to 8 gathers may be
- * outstanding.  Call from one thread; the members' threads may keep
+ * outstanding (a 9th first waits for the oldest, bounded like b2p_group_wait:
+ * B2P_ETIMEDOUT past the group's limit).  Call from one thread; the members' threads may keep
  * launching meanwhile. */
 int b2p_group_gather_async(b2p_group_t *grp, float *const *spectra, uint32_t nspec, float *root_out,
                            const uint64_t *tickets, float *host_out, uint64_t *gticket);

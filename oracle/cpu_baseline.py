@@ -7,7 +7,10 @@ block of the bench's workload held in host RAM (no file I/O), so the passes
 stream from DRAM rather than the L3 (the EPYC 9575F host has 512 MiB of L3;
 a 1 GiB block does not fit).  SURVEY.md 8(d) "CPU baseline": the reference has
 no CPU path, so the baseline is the port, at 1 thread and at every CPU this
-process may use.
+process may use.  bench.py picks the CPUs (pick_cpus): one per physical core, the
+idlest allowed cores of one NUMA node, listed as explicit OpenMP places; every
+leg reports the cgroup's cpu.stat deltas (periods throttled, time throttled)
+beside its median and interquartile range, so a slow box shows why.
 
 Run as a child process of bench.py (never imported into the GPU process), so
 that OpenMP reads OMP_PROC_BIND / OMP_PLACES / OMP_NUM_THREADS from an
@@ -15,9 +18,9 @@ environment set for it alone:
 
     python3 oracle/cpu_baseline.py '<geom json>' SECONDS SEED
 
-and prints ONE JSON object.  Threads are bound one per physical core, packed
-from core 0 (OMP_PLACES=cores, OMP_PROC_BIND=close); the block is filled by the
-same threads first, so its pages sit on the NUMA node those cores belong to.
+and prints ONE JSON object.  Threads are bound one per OpenMP place
+(OMP_PROC_BIND=close); the block is filled by the same threads first, so its
+pages sit on the NUMA node those cores belong to.
 """
 from __future__ import annotations
 
@@ -30,21 +33,75 @@ import time
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def _read(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def _cpulist(text: str | None) -> set:
+    """'0-3,8,10-11' -> {0,1,2,3,8,10,11}"""
+    out = set()
+    for part in (text or "").strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.update(range(int(a), int(b or a) + 1))
+    return out
+
+
 def cgroup_cpus() -> float | None:
     """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), None if
     unlimited or absent.  On the GPU box nproc shows the whole 256-CPU host
     while cpu.max grants this job 16 CPUs."""
+    t = _read("/sys/fs/cgroup/cpu.max")
     try:
-        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-    except (OSError, ValueError):
+        q, p = t.split()[:2]
+    except (AttributeError, ValueError):
         return None
     if q == "max":
         return None
     return int(q) / int(p)
 
 
+def cgroup_info() -> dict:
+    """the quota and the CPUs the job's cgroup lets it run on"""
+    eff = _cpulist(_read("/sys/fs/cgroup/cpuset.cpus.effective"))
+    return {"cpu.max": (_read("/sys/fs/cgroup/cpu.max") or "").strip() or None,
+            "cpuset.cpus.effective": len(eff) or None}
+
+
+def cpu_stat() -> dict:
+    """cgroup v2 cpu.stat counters (usage / throttling), {} if absent"""
+    out = {}
+    for line in (_read("/sys/fs/cgroup/cpu.stat") or "").splitlines():
+        k, _, v = line.partition(" ")
+        if v.strip().isdigit():
+            out[k] = int(v)
+    return out
+
+
+def cpu_stat_delta(before: dict, after: dict) -> dict | None:
+    """what the cgroup's CPU controller did during a leg: periods, how many of
+    them were throttled and for how long, CPU time used"""
+    keys = ("nr_periods", "nr_throttled", "throttled_usec", "usage_usec")
+    d = {k: after[k] - before[k] for k in keys if k in before and k in after}
+    return d or None
+
+
+def allowed_cpus() -> list:
+    """logical CPUs this process may run on: its affinity, within the
+    cgroup's effective cpuset when the cgroup names one"""
+    cpus = set(os.sched_getaffinity(0))
+    eff = _cpulist(_read("/sys/fs/cgroup/cpuset.cpus.effective"))
+    if eff and cpus & eff:
+        cpus &= eff
+    return sorted(cpus)
+
+
 def effective_cpus() -> int:
-    n = len(os.sched_getaffinity(0))
+    n = len(allowed_cpus())
     q = cgroup_cpus()
     if q is not None:
         n = min(n, max(1, int(q)))
@@ -58,36 +115,97 @@ def numa_nodes() -> dict:
     try:
         for d in sorted(os.listdir(base)):
             if d.startswith("node") and d[4:].isdigit():
-                cpus = set()
-                for part in open(os.path.join(base, d, "cpulist")).read().strip().split(","):
-                    if not part:
-                        continue
-                    a, _, b = part.partition("-")
-                    cpus.update(range(int(a), int(b or a) + 1))
-                out[int(d[4:])] = cpus
+                out[int(d[4:])] = _cpulist(_read(os.path.join(base, d, "cpulist")))
     except OSError:
         pass
     return out
 
 
+def _idle_ticks() -> dict:
+    """{cpu: (idle + iowait ticks, total ticks)} from /proc/stat"""
+    out = {}
+    for line in (_read("/proc/stat") or "").splitlines():
+        if line.startswith("cpu") and line[3:4].isdigit():
+            f = line.split()
+            v = [int(x) for x in f[1:]]
+            out[int(f[0][3:])] = (v[3] + (v[4] if len(v) > 4 else 0), sum(v[:8]))
+    return out
+
+
+def busy_fraction(cpus, seconds: float = 0.25) -> dict:
+    """{cpu: fraction of the last `seconds` it spent busy}, from /proc/stat
+    (other tenants of the host included: this job does not run meanwhile)"""
+    import time
+    a = _idle_ticks()
+    time.sleep(seconds)
+    b = _idle_ticks()
+    out = {}
+    for c in cpus:
+        if c in a and c in b:
+            dt = b[c][1] - a[c][1]
+            out[c] = 1.0 - (b[c][0] - a[c][0]) / dt if dt > 0 else 0.0
+    return out
+
+
+def pick_cpus(n: int, sample_s: float = 0.25) -> dict:
+    """n logical CPUs for the timed leg, one per physical core, on one NUMA
+    node: the allowed cores that were idlest over `sample_s` (the GPU box's
+    host is shared with other jobs whose threads are not confined to a
+    cpuset, so packing from CPU 0 can land on busy cores), preferring the
+    node with the most idle capacity.  Returns the CPUs, their node and how
+    busy they and the host were beforehand."""
+    allowed = allowed_cpus()
+    busy = busy_fraction(allowed, sample_s)
+    cores = {}   # (package, core) -> first allowed sibling
+    for c in allowed:
+        t = "/sys/devices/system/cpu/cpu%d/topology/" % c
+        key = ((_read(t + "physical_package_id") or "0").strip(), (_read(t + "core_id") or str(c)).strip())
+        cores.setdefault(key, c)
+    reps = sorted(cores.values(), key=lambda c: (busy.get(c, 0.0), c))
+    nodes = numa_nodes()
+    node_of = {c: nd for nd, cs in nodes.items() for c in cs}
+    by_node = {}
+    for c in reps:
+        by_node.setdefault(node_of.get(c), []).append(c)
+    full = [nd for nd, cs in by_node.items() if len(cs) >= n]
+    if full:   # the node whose n idlest cores are idlest together
+        nd = min(full, key=lambda nd: sum(busy.get(c, 0.0) for c in by_node[nd][:n]))
+        pick = by_node[nd][:n]
+    else:
+        nd, pick = None, reps[:n]
+    if len(pick) < n:   # fewer physical cores than threads: add SMT siblings
+        pick += [c for c in sorted(allowed, key=lambda c: busy.get(c, 0.0)) if c not in pick][:n - len(pick)]
+    return {"cpus": sorted(pick), "node": nd,
+            "busy_before": round(sum(busy.get(c, 0.0) for c in pick) / max(1, len(pick)), 4),
+            "host_busy_before": round(sum(busy.values()) / max(1, len(busy)), 4),
+            "sample_s": sample_s}
+
+
 def host_cpu() -> dict:
     model = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    for line in (_read("/proc/cpuinfo") or "").splitlines():
+        if line.startswith("model name"):
+            model = line.split(":", 1)[1].strip()
+            break
     return {"model": model, "logical_cpus": os.cpu_count(), "numa_nodes": len(numa_nodes()) or None,
-            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus()}
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus(),
+            "cgroup": cgroup_info()}
 
 
-def child_env(threads: int, places: str = "cores", wait: str = "active") -> dict:
+def child_env(threads: int, places: str = "cores", wait: str = "active", cpus=None) -> dict:
+    """environment of a timed child: with `cpus`, one OpenMP place per listed
+    CPU (pick_cpus), else OMP_PLACES=`places` packed from the first CPU"""
     env = dict(os.environ)
+    if cpus:
+        places = ",".join("{%d}" % c for c in cpus[:threads])
     env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES=places,
                OMP_WAIT_POLICY=wait)
     return env
+
+
+def _quartiles(xs):
+    q = statistics.quantiles(xs, n=4, method="inclusive") if len(xs) >= 2 else [xs[0]] * 3
+    return [round(q[0], 2), round(q[2], 2)]
 
 
 def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str = "auto") -> dict:
@@ -99,7 +217,8 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
     host = host_cpu()  # before OpenMP binds this thread to its first place
-    first = min(os.sched_getaffinity(0))
+    pl = os.environ.get("OMP_PLACES", "")
+    first = int(pl[1:pl.index("}")]) if pl.startswith("{") else min(os.sched_getaffinity(0))
     g = npo.Geom(**geom)
     buf = np.empty(g.block_bytes, dtype=np.uint8)
     co.fill_synthetic(g, g.block_bytes, seed, 0, 0, out=buf)   # first touch by the bound threads
@@ -115,6 +234,7 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
         warm = buf[: g.frame_bytes * max(1, (64 << 20) // g.frame_bytes)]
         (co.port_integrate(g, warm, nthreads=nt, isa=isa) if fn is port
          else co.integrate(g, warm, nthreads=nt))
+        st0 = cpu_stat()
         rates, t_all = [], time.perf_counter()
         while len(rates) < min_passes or time.perf_counter() - t_all < budget:
             t0 = time.perf_counter()
@@ -122,38 +242,48 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
             rates.append(per_pass / (time.perf_counter() - t0) / 1e6)
             if len(rates) >= 10000:
                 break
-        return rates, time.perf_counter() - t_all
+        return rates, time.perf_counter() - t_all, cpu_stat_delta(st0, cpu_stat())
+
+    def leg(rates, el, thr):
+        return {"value": round(statistics.median(rates), 2), "passes": len(rates), "seconds": round(el, 2),
+                "iqr": _quartiles(rates), "passes_range": [round(min(rates), 2), round(max(rates), 2)],
+                "cgroup_cpu_stat_delta": thr}
 
     used = co.port_isa(isa)
+    binding = (f"OMP_PLACES={os.environ.get('OMP_PLACES')} OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} "
+               f"OMP_WAIT_POLICY={os.environ.get('OMP_WAIT_POLICY')}")
     if not one_thread:  # one setting only (bench.py's every-logical-CPU leg)
-        r_n, el_n = timed(port, threads, seconds)
-        return {"threads": threads, "value": round(statistics.median(r_n), 2), "passes": len(r_n),
-                "passes_range": [round(min(r_n), 2), round(max(r_n), 2)], "isa": used,
-                "binding": f"OMP_PLACES={os.environ.get('OMP_PLACES')} "
-                           f"OMP_WAIT_POLICY={os.environ.get('OMP_WAIT_POLICY')}"}
-    r_n, el_n = timed(port, threads, seconds * 0.55)
-    r_1, el_1 = timed(port, 1, seconds * 0.25)
-    r_o, el_o = timed(oracle, threads, seconds * 0.2)
+        r_n, el_n, thr_n = timed(port, threads, seconds)
+        return {"threads": threads, **leg(r_n, el_n, thr_n), "isa": used, "binding": binding}
+    r_n, el_n, thr_n = timed(port, threads, seconds * 0.6)
+    r_1, el_1, thr_1 = timed(port, 1, seconds * 0.25)
+    r_o, el_o, _ = timed(oracle, threads, seconds * 0.15)
     # the port is a baseline, not the checker: its sums must equal the oracle's
     equal = bool(np.array_equal(port(threads), oracle(threads)))
     nodes = numa_nodes()
     node = next((n for n, c in nodes.items() if first in c), None)
+    ln = leg(r_n, el_n, thr_n)
     return {
-        "value": round(statistics.median(r_n), 2), "unit": "Msamples/s", "cores": threads,
+        "value": ln["value"], "unit": "Msamples/s", "cores": threads,
         "kind": "port-tuned",
         "isa": used,
         "sample": (f"tuned port ({used}, OpenMP time tiles): {len(r_n)} passes ({el_n:.1f} s) at "
                    f"{threads} threads and {len(r_1)} passes ({el_1:.1f} s) at 1 thread over one "
                    f"full {g.block_bytes >> 20} MiB {g.nchan}-chan int{g.nbit} integration block "
                    "in host RAM (no file I/O); value = median pass"),
+        "iqr": ln["iqr"],
+        "passes_range": ln["passes_range"],
+        "passes": ln["passes"],
+        "leg_seconds": ln["seconds"],
+        "cgroup_cpu_stat_delta": thr_n,
         "value_1thread": round(statistics.median(r_1), 2),
-        "passes_range": [round(min(r_n), 2), round(max(r_n), 2)],
+        "iqr_1thread": _quartiles(r_1),
+        "cgroup_cpu_stat_delta_1thread": thr_1,
         "equals_oracle": equal,
         "oracle_value": round(statistics.median(r_o), 2),
         "oracle": (f"scalar C restatement (the checker, oracle/b2p_oracle.c): {len(r_o)} passes "
                    f"({el_o:.1f} s) at {threads} threads, median"),
-        "numa": {"node": node, "binding": "OMP_PLACES=cores OMP_PROC_BIND=close, packed from the "
-                                          "first allowed CPU; block first-touched by the same threads"},
+        "numa": {"node": node, "binding": binding + "; block first-touched by the same threads"},
         "host": host,
     }
 

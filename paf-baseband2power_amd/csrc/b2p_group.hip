@@ -268,10 +268,11 @@ int b2p_group_gather_async(b2p_group_t *g, float *const *spectra, uint32_t nspec
                            const uint64_t *tickets, float *host_out, uint64_t *gticket) {
   if (!g || !spectra || !root_out || !tickets || !gticket || nspec < 1) return B2P_EINVAL;
   if (g->dead) return gerr(g, B2P_ETIMEDOUT, "b2p_group_gather_async", "group aborted earlier; close it");
-  if (g->gnext >= 8) {  // the event of gather gnext - 8 is recorded again: it must have completed
-    (void)hipSetDevice(g->dev[0]);
-    if (hipEventSynchronize(g->gev[g->gnext % 8]) != hipSuccess)
-      return gerr(g, B2P_EHIP, "hipEventSynchronize", "");
+  if (g->gnext >= 8) {  // gather gnext - 8's event is recorded again: it must have completed,
+    // waited for like b2p_group_wait (bounded by the group's limit, the
+    // communicators aborted past it), never in an unbounded event sync
+    int rc = b2p_group_wait(g, g->gnext - 8);
+    if (rc != B2P_OK) return rc;
   }
   if (g->gstream.empty()) {
     g->gstream.assign(g->n, nullptr);

@@ -510,6 +510,7 @@ static void rd_set(ipcbuf_t *id, int open, int eod_held) {
   id->viewbuf = (id->viewbuf & 0xff) | ((uint64_t)open << 8) | ((uint64_t)(eod_held != 0) << 16);
 }
 
+/* before or after ipcbuf_lock_read: lock_read / unlock_read keep the depth */
 int ipcbuf_set_read_depth(ipcbuf_t *id, int depth) {
   if (!id || !id->sync || depth < 1 || depth > 255 || (uint64_t)depth > id->sync->nbufs) return -1;
   id->viewbuf = (id->viewbuf & ~(uint64_t)0xff) | (uint64_t)depth;
@@ -541,7 +542,7 @@ int ipcbuf_lock_read(ipcbuf_t *id) {  /* @0x404360 */
   }
   id->state = s->r_states[id->iread] ? ST_READING : ST_READER;
   id->xfer = s->r_xfers[id->iread] % IPCBUF_XFERS;
-  id->viewbuf = 0;
+  id->viewbuf &= 0xff; /* a read depth set before the lock stays (blocks held: none) */
   return 0;
 }
 
@@ -551,7 +552,7 @@ int ipcbuf_unlock_read(ipcbuf_t *id) {  /* @0x4045f0 */
   if (sem_op(id->semid_connect, SEM_READ, 1, SEM_UNDO) < 0) return -1;
   id->state = ST_VIEWER;
   id->iread = -1;
-  id->viewbuf = 0;
+  id->viewbuf &= 0xff; /* the read depth stays for the next lock_read */
   return 0;
 }
 
@@ -646,6 +647,22 @@ int ipcbuf_mark_cleared(ipcbuf_t *id) {  /* @0x404b80: the oldest block held */
   return 0;
 }
 
+/* Every transfer slot as ring_create leaves it: end of data set, no start
+ * or end block recorded.  A reset that kept the old e_buf[x] / e_byte[x]
+ * would leave transfer x >= 1 of the next sequence (whose eod[x] is already
+ * set, enable_sod clears it only for a transfer starting at block 0) ending
+ * early at a stale block number.  Departure: the resets of the libpsrdada
+ * the reference links rewrite eod[] only (tests/golden/psrdada_abi.json,
+ * "resets"), so there a second transfer after a reset that spans an old
+ * e_buf ends there; here the slots go back to their created state. */
+static void clear_xfers(ipcsync_t *s) {
+  for (int x = 0; x < IPCBUF_XFERS; x++) {
+    s->eod[x] = 1;
+    s->s_buf[x] = s->s_byte[x] = 0;
+    s->e_buf[x] = s->e_byte[x] = 0;
+  }
+}
+
 /* ipcbuf_reset (@0x404ca0).  A reader at end of data gets ready for the
  * next transfer.  A writer takes the ring back to its created state once
  * every reader has cleared every block and acknowledged every transfer
@@ -675,7 +692,7 @@ int ipcbuf_reset(ipcbuf_t *id) {
   }
   s->w_buf = 0;
   s->w_xfer = 0;
-  for (int x = 0; x < IPCBUF_XFERS; x++) s->eod[x] = 1;
+  clear_xfers(s);
   return 0;
 }
 
@@ -688,7 +705,7 @@ int ipcbuf_hard_reset(ipcbuf_t *id) {
   ipcsync_t *s = id->sync;
   s->w_buf = 0;
   s->w_xfer = 0;
-  for (int x = 0; x < IPCBUF_XFERS; x++) s->eod[x] = 1;
+  clear_xfers(s);
   memset(id->count, 0, s->nbufs);
   for (unsigned r = 0; r < s->n_readers; r++) {
     s->r_bufs[r] = 0;

@@ -34,6 +34,7 @@
 #include <inttypes.h>
 #include <pthread.h>
 #include <signal.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -243,7 +244,13 @@ static int read_header(dada_hdu_t *h, char **hdr, uint64_t *size) {
 
 /* ring location of an input ring's blocks: -1 host, else the HIP device */
 static int ring_device(dada_hdu_t *h) {
-#if DEVICE_RINGS
+#if DEVICE_RINGS && defined(B2P_TEST_HOST_RING_AS_DEVICE)
+  /* test build only (tests/test_sanitizers.py): host rings take the
+   * GPU-resident paths, driven by the CPU test double tests/c/b2p_cpu_stub.c,
+   * so their threads run under ThreadSanitizer on a machine with no GPU */
+  (void)h;
+  return 0;
+#elif DEVICE_RINGS
   return ipcbuf_get_device(data_buf(h));
 #else
   (void)h;
@@ -297,7 +304,14 @@ typedef struct shared_t {
   uint64_t tick[MAX_SUB]; /* each member's fence after its latest launch */
   uint64_t tick2[MAX_SUB]; /* ... after finishing its batch at once (nothing queued) */
   int idle[MAX_SUB];       /* nothing queued behind this round's batch */
-  int failed;
+  /* Any thread may raise `failed`, and a worker reads it at the top of its
+   * next round while the root may still be writing it after the round's last
+   * barrier: atomic (seq_cst), so those reads and writes are not a data race.
+   * Whether a round stops is never decided from a read that can meet a write
+   * in the same barrier phase: the per-member flags below are raised between
+   * barriers and folded into `failed` by the root after the next one. */
+  atomic_int failed;
+  int mfail[MAX_SUB]; /* worker / worker_split: this member failed this round */
   uint64_t nblocks, nskipped;
   uint64_t nlaunches; /* device ring: integrate launches, several queued blocks each at most */
   uint32_t max_batch;
@@ -376,11 +390,13 @@ static void *worker(void *arg) {
                                               sh->nsub == 1 ? 0 : 1);
       if (rc == B2P_OK && sh->nsub == 1) rc = b2p_sync(s->ctx);
     }
-    if (rc != B2P_OK) {
+    if (rc != B2P_OK)
       multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", w->r, b2p_strerror(rc), b2p_last_error(s->ctx));
-      sh->failed = 1;
-    }
+    sh->mfail[w->r] = rc != B2P_OK;
     pthread_barrier_wait(&sh->bar); /* every spectrum of this round is enqueued */
+    if (w->r == 0)
+      for (int r = 0; r < sh->nsub; r++)
+        if (sh->mfail[r]) sh->failed = 1;
     if (w->r == 0 && !sh->failed) {
       if (sh->nsub > 1) {
         float *specs[MAX_SUB];
@@ -410,7 +426,7 @@ static void *worker(void *arg) {
         }
       }
     }
-    t_prev = sh->t_last;
+    if (w->r == 0) t_prev = sh->t_last; /* written by the root only (write_output) */
     pthread_barrier_wait(&sh->bar);
     if (sh->failed) break;
   }
@@ -810,12 +826,13 @@ static void *worker_split(void *arg) {
     if (w->r == 0 && sh->t_first == 0) sh->t_first = t0;
     int rc = b2p_push(s->ctx, sh->blk + (uint64_t)w->r * sh->share_bytes, sh->share_bytes, 0);
     if (rc == B2P_OK) rc = b2p_finish_partial_async(s->ctx, s->part_dev, 1);
-    if (rc != B2P_OK) {
+    if (rc != B2P_OK)
       multilog(sh->log, LOG_ERR, "member %d: %s (%s)", w->r, b2p_strerror(rc), b2p_last_error(s->ctx));
-      sh->failed = 1;
-    }
+    sh->mfail[w->r] = rc != B2P_OK;
     pthread_barrier_wait(&sh->bar); /* every share has left the host block */
     if (w->r == 0) {
+      for (int r = 0; r < sh->nsub; r++)
+        if (sh->mfail[r]) sh->failed = 1;
       ipcio_close_block_read(s0->in->data_block, sh->blk_bytes);
       if (!sh->failed) {
         uint64_t *parts[MAX_SUB];

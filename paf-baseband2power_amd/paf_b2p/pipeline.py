@@ -66,7 +66,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
         device_ring: bool = False, split: int = 1, bin_dir: str | None = None,
-        stage_args: list | None = None) -> list:
+        stage_args: list | None = None, stage_exe: str | None = None) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
     sub-bands and gathers their spectra to its first GPU).
@@ -75,10 +75,11 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
     paf_baseband2power integrates the block in place.  split=N cuts every
     integration of a (single) chain by time over N GPUs (paf_baseband2power
     -t N, SURVEY.md 8e second mode).  stage_args: extra paf_baseband2power
-    options (e.g. ["-G", "rccl", "-T", "30"])."""
+    options (e.g. ["-G", "rccl", "-T", "30"]).  stage_exe: another build of
+    paf_baseband2power (e.g. a sanitizer build in tests/test_sanitizers.py)."""
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
-                             timeout, hfname, device_ring, stage_args)
+                             timeout, hfname, device_ring, stage_args, stage_exe)
     c = read_conf(conf_path)
     hdr = hfname or c["diskdb_hfname"]
     if not os.path.isabs(hdr):
@@ -107,7 +108,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
             out = (outfiles[r] if outfiles else os.path.join(sub_dir, "power.dada"))
             outs.append(out)
             dfile = datafile if isinstance(datafile, str) else datafile[r]
-            b2p_cmd = [_bin("paf_baseband2power", bin_dir), "-a", f"{kin:x}", "-b", f"{kout:x}",
+            b2p_cmd = [stage_exe or _bin("paf_baseband2power", bin_dir), "-a", f"{kin:x}", "-b", f"{kout:x}",
                        "-c", sub_dir, "-d", str(gpu + r), "-p", str(npol_out)]
             if layout:
                 b2p_cmd += ["-f", layout]
@@ -177,7 +178,7 @@ def _wait_all(procs, timeout):
 
 
 def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, mean, timeout,
-                  hfname, device_ring=False, stage_args=None):
+                  hfname, device_ring=False, stage_args=None, stage_exe=None):
     c = read_conf(conf_path)
     hdr = _resolve_header(c, conf_path, hfname)
     os.makedirs(directory, exist_ok=True)
@@ -196,7 +197,7 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
         out = os.path.join(directory, "power.dada")
         procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
                                       stderr=subprocess.PIPE))
-        cmd = [_bin("paf_baseband2power"), "-a", f"{c['diskdb_key']:x}", "-b", f"{kout:x}",
+        cmd = [stage_exe or _bin("paf_baseband2power"), "-a", f"{c['diskdb_key']:x}", "-b", f"{kout:x}",
                "-c", directory, "-d", str(gpu), "-p", str(npol_out), "-n", str(nsub)]
         if layout:
             cmd += ["-f", layout]

@@ -124,12 +124,41 @@ def test_pmc_traffic_follows_the_launch_size():
     import json
     d = json.load(open(os.path.join(REPO, "profiles", "pmc_c2.json")))
     alg, hbm = d["algorithmic_bytes_per_launch"], d["hbm_bytes_per_launch"]
-    t, src = bench.pmc_traffic("c2", alg)
-    assert t == hbm and src == "profiles/pmc_c2.json"
-    t1, src1 = bench.pmc_traffic("c2", 1 << 30)
+    t, src, prov = bench.pmc_traffic("c2", alg)
+    assert t == hbm and src.startswith("profiles/pmc_c2.json")
+    t1, src1, _ = bench.pmc_traffic("c2", 1 << 30)
     assert abs(t1 / (1 << 30) - hbm / alg) < 1e-6 and "scaled to 1073741824 B" in src1
     assert 1.0 <= hbm / alg < 1.01          # no wasted re-reads
-    assert bench.pmc_traffic("no_such_config", 1 << 30) == (None, None)
+    assert bench.pmc_traffic("no_such_config", 1 << 30) == (None, None, None)
+    # provenance: the summary names the kernel sources it was measured on
+    if "kernel_sources_sha256" in d:
+        assert prov["stale"] == (d["kernel_sources_sha256"] != bench.kernel_sources_sha())
+        assert ("STALE" in src) == prov["stale"]
+
+
+def test_pmc_traffic_is_marked_stale_when_kernel_sources_change(tmp_path, monkeypatch):
+    """a PMC summary stamped with other kernel sources' sha256 is quoted as
+    STALE; one stamped with today's is not"""
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    base = {"hbm_bytes_per_launch": 1074, "algorithmic_bytes_per_launch": 1073, "commit": "abc"}
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    for f in bench.KERNEL_SOURCES:   # a copy of today's sources under the fake repo
+        (tmp_path / f).parent.mkdir(parents=True, exist_ok=True)
+        (tmp_path / f).write_bytes(open(os.path.join(REPO, f), "rb").read())
+    sha = bench.kernel_sources_sha()
+    (prof / "pmc_c2.json").write_text(json.dumps({**base, "kernel_sources_sha256": sha}))
+    t, src, prov = bench.pmc_traffic("c2", 1073)
+    assert t == 1074 and prov["stale"] is False and "STALE" not in src and prov["measured_commit"] == "abc"
+    (prof / "pmc_c2.json").write_text(json.dumps({**base, "kernel_sources_sha256": "0" * 64}))
+    t, src, prov = bench.pmc_traffic("c2", 1073)
+    assert prov["stale"] is True and "STALE" in src
+    (tmp_path / bench.KERNEL_SOURCES[0]).write_bytes(b"// edited\n")
+    (prof / "pmc_c2.json").write_text(json.dumps({**base, "kernel_sources_sha256": sha}))
+    assert bench.pmc_traffic("c2", 1073)[2]["stale"] is True
+    (prof / "pmc_c2.json").write_text(json.dumps(base))     # unstamped: freshness unknown
+    assert bench.pmc_traffic("c2", 1073)[2]["stale"] is None
 
 
 def test_baseline_config_names():

@@ -54,6 +54,9 @@ for name, res, args in [
     ("ipcbuf_mark_cleared", C.c_int, [P]),
     ("ipcbuf_get_write_byte_xfer", C.c_uint64, [P]), ("ipcbuf_set_soclock_buf", C.c_uint64, [P]),
     ("ipcio_get_start_minimum", C.c_uint64, [P]),
+    ("ipcbuf_set_read_depth", C.c_int, [P, C.c_int]),
+    ("ipcbuf_lock_read", C.c_int, [P]), ("ipcbuf_unlock_read", C.c_int, [P]),
+    ("ipcbuf_get_next_read", C.c_void_p, [P, C.POINTER(C.c_uint64)]),
 ]:
     f = getattr(L, name)
     f.restype, f.argtypes = res, args
@@ -313,6 +316,72 @@ def test_writer_reset_returns_the_ring_to_its_created_state(ring):
             w.write_block(x)
     with dada.Hdu(k, "R") as r:
         assert [r.read_block() for _ in range(3)] == b[2:] + [None]
+
+
+def test_transfer_after_reset_is_not_cut_at_an_old_end_block(ring):
+    """a writer reset returns every transfer slot to its created state: the
+    second transfer after it runs past the block where the second transfer
+    before it ended (e_buf[1] = 3), instead of ending there with that
+    transfer's byte count (libpsrdada's reset rewrites only eod[])"""
+    k = ring(4, 64)
+    b = blocks(8, 64, seed=11)
+    for x in ([b[0]], [b[1]]):         # transfers 0 and 1: a block, then the 0-byte end block
+        with dada.Hdu(k, "W") as w:
+            w.write_block(x[0])
+        with dada.Hdu(k, "R") as r:
+            assert [r.read_block() for _ in range(2)] == x + [None]
+    m = pm.Ring(k)
+    assert [m.s.get("e_buf", x) for x in (0, 1)] == [1, 3]
+    m.close()
+    with dada.Hdu(k, "W") as w:
+        assert L.ipcbuf_reset(w.data) == 0
+        m = pm.Ring(k)
+        assert [m.s.get("e_buf", x) for x in range(8)] == [0] * 8
+        assert [m.s.get("e_byte", x) for x in range(8)] == [0] * 8
+        m.close()
+        w.write_block(b[2])            # transfer 0 after the reset: blocks 0, 1
+    with dada.Hdu(k, "R") as r:
+        assert [r.read_block() for _ in range(2)] == [b[2], None]
+    got = []
+
+    def reader():
+        with dada.Hdu(k, "R") as r:
+            while (x := r.read_block()) is not None:
+                got.append(x)
+
+    t = threading.Thread(target=reader)
+    t.start()
+    with dada.Hdu(k, "W") as w:        # transfer 1 after the reset: blocks 2..6 (old end: 3)
+        for x in b[3:8]:
+            w.write_block(x)
+    t.join(timeout=30)
+    assert not t.is_alive() and got == b[3:8]
+
+
+def test_read_depth_set_before_the_read_lock_is_kept(ring):
+    """ipcbuf_set_read_depth may come before ipcbuf_lock_read: the lock (and
+    an unlock / relock) keeps it, so the reader can hold two blocks"""
+    k = ring(4, 64)
+    b = blocks(3, 64, seed=12)
+    with dada.Hdu(k, "W") as w:
+        for x in b:
+            w.write_block(x)
+    ib = C.create_string_buffer(104)
+    assert L.ipcbuf_connect(ib, k) == 0
+    assert L.ipcbuf_set_read_depth(ib, 2) == 0
+    assert L.ipcbuf_lock_read(ib) == 0
+    n = C.c_uint64()
+    p0 = L.ipcbuf_get_next_read(ib, C.byref(n))
+    p1 = L.ipcbuf_get_next_read(ib, C.byref(n))    # a second block held at once
+    assert p0 and p1 and C.string_at(p0, 64) == b[0] and C.string_at(p1, 64) == b[1]
+    assert L.ipcbuf_mark_cleared(ib) == 0 and L.ipcbuf_mark_cleared(ib) == 0
+    assert L.ipcbuf_unlock_read(ib) == 0 and L.ipcbuf_lock_read(ib) == 0
+    q0 = L.ipcbuf_get_next_read(ib, C.byref(n))
+    q1 = L.ipcbuf_get_next_read(ib, C.byref(n))    # still depth 2 after the relock
+    assert q0 and C.string_at(q0, 64) == b[2] and q1 and n.value == 0   # the 0-byte end block
+    assert L.ipcbuf_mark_cleared(ib) == 0 and L.ipcbuf_mark_cleared(ib) == 0
+    assert L.ipcbuf_unlock_read(ib) == 0
+    L.ipcbuf_disconnect(ib)
 
 
 def test_hard_reset_without_anyone_reading(ring):

@@ -14,8 +14,9 @@ pytestmark = pytest.mark.gpu
 
 
 def test_bench_prints_one_contract_line(gpu):
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--cpu-seconds", "1", "--min-seconds", "0.05"], capture_output=True, text=True, timeout=600, cwd=REPO)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "4", "--warmup", "1",
+                        "--cpu-seconds", "1", "--min-seconds", "0.05", "--bpl1-seconds", "0.2"],
+                       capture_output=True, text=True, timeout=600, cwd=REPO)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
@@ -25,20 +26,35 @@ def test_bench_prints_one_contract_line(gpu):
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
     assert d["metric"] == base["metric"]
-    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1
+    assert d["n_gpus"] == 1 and d["steps"] == 4 and d["warmup"] == 1
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["vs_baseline"] is None
     assert d["config"]["baseline_config"] == "configs[1]" and "workload" in d["config"]
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
-    # the kernel alone (per-launch packet events) is never slower than the
-    # region average it sits inside
+    # the kernel alone (per-launch packet events, >= 16 launches) is never
+    # slower than the region average it sits inside
     assert rf["kernel_only_us"] > 0 and rf["frac_kernel_only"] >= rf["frac"] * 0.97
     assert rf["traffic"] is None or rf["traffic"] > 0
+    # the fraction that goes with `value`: the headline's own numbers
+    per_int = d["config"]["bytes_per_integration"]
+    assert abs(rf["frac_of_value"] - per_int / (d["ms_per_step"] * 1e-3) / 1e9 / 8000.0) < 2e-3
+    assert 0.5 * rf["frac"] < rf["frac_of_value"] <= rf["frac"] * 1.01
+    assert rf["traffic_provenance"] is None or "stale" in rf["traffic_provenance"]
+    assert len(d["provenance"]["kernel_sources_sha256"]) == 64
+    # 4 queued 1 GiB blocks per launch in the headline; the real-time shape
+    # (one per launch) timed and verified beside it
+    assert d["config"]["blocks_per_launch"] == 4
+    one = d["one_per_launch"]
+    assert one["blocks_per_launch"] == 1 and one["verified"] is True and one["value"] > 0
+    assert one["timed_regions"] >= 1 and 0.3 < one["frac_of_value"] < 1.0
     cb = d["cpu_baseline"]
     assert cb["unit"] == d["unit"] and cb["kind"] == "port-tuned" and cb["cores"] >= 1
     assert d["value"] > 0 and cb["value"] > 0 and cb["value_1thread"] > 0
     assert cb["equals_oracle"] is True and cb["oracle_value"] > 0
+    lo, hi = cb["iqr"]
+    assert cb["passes_range"][0] <= lo <= cb["value"] <= hi <= cb["passes_range"][1]
+    assert len(cb["cpus_picked"]["cpus"]) == cb["cores"] and "cgroup_cpu_stat_delta" in cb
     assert cb["isa"] in ("avx512vnni", "avx512bw", "avx2", "scalar")
     # the ranks that ran, read back from the process (no group at N = 1)
     assert d["rccl_ranks"] == 0 and d["distinct_gpus"] == 1
@@ -110,3 +126,30 @@ def test_configs3_four_rank_rehearsal_full_size(gpu):
     assert "4 distinct block" in d["verification"]["what"]
     assert [x["rank"] for x in d["rank_devices"]] == [0, 1, 2, 3]
     assert d["distinct_gpus"] >= 1 and d["dist_backend"] == "gloo" and d["rccl_ranks"] == 0
+
+
+def test_configs4_eight_subbands_full_size(gpu):
+    """configs[4] as the driver's 8-GPU run would do it, rehearsed with gloo
+    on this box's one GPU: 8 ranks, each integrating full 4 GiB blocks of
+    1024 ch x 2 pol int8 of its own sub-band (2 distinct blocks per rank, 64
+    GiB in HBM), the spectra of every rank gathered to rank 0 and every one
+    checked against the C oracle (BASELINE.json configs[4]; SURVEY 8d C5,
+    8e).  The ranks share one GPU, so the rate is not a scaling figure."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--config", "c5", "--gpus", "8",
+                        "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--min-seconds", "0",
+                        "--cpu-seconds", "0", "--blocks", "2", "--dist-timeout", "240"],
+                       capture_output=True, text=True, timeout=900, cwd=REPO,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["verified"] is True and d["n_gpus"] == 8 and d["ranks"] == 8
+    assert d["config"]["baseline_config"] == "configs[4]"
+    assert d["config"]["bytes_per_integration"] == 1 << 32 and d["config"]["nchan"] == 1024
+    assert d["config"]["input"].startswith("HBM-resident, 2 rotating blocks")
+    assert [x["rank"] for x in d["rank_devices"]] == list(range(8))
+    assert d["distinct_gpus"] >= 1 and d["dist_backend"] == "gloo"
+    assert d["verification"]["gather"] == "rank 0 holds every rank's K spectra"
+    assert "2 distinct block" in d["verification"]["what"]
+    assert len(d["per_rank_ms_per_step"]) == 8

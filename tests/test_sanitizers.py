@@ -30,6 +30,91 @@ def test_dada_layer_under_sanitizer(tmp_path, san, key):
     assert "runtime error" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr
 
 
+STAGE = os.path.join(REPO, "paf-baseband2power_amd", "csrc", "host", "paf_baseband2power.c")
+STUB = os.path.join(REPO, "tests", "c", "b2p_cpu_stub.c")
+DADA_SRC = [os.path.join(REPO, "paf-baseband2power_amd", "csrc", "dada", f)
+            for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c")]
+
+
+def _stage_tsan(tmp_path, as_device: bool) -> str:
+    """paf_baseband2power built with -fsanitize=thread against the CPU test
+    double of libpafb2p (tests/c/b2p_cpu_stub.c) and libpafdada's sources;
+    as_device: host rings take the GPU-resident paths (test-only
+    -DB2P_TEST_HOST_RING_AS_DEVICE), i.e. worker_gather_dev for -n N and
+    run_device_pipelined for one sub-band"""
+    exe = tmp_path / ("stage_tsan_dev" if as_device else "stage_tsan")
+    defs = ["-DB2P_TEST_HOST_RING_AS_DEVICE"] if as_device else []
+    subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
+                    "-fsanitize=thread", "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"),
+                    *defs, STAGE, STUB, *DADA_SRC, "-o", str(exe), "-pthread", "-ldl", "-lm"], check=True)
+    return str(exe)
+
+
+@pytest.mark.parametrize("mode", ["gathered", "gathered_dev", "split", "single_dev"])
+def test_stage_threads_under_tsan(tmp_path, mode):
+    """The stage's worker threads under ThreadSanitizer (CPU, no GPU):
+      gathered      -n 3 over host rings (worker: one thread per sub-band,
+                    barriers per round, the root gathers and writes)
+      gathered_dev  -n 3 taking the GPU-resident path (worker_gather_dev:
+                    rounds of queued blocks, launches in flight, the root's
+                    asynchronous gathers, the real-time drain)
+      split         -t 2 (worker_split: shares of one host block, exact
+                    partials reduced by the root)
+      single_dev    one sub-band on the GPU-resident path (run_device_pipelined)
+    Producers are the normal paf_diskdb builds; every spectrum is checked
+    against the C oracle, so the threads also moved the right data."""
+    import numpy as np
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_c as co
+    import b2p_oracle as npo
+    from paf_b2p import dada, pipeline
+    from test_gpu_pipeline import write_conf
+    seed = 20181105
+    exe = _stage_tsan(tmp_path, as_device=mode.endswith("_dev"))
+    g = npo.Geom(nbit=8, nchan_chunk=64, nsamp_int=1 << 10)
+    nblk = 7   # more blocks than the 3-block ring: producers wait, rounds overlap
+    nsub = 3 if mode.startswith("gathered") else 1
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 64\nTSAMP 0.84375\n")
+    files, payloads = [], []
+    for r in range(nsub):
+        p = co.fill_synthetic(g, g.block_bytes * nblk, seed, r, 3)
+        f = tmp_path / f"sb{r}.dada"
+        dada.write_dada_file(str(f), "x 1\n", p)
+        files.append(str(f))
+        payloads.append(p)
+    kin = 0x6a10 + (os.getpid() % 64) * 0x100 + ["gathered", "gathered_dev", "split", "single_dev"].index(mode) * 0x40
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 10, 1, 256, 64, kin, kin + 0x8000, str(hfile))
+    env_keep = dict(os.environ)
+    os.environ["TSAN_OPTIONS"] = "halt_on_error=1 second_deadlock_stack=1"
+    try:
+        if nsub > 1:
+            outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, files, nsub=nsub, gather=True,
+                                timeout=240, stage_exe=exe)
+        else:
+            outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, files[0], split=2 if mode == "split" else 1,
+                                timeout=240, stage_exe=exe)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_keep)
+    hdr, data = dada.read_dada_file(outs[0])
+    sp = data.view(np.float32).reshape(-1, nsub, g.nout)
+    assert sp.shape[0] == nblk
+    for i in range(nblk):
+        for r in range(nsub):
+            blk = payloads[r][i * g.block_bytes:(i + 1) * g.block_bytes]
+            assert np.array_equal(sp[i, r].view(np.uint32), co.power(g, blk).view(np.uint32)), (i, r)
+    log = open(str(tmp_path / "out" / "paf_baseband2power.log")).read()
+    assert "WARNING: ThreadSanitizer" not in log
+    assert f"FINISH PAF_PROCESS: {nblk} integrations, 0 skipped, ok" in log, log[-2000:]
+    if mode == "gathered_dev":
+        assert "queued blocks in rounds" in log
+    if mode == "split":
+        assert "reduce of 2 time shares" in log
+
+
 def test_capture_receive_threads_under_tsan(tmp_path):
     """paf_capture's receive threads and the sorting thread (slot rings with
     C11 acquire/release, the stop flag) under ThreadSanitizer, in record

@@ -3,7 +3,7 @@
 # Each GPU step has its own time limit; a fault/abort/timeout (exit other
 # than 0 or 1) ends the script at once -- nothing further touches the GPU.
 #   usage: tools/gpu_check.sh [steps...]
-#   steps: smoke tests bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
+#   steps: smoke tests contract bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 #          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs
@@ -33,6 +33,8 @@ for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -q -rf ;;
+    contract) run pytest_contract 900 python3 -u -m pytest tests/test_gpu_bench_contract.py -x -v -rf \
+                --timeout 800 --timeout-method thread ;;
     bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
     benchdrv) run bench_drv 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchnf) run bench_nofuse 600 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-fuse ;;

@@ -9,6 +9,12 @@ HBM traffic per launch follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and
 WRITE_SIZE come from separate --pmc passes (they do not fit one TCC pass),
 are in KiB, and FETCH_SIZE reports exactly half the bytes of a wide
 coalesced streaming read on gfx950, so it is doubled.
+
+Provenance: the summary records the sha256 of the integrate kernel's sources
+(bench.KERNEL_SOURCES) the passes ran -- read from the profiled bench.py's own
+JSON line (--bench-log; the GPU box has no git) or else hashed here -- plus
+the git commit and the last commit that touched those sources.  bench.py
+marks the traffic it quotes STALE when today's sources hash differently.
 """
 from __future__ import annotations
 
@@ -18,6 +24,8 @@ import json
 import os
 import shutil
 import statistics
+import subprocess
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = "b2p_integrate_kernel"
@@ -46,7 +54,22 @@ def main():
     ap.add_argument("--blocks-per-launch", type=int, default=1,
                     help="integrations per integrate launch in the profiled run (bench.py's)")
     ap.add_argument("--kernel", default=KERNEL)
+    ap.add_argument("--bench-log", help="stdout of a profiled bench.py run (its JSON line names the "
+                                        "kernel sources' sha256 it ran)")
     a = ap.parse_args()
+    sys.path.insert(0, REPO)
+    import bench
+    sha, sha_from = bench.kernel_sources_sha(), "hashed by tools/pmc_summary.py at summary time"
+    for path in filter(None, [a.bench_log]):
+        for ln in open(path):
+            if ln.startswith("{"):
+                got = (json.loads(ln).get("provenance") or {}).get("kernel_sources_sha256")
+                if got:
+                    sha, sha_from = got, f"from the profiled run's JSON line ({os.path.relpath(path, REPO)})"
+
+    def git(*args):
+        r = subprocess.run(["git", "-C", REPO, *args], capture_output=True, text=True)
+        return r.stdout.strip() if r.returncode == 0 else None
     f = counter(a.fetch, "FETCH_SIZE", a.kernel)
     w = counter(a.write, "WRITE_SIZE", a.kernel)
     fetch_kib, write_kib = statistics.median(f), statistics.median(w)
@@ -66,6 +89,11 @@ def main():
         "blocks_per_launch": a.blocks_per_launch,
         "traffic_over_algorithmic": round(hbm / alg, 4) if alg else None,
         "source": [fetch_dst, write_dst],
+        "kernel_sources_sha256": sha,
+        "kernel_sources_sha256_from": sha_from,
+        "kernel_sources_match_tree": sha == bench.kernel_sources_sha(),
+        "commit": git("rev-parse", "HEAD"),
+        "kernel_sources_commit": git("log", "-1", "--format=%H", "--", *bench.KERNEL_SOURCES),
     }
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
     json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{a.config}.json"), "w"), indent=1)
