@@ -1,7 +1,11 @@
-"""Host-code sanitizers (CPU): the DADA layer built with ASan+UBSan and with
-TSan, driven by tests/c/ring_stress.c (writer + 2 reader threads, EOD, header
-edits).  GPU sanitizers are not available on the test pool; these cover the
-C code around the kernels."""
+"""Host-code sanitizers (CPU).  GPU sanitizers are not available on the test
+pool; these cover the C code around the kernels:
+  * the DADA layer with ASan+UBSan and with TSan: tests/c/ring_stress.c
+    (writer + 2 reader threads, EOD, header edits) and tests/c/ring_surface.c
+    (deferred start of data, resets, a viewer, tell / seek, read depth 2);
+  * the stage's worker threads (paf_baseband2power.c) under TSan, linked
+    against a CPU test double of libpafb2p (tests/c/b2p_cpu_stub.c);
+  * paf_capture's receive and sorting threads under TSan."""
 import os
 import subprocess
 
@@ -16,6 +20,7 @@ DRIVER = os.path.join(REPO, "tests", "c", "ring_stress.c")
 
 @pytest.mark.parametrize("san,key", [("address,undefined", "7c10"), ("thread", "7c20")])
 def test_dada_layer_under_sanitizer(tmp_path, san, key):
+    """writer + two readers (depth 1 and 2) through a 3-block ring"""
     exe = tmp_path / "ring_stress"
     cmd = ["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", f"-fsanitize={san}",
            "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"), DRIVER, *SRC,
@@ -24,6 +29,27 @@ def test_dada_layer_under_sanitizer(tmp_path, san, key):
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
                TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([str(exe), key], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "errors 0" in r.stdout
+    assert "runtime error" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr
+
+
+@pytest.mark.parametrize("san,key", [("address,undefined", "7c30"), ("thread", "7c40")])
+def test_ring_surface_under_sanitizer(tmp_path, san, key):
+    """round 3's libpafdada surface (tests/c/ring_surface.c) under ASan+UBSan
+    and TSan: a deferred start of data (ipcio 'w', ipcio_start mid-block,
+    ipcio_stop) three times, a writer ipcbuf_reset, a viewer attached during
+    a transfer, ipcbuf_hard_reset between transfers, ipcio_tell / seek, two
+    readers, one holding two blocks at read depth 2 (set before its read
+    lock), every transfer checked byte for byte"""
+    exe = tmp_path / "ring_surface"
+    subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
+                    f"-fsanitize={san}", "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "c", "ring_surface.c"), *SRC, "-o", str(exe), "-pthread",
+                    "-ldl", "-lm"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([str(exe), key], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "errors 0" in r.stdout
