@@ -315,7 +315,7 @@ int b2p_group_close(b2p_group_t *grp);
  *   region's elapsed time (inter-launch gaps and finalizes included), i.e.
  *   an upper bound of the summed launch durations, with no per-launch cost.
  *   The opening event goes on the stream with the region's first piece of
- *   work (launch, staging copy or finalize), so the caller's own time
+ *   work (integrate or assembly launch, staging copy, memset or finalize), so the caller's own time
  *   between set_timing(ctx, 2) and that call is not counted.
  * mode 0: off.  Closing a mode-2 region records its end event and returns
  *   without waiting; b2p_get_stats waits for it and adds the region. */

@@ -1017,6 +1017,7 @@ int b2p_assemble(b2p_ctx_t *c, const void *dfs, uint64_t ndf, uint32_t df_bytes,
   a.block_ndf = block_ndf;
   a.nchunk = nchunk;
   a.counts = counts;
+  if (int rm = region_mark(c)) return rm;  // a timing region may open with an assembly
   CK(c, launch_assemble(a, (uint32_t)c->tun.assemble_grid, c->stream));
   return B2P_OK;
 }
@@ -1040,6 +1041,7 @@ int b2p_memset(b2p_ctx_t *c, void *dev, int value, size_t bytes) {
   if (!c || (!dev && bytes)) return B2P_EINVAL;
   if (!bytes) return B2P_OK;
   CK(c, hipSetDevice(c->device));
+  if (int rm = region_mark(c)) return rm;
   CK(c, hipMemsetAsync(dev, value, bytes, c->stream));
   return B2P_OK;
 }

@@ -240,3 +240,37 @@ def test_missing_rank_rendezvous_is_bounded():
     assert r.returncode != 0
     assert time.time() - t0 < 120
     assert r.stdout.strip() == ""
+
+
+def test_trace_legs_cuts_a_kernel_trace_by_the_bench_phases(tmp_path):
+    """tools/trace_legs.py: the bench line's launch_phases slice the trace's
+    integrate dispatches (in dispatch order) into legs of one shape each"""
+    import json
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import trace_legs
+    hdr = ('"Kind","Agent_Id","Queue_Id","Stream_Id","Thread_Id","Dispatch_Id","Kernel_Id","Kernel_Name",'
+           '"Correlation_Id","Start_Timestamp","End_Timestamp"\n')
+    rows, t, did = [], 1000, 0
+    plan = [("warmup", 2, 600), ("headline", 10, 596), ("one_per_launch_warmup", 1, 150),
+            ("one_per_launch", 20, 149), ("calibration_warmup", 1, 597), ("calibration", 16, 591)]
+    for _, n, us in plan:
+        for _ in range(n):
+            did += 1
+            rows.append(f'"KERNEL_DISPATCH","Agent 2",1,1,1,{did},7,"void b2p::b2p_integrate_kernel<0, 1, 4, true>'
+                        f'(b2p::IntegrateArgs)",{did},{t},{t + us * 1000}\n')
+            did += 1   # another kernel in between (a finalize) is skipped
+            rows.append(f'"KERNEL_DISPATCH","Agent 2",1,1,1,{did},8,"b2p::b2p_finalize_kernel(b2p::FinalizeArgs)",'
+                        f'{did},{t},{t + 4000}\n')
+            t += us * 1000 + 5000
+    tr = tmp_path / "trace.csv"
+    tr.write_text(hdr + "".join(rows[::-1]))   # order is restored by dispatch id
+    line = {"config": {"bytes_per_integration": 1 << 30},
+            "roofline": {"launch_phases": [[n, c] for n, c, _ in plan], "algorithmic_bytes_per_launch": 4 << 30,
+                         "peak": 8000.0, "avg_launch_us": 596.5, "kernel_only_us": 591.0}}
+    out = trace_legs.legs(str(tr), line)
+    assert out["counts_agree"] and out["integrate_dispatches"] == 50
+    assert out["legs"]["headline"]["avg_us"] == 596.0 and out["legs"]["headline"]["launches"] == 10
+    assert out["legs"]["one_per_launch"]["avg_us"] == 149.0
+    assert out["legs"]["calibration"]["launches"] == 16
+    assert abs(out["legs"]["headline"]["frac_of_8TBps"] - (4 << 30) / 596e-6 / 1e9 / 8000) < 1e-4
+    assert json.dumps(out)

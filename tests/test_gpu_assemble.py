@@ -69,3 +69,37 @@ def test_df_stream_to_spectrum(gpu):
         for b in (d_dfs, d_chk, d_blk, d_cnt):
             b.free()
     assert np.array_equal(out.view(np.uint32), co.power(g, block).view(np.uint32))
+
+
+def test_assembly_opens_a_timing_region(gpu):
+    """b2p_set_timing(2) around assembly launches only: the region's opening
+    event goes in front of the first assembly (as for integrate launches),
+    so the region spans the work -- tools/bench_assemble.py's figure.  Before
+    round 4 only integrate launches, copies and finalizes opened a region,
+    and an assembly-only region measured ~0.5 us."""
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * 1024)
+    block_ndf, nchunk = 1024, 48
+    block = npo.fill_synthetic(g, g.block_bytes, SEED, 2, 5)
+    dfs, chunk = npo.df_stream(block, nchunk, 1000, 54)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        d_dfs, d_chk = it.upload(dfs.reshape(-1)), it.upload(chunk)
+        d_blk, d_cnt = it.alloc(g.block_bytes), it.upload(np.zeros(nchunk + 3, np.uint64))
+        it.assemble(d_dfs, dfs.shape[0], d_chk, 1000, 54, d_blk, block_ndf, nchunk, d_cnt)   # warm
+        it.sync()
+        it.reset_stats()
+        it.set_timing(2)
+        for _ in range(4):
+            it.assemble(d_dfs, dfs.shape[0], d_chk, 1000, 54, d_blk, block_ndf, nchunk, d_cnt)
+        it.set_timing(0)
+        it.sync()
+        us = it.stats()["kernel_ms"] * 1e3 / 4
+        got = it.download(d_blk)
+        for b in (d_dfs, d_chk, d_blk, d_cnt):
+            b.free()
+    assert np.array_equal(got, block)
+    # 1024 x 48 frames, 7232 B read + 7168 B written each: 708 MB per assembly;
+    # at <= 8 TB/s that is >= 88 us
+    moved = block_ndf * nchunk * (7232 + 7168)
+    assert moved / (us * 1e-6) / 1e9 < 8000.0, us
+    assert us > 50, us

@@ -36,6 +36,7 @@ for s in $STEPS; do
     contract) run pytest_contract 900 python3 -u -m pytest tests/test_gpu_bench_contract.py -x -v -rf \
                 --timeout 800 --timeout-method thread ;;
     bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
+    syncprobe) run sync_probe 300 python3 tools/sync_probe.py --regions 400 ;;
     benchdrv) run bench_drv 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchnf) run bench_nofuse 600 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-fuse ;;
     bench5) run bench_c5 600 python3 bench.py --config c5 --steps 30 --warmup 3 --cpu-seconds 0 ;;
@@ -150,11 +151,11 @@ for s in $STEPS; do
     tunebmf) run tune_bmf2 600 python3 tools/tune.py --config bmf --threads 168,256,336,448,512 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run \
             -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
-    pmc) # 12 steps: every launch carries bench.py's default 4 blocks (c2)
+    pmc) # 12 steps: every launch carries bench.py's default 4 blocks (c2); no one-per-launch leg
          run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
-            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
-            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 ;;
     pmc5) run pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run \
             -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run \

@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--repeat", type=int, default=1, help="run each case this many times")
     ap.add_argument("--sleep", type=float, default=2.0,
                     help="idle seconds before each run: the previous run freed GiBs, and launches "
-                         "in the next seconds run 2-8 %% slower (profiles/r01_free_effect.txt)")
+                         "in the next seconds run 2-8 %% slower (profiles/archive/r01_free_effect.txt)")
     ap.add_argument("--keep", action="store_true", help="never free a run's buffers")
     ap.add_argument("--multi", type=int, default=1,
                     help="integrations per launch (b2p_integrate_n), e.g. 8")
