@@ -304,8 +304,10 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
 
     res = child(cb.child_env(threads, cpus=picked["cpus"]), seconds)
     if res is not None:
-        res["cpus_picked"] = {**picked, "rule": "one logical CPU per physical core, the idlest allowed "
-                                                "cores of one NUMA node over the sample before the legs"}
+        res["cpus_picked"] = {**picked, "rule": "one logical CPU per physical core, dealt round-robin over "
+                                                "every L3 domain (CCD) of every NUMA node, the idlest allowed "
+                                                "core of each over the sample before the legs; CPU order, so "
+                                                "each thread's first-touched tile is on its own node"}
     ncpu = os.cpu_count() or threads
     if res is not None and ncpu > threads:
         res["all_cpus"] = child(cb.child_env(ncpu, places="threads", wait="passive"),
@@ -459,12 +461,20 @@ def main(argv=None) -> int:
             it.integrate(blk, dst, True)
 
     cur = {"bpl": bpl}  # the launch shape of the regions being timed
+    # integrate launches per bench phase, in issue order (roofline.launch_phases:
+    # tools/trace_legs.py cuts a rocprofv3 kernel trace of this run by them)
+    phases, nl = [], {"n": 0, "mark": 0}
+
+    def phase(name):
+        phases.append([name, nl["n"] - nl["mark"]])
+        nl["mark"] = nl["n"]
 
     def steps(k0, row0, n):
         """integrations k0 .. k0+n-1 into output rows row0 .."""
         j = 0
         while j < n:
             m = min(cur["bpl"], n - j)
+            nl["n"] += 1
             if m == 1:
                 step(k0 + j, row0 + j)
             else:
@@ -511,6 +521,7 @@ def main(argv=None) -> int:
         steps(kk, 0, 1 if bpl == 1 else min(bpl, K))
         kk += 1 if bpl == 1 else min(bpl, K)
     it.sync()
+    phase("warmup")
     if dist_on:  # a communicator's first collective sets up its channels
         wd.arm(f"first {a.dist_backend} collective (communicator set-up)")
         try:
@@ -572,6 +583,7 @@ def main(argv=None) -> int:
         return els_max, els, got, kk - K, it.stats()
 
     els_max, els, gathered, last_k0, st = timed_leg(a.min_seconds)
+    phase("headline")
     if dist_on:
         mine = torch.tensor([statistics.median(els)], dtype=torch.float64,
                             device="cuda" if rccl else "cpu")
@@ -656,7 +668,9 @@ def main(argv=None) -> int:
         cur["bpl"] = 1
         steps(kk, 0, 1)  # warm the one-block launch shape
         kk += 1
+        phase("one_per_launch_warmup")
         els1_max, _, gathered1, last1_k0, st1 = timed_leg(a.bpl1_seconds)
+        phase("one_per_launch")
         el1 = statistics.median(els1_max)
         if dist_on:
             wd.arm("verification against the oracle (one block per launch)", max(a.dist_timeout, 900.0))
@@ -684,12 +698,14 @@ def main(argv=None) -> int:
         n_c = (K // bpl) * bpl or K  # whole launches of the headline shape, rows < K
         steps(0, 0, n_c)
         it.sync()
+        phase("calibration_warmup")
         it.reset_stats()
         it.set_timing(1)
         while it.stats()["launches"] < 16:
             steps(0, 0, n_c)
         it.set_timing(0)
         it.sync()
+        phase("calibration")
         cs = it.stats()
         if cs["launches"]:
             calib_us = cs["kernel_ms"] / cs["launches"] * 1e3
@@ -780,6 +796,7 @@ def main(argv=None) -> int:
                 "frac_kernel_only": (round(bytes_per_launch / (calib_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
                                      if calib_us else None),
                 "launches_timed": int(st["launches"]),
+                "launch_phases": phases,
                 "timing": ("frac: HIP events on the integrator stream bracketing each timed region's "
                            "launches, summed over the regions (region / launches: gaps and finalizes "
                            "included, the region's host bracketing not); frac_of_value: the host-timed "

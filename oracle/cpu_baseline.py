@@ -7,9 +7,9 @@ block of the bench's workload held in host RAM (no file I/O), so the passes
 stream from DRAM rather than the L3 (the EPYC 9575F host has 512 MiB of L3;
 a 1 GiB block does not fit).  SURVEY.md 8(d) "CPU baseline": the reference has
 no CPU path, so the baseline is the port, at 1 thread and at every CPU this
-process may use.  bench.py picks the CPUs (pick_cpus): one per physical core, the
-idlest allowed cores of one NUMA node, listed as explicit OpenMP places; every
-leg reports the cgroup's cpu.stat deltas (periods throttled, time throttled)
+process may use.  bench.py picks the CPUs (pick_cpus): one per physical core,
+dealt over every L3 domain (CCD) of both NUMA nodes, listed as explicit OpenMP
+places; every leg reports the cgroup's cpu.stat deltas (periods throttled, time throttled)
 beside its median and interquartile range, so a slow box shows why.
 
 Run as a child process of bench.py (never imported into the GPU process), so
@@ -20,7 +20,7 @@ environment set for it alone:
 
 and prints ONE JSON object.  Threads are bound one per OpenMP place
 (OMP_PROC_BIND=close); the block is filled by the same threads first, so its
-pages sit on the NUMA node those cores belong to.
+pages sit on the NUMA node of the thread that streams them.
 """
 from __future__ import annotations
 
@@ -148,12 +148,22 @@ def busy_fraction(cpus, seconds: float = 0.25) -> dict:
 
 
 def pick_cpus(n: int, sample_s: float = 0.25) -> dict:
-    """n logical CPUs for the timed leg, one per physical core, on one NUMA
-    node: the allowed cores that were idlest over `sample_s` (the GPU box's
-    host is shared with other jobs whose threads are not confined to a
-    cpuset, so packing from CPU 0 can land on busy cores), preferring the
-    node with the most idle capacity.  Returns the CPUs, their node and how
-    busy they and the host were beforehand."""
+    """n logical CPUs for the timed leg, one per physical core, dealt
+    round-robin over every L3 domain (CCD) of every NUMA node, the idlest
+    allowed core of each domain first (the GPU box's host is shared with other
+    jobs whose threads are not confined to a cpuset).  Listed in CPU order,
+    so with OMP_PROC_BIND=close the first threads sit on node 0 and the equal
+    contiguous time tiles they first-touch stay on their own node.  Returns
+    the CPUs, their nodes and L3 domains, and how busy they and the host were
+    beforehand.
+
+    Why every CCD of both sockets: a streaming pass is bound by each CCD's
+    link to the IO die and then by each socket's DRAM, not by the cores.  On
+    one GPU-box host (profiles/r04_cpu_spread.jsonl) the same 16 threads read
+    77 x 10^3 Msamples/s packed into 2 CCDs, 238-240 x 10^3 dealt over the 8
+    CCDs of one node and 299-305 x 10^3 over the 16 CCDs of both; round 3's
+    rule (idlest cores of one node, in core order) landed on 3-6 CCDs and so
+    moved between 54 and 133 x 10^3 from box to box."""
     allowed = allowed_cpus()
     busy = busy_fraction(allowed, sample_s)
     cores = {}   # (package, core) -> first allowed sibling
@@ -162,23 +172,39 @@ def pick_cpus(n: int, sample_s: float = 0.25) -> dict:
         key = ((_read(t + "physical_package_id") or "0").strip(), (_read(t + "core_id") or str(c)).strip())
         cores.setdefault(key, c)
     reps = sorted(cores.values(), key=lambda c: (busy.get(c, 0.0), c))
-    nodes = numa_nodes()
-    node_of = {c: nd for nd, cs in nodes.items() for c in cs}
-    by_node = {}
-    for c in reps:
-        by_node.setdefault(node_of.get(c), []).append(c)
-    full = [nd for nd, cs in by_node.items() if len(cs) >= n]
-    if full:   # the node whose n idlest cores are idlest together
-        nd = min(full, key=lambda nd: sum(busy.get(c, 0.0) for c in by_node[nd][:n]))
-        pick = by_node[nd][:n]
-    else:
-        nd, pick = None, reps[:n]
+    pick = spread_l3(reps, n)
     if len(pick) < n:   # fewer physical cores than threads: add SMT siblings
         pick += [c for c in sorted(allowed, key=lambda c: busy.get(c, 0.0)) if c not in pick][:n - len(pick)]
-    return {"cpus": sorted(pick), "node": nd,
+    nodes = numa_nodes()
+    node_of = {c: nd for nd, cs in nodes.items() for c in cs}
+    return {"cpus": sorted(pick), "nodes": sorted({node_of.get(c) for c in pick if c in node_of}),
+            "l3_domains": len({l3_domain(c) for c in pick}),
+            "l3_domains_allowed": len({l3_domain(c) for c in reps}),
             "busy_before": round(sum(busy.get(c, 0.0) for c in pick) / max(1, len(pick)), 4),
             "host_busy_before": round(sum(busy.values()) / max(1, len(busy)), 4),
             "sample_s": sample_s}
+
+
+def l3_domain(cpu: int) -> str:
+    """the L3 (on EPYC: the CCD) a logical CPU sits behind"""
+    c = "/sys/devices/system/cpu/cpu%d/cache/index3/" % cpu
+    return ((_read(c + "id") or "").strip() or (_read(c + "shared_cpu_list") or "").strip()
+            or "cpu%d" % cpu)
+
+
+def spread_l3(cores: list, n: int) -> list:
+    """n of `cores` (idlest first), dealt round-robin over their L3 domains
+    taken in CPU order"""
+    doms = {}
+    for c in cores:
+        doms.setdefault(l3_domain(c), []).append(c)
+    order = sorted(doms.values(), key=lambda cs: cs[0])
+    pick = []
+    while len(pick) < n and any(order):
+        for cs in order:
+            if cs and len(pick) < n:
+                pick.append(cs.pop(0))
+    return pick
 
 
 def host_cpu() -> dict:
@@ -261,7 +287,8 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
     # the port is a baseline, not the checker: its sums must equal the oracle's
     equal = bool(np.array_equal(port(threads), oracle(threads)))
     nodes = numa_nodes()
-    node = next((n for n, c in nodes.items() if first in c), None)
+    places = [int(x.strip("{}")) for x in pl.split(",")] if pl.startswith("{") else [first]
+    used_nodes = sorted({n for n, c in nodes.items() for p in places if p in c})
     ln = leg(r_n, el_n, thr_n)
     return {
         "value": ln["value"], "unit": "Msamples/s", "cores": threads,
@@ -283,7 +310,8 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
         "oracle_value": round(statistics.median(r_o), 2),
         "oracle": (f"scalar C restatement (the checker, oracle/b2p_oracle.c): {len(r_o)} passes "
                    f"({el_o:.1f} s) at {threads} threads, median"),
-        "numa": {"node": node, "binding": binding + "; block first-touched by the same threads"},
+        "numa": {"nodes": used_nodes, "binding": binding + "; block first-touched by the same threads "
+                 "(equal contiguous tiles, the split the passes use)"},
         "host": host,
     }
 

@@ -6,7 +6,7 @@
 #   steps: smoke tests contract bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs
+#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -32,10 +32,13 @@ run() {  # name limit cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python3 -m pytest tests -m gpu -q -rf ;;
+    tests) run pytest_gpu 1000 python3 -u -m pytest tests -m gpu -v -rf --timeout 600 --timeout-method thread ;;
     contract) run pytest_contract 900 python3 -u -m pytest tests/test_gpu_bench_contract.py -x -v -rf \
                 --timeout 800 --timeout-method thread ;;
     bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
+    cpuspread) run cpu_spread 300 python3 tools/cpu_spread_probe.py 4 ;;
+    cpuspread2) run cpu_spread_a 300 python3 tools/cpu_spread_probe.py 4 spread,spread2,packed &&
+                run cpu_spread_b 300 python3 tools/cpu_spread_probe.py 4 spread2,spread,packed ;;
     syncprobe) run sync_probe 300 python3 tools/sync_probe.py --regions 400 ;;
     benchdrv) run bench_drv 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchnf) run bench_nofuse 600 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-fuse ;;
