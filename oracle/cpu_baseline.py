@@ -132,6 +132,19 @@ def _idle_ticks() -> dict:
     return out
 
 
+def others_busy(a: dict, b: dict, mine: set) -> float | None:
+    """mean busy fraction, between two /proc/stat samples, of the host's
+    logical CPUs this leg did not run on: the other tenants of a shared host,
+    whose memory traffic competes with a streaming pass"""
+    fr = []
+    for c in b:
+        if c in a and c not in mine:
+            dt = b[c][1] - a[c][1]
+            if dt > 0:
+                fr.append(1.0 - (b[c][0] - a[c][0]) / dt)
+    return round(sum(fr) / len(fr), 4) if fr else None
+
+
 def busy_fraction(cpus, seconds: float = 0.25) -> dict:
     """{cpu: fraction of the last `seconds` it spent busy}, from /proc/stat
     (other tenants of the host included: this job does not run meanwhile)"""
@@ -245,6 +258,7 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
     host = host_cpu()  # before OpenMP binds this thread to its first place
     pl = os.environ.get("OMP_PLACES", "")
     first = int(pl[1:pl.index("}")]) if pl.startswith("{") else min(os.sched_getaffinity(0))
+    places = [int(x.strip("{}")) for x in pl.split(",")] if pl.startswith("{") else [first]
     g = npo.Geom(**geom)
     buf = np.empty(g.block_bytes, dtype=np.uint8)
     co.fill_synthetic(g, g.block_bytes, seed, 0, 0, out=buf)   # first touch by the bound threads
@@ -260,7 +274,7 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
         warm = buf[: g.frame_bytes * max(1, (64 << 20) // g.frame_bytes)]
         (co.port_integrate(g, warm, nthreads=nt, isa=isa) if fn is port
          else co.integrate(g, warm, nthreads=nt))
-        st0 = cpu_stat()
+        st0, tk0 = cpu_stat(), _idle_ticks()
         rates, t_all = [], time.perf_counter()
         while len(rates) < min_passes or time.perf_counter() - t_all < budget:
             t0 = time.perf_counter()
@@ -268,7 +282,9 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
             rates.append(per_pass / (time.perf_counter() - t0) / 1e6)
             if len(rates) >= 10000:
                 break
-        return rates, time.perf_counter() - t_all, cpu_stat_delta(st0, cpu_stat())
+        d = cpu_stat_delta(st0, cpu_stat()) or {}
+        d["others_busy"] = others_busy(tk0, _idle_ticks(), set(places[:nt]))
+        return rates, time.perf_counter() - t_all, d
 
     def leg(rates, el, thr):
         return {"value": round(statistics.median(rates), 2), "passes": len(rates), "seconds": round(el, 2),
@@ -287,7 +303,6 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
     # the port is a baseline, not the checker: its sums must equal the oracle's
     equal = bool(np.array_equal(port(threads), oracle(threads)))
     nodes = numa_nodes()
-    places = [int(x.strip("{}")) for x in pl.split(",")] if pl.startswith("{") else [first]
     used_nodes = sorted({n for n, c in nodes.items() for p in places if p in c})
     ln = leg(r_n, el_n, thr_n)
     return {

@@ -4,9 +4,10 @@ port (oracle/cpu_baseline.py, one full configs[1] block in host RAM) bound
 three ways on one host, one child process each:
 
   packed  -- 16 cores filling the fewest L3 domains (CCDs) of one node
-  spread  -- 16 cores dealt over every L3 domain of one node (bench.py's rule)
+  spread  -- 16 cores dealt over every L3 domain of one node
   idlest  -- the 16 idlest cores of the node in core order (round 3's rule)
   spread2 -- 16 cores dealt over every L3 domain of every node, node-major
+             (bench.py's rule; spread2:K = its first K CPUs, K threads)
              (threads 0..7 on node 0: the time tiles they first-touch stay local)
 
 A streaming pass is bound by each CCD's link to the IO die, so `packed` is
@@ -33,7 +34,7 @@ def main():
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 3.0
     n = cb.effective_cpus()
     picked = cb.pick_cpus(n)
-    nd = picked["node"]
+    nd = picked["nodes"][0] if picked["nodes"] else None
     nodes = cb.numa_nodes()
     allowed = set(cb.allowed_cpus())
     cores = {}
@@ -42,9 +43,11 @@ def main():
         key = ((cb._read(t + "physical_package_id") or "0").strip(), (cb._read(t + "core_id") or str(c)).strip())
         cores.setdefault(key, c)
     reps = sorted(cores.values())
+    busy0 = cb.busy_fraction(reps, 0.25)
     doms = {}
     for c in reps:
         doms.setdefault(cb.l3_domain(c), []).append(c)
+    spread_l3_node = sorted(cb.spread_l3(sorted(reps, key=lambda c: (busy0.get(c, 0.0), c)), n))
     packed = [c for cs in sorted(doms.values(), key=lambda cs: cs[0]) for c in cs][:n]
     busy = cb.busy_fraction(reps, 0.25)
     idlest = sorted(sorted(reps, key=lambda c: (busy.get(c, 0.0), c))[:n])
@@ -54,11 +57,18 @@ def main():
         key = ((cb._read(t + "physical_package_id") or "0").strip(), (cb._read(t + "core_id") or str(c)).strip())
         every.setdefault(key, c)
     spread2 = sorted(cb.spread_l3(sorted(every.values()), n))
-    bindings = {"packed": packed, "spread": picked["cpus"], "idlest": idlest, "spread2": spread2}
+    bindings = {"packed": packed, "spread": spread_l3_node, "idlest": idlest, "spread2": spread2}
     if len(sys.argv) > 2:
-        bindings = {k: bindings[k] for k in sys.argv[2].split(",")}
+        want = sys.argv[2].split(",")
+        bindings.update({k: None for k in want if k not in bindings})
+        bindings = {k: bindings[k] for k in want}
+    for name in list(bindings):   # "spread2:15": the first 15 CPUs of a binding, 15 threads
+        if ":" in name:
+            base, k = name.split(":")
+            full = bindings[base] if base != "spread2" else sorted(cb.spread_l3(sorted(every.values()), int(k)))
+            bindings[name] = full[:int(k)]
     for name, cpus in bindings.items():
-        env = cb.child_env(n, cpus=cpus)
+        env = cb.child_env(len(cpus), cpus=cpus)
         r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"),
                             json.dumps(GEOM), str(secs), "20181105", "only"], env=env,
                            capture_output=True, text=True, timeout=max(120, secs * 20))
@@ -66,7 +76,7 @@ def main():
         print(json.dumps({"binding": name, "cpus": cpus, "node": nd,
                           "nodes": sorted({k for k, cs in nodes.items() for c in cpus if c in cs}),
                           "l3_domains": len({cb.l3_domain(c) for c in cpus}),
-                          "l3_domains_on_node": len(doms), "threads": n,
+                          "l3_domains_on_node": len(doms), "threads": len(cpus),
                           "value": res.get("value"), "iqr": res.get("iqr"), "passes": res.get("passes"),
                           "cgroup_cpu_stat_delta": res.get("cgroup_cpu_stat_delta"),
                           "error": res.get("error")}), flush=True)

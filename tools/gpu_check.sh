@@ -6,7 +6,7 @@
 #   steps: smoke tests contract bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread
+#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -37,8 +37,11 @@ for s in $STEPS; do
                 --timeout 800 --timeout-method thread ;;
     bench) run bench 600 python3 bench.py --steps 50 --warmup 5 ;;
     cpuspread) run cpu_spread 300 python3 tools/cpu_spread_probe.py 4 ;;
+    cputhreads) run cpu_threads_a 300 python3 tools/cpu_spread_probe.py 4 spread2,spread2:14,spread2:15,spread2:12 &&
+                run cpu_threads_b 300 python3 tools/cpu_spread_probe.py 4 spread2:15,spread2:14,spread2:12,spread2 ;;
     cpuspread2) run cpu_spread_a 300 python3 tools/cpu_spread_probe.py 4 spread,spread2,packed &&
                 run cpu_spread_b 300 python3 tools/cpu_spread_probe.py 4 spread2,spread,packed ;;
+    sustained) run bench_sustained 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 --min-seconds 30 --cpu-seconds 0 ;;
     syncprobe) run sync_probe 300 python3 tools/sync_probe.py --regions 400 ;;
     benchdrv) run bench_drv 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchnf) run bench_nofuse 600 python3 bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-fuse ;;
