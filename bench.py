@@ -776,7 +776,9 @@ def main(argv=None) -> int:
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "b2p_integrate_kernel",
+                # the instantiation rocprofv3 lists for these launches: MULTI
+                # (last template argument) true when queued blocks share one
+                "kernel": "b2p_integrate_kernel<..., MULTI=%s>" % ("true" if bpl > 1 else "false"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -142,7 +142,11 @@ __device__ __forceinline__ float to_output(unsigned long long tot, uint32_t mean
 // rows; 1 = group g owns rows g, g+G, g+2G, ... so that the whole grid
 // sweeps the span front to back together (the probe in tools/hbm_probe.hip
 // reads faster that way).  Either way a lane's channels never change.
-template <int MODE, int NPO, int UNROLL, bool NT>
+//
+// MULTI: the launch carries several queued blocks (b2p_integrate_n, a.nblk >
+// 1) rather than one.  The two shapes are separate instantiations so that a
+// rocprofv3 summary lists them as separate kernels (bench.py times both).
+template <int MODE, int NPO, int UNROLL, bool NT, bool MULTI>
 __global__ void __launch_bounds__(1024)
 b2p_integrate_kernel(IntegrateArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds[];
@@ -210,8 +214,9 @@ b2p_integrate_kernel(IntegrateArgs a) {
   }
   // one integration per block: the rows of block b stream through the same
   // lanes (same channels), then the workgroup's sums go to block b's set
-  for (uint32_t b = 0; b < a.nblk; ++b) {
-  const u32x4 *data = reinterpret_cast<const u32x4 *>(a.nblk > 1 ? a.blk[b] : a.data);
+  const uint32_t nblk = MULTI ? a.nblk : 1u;
+  for (uint32_t b = 0; b < nblk; ++b) {
+  const u32x4 *data = reinterpret_cast<const u32x4 *>(MULTI ? a.blk[b] : a.data);
   A acc;
   acc.zero_all();
   if (b) {  // LDS of the previous block was drained into its set
@@ -461,33 +466,39 @@ hipError_t launch_assemble(const AssembleArgs &a, uint32_t grid_cap, hipStream_t
 // ---- launchers --------------------------------------------------------------
 typedef void (*IntegrateFn)(IntegrateArgs);
 
-template <int MODE, int NPO>
+template <int MODE, int NPO, bool MULTI>
 static IntegrateFn pick_t(int unroll, bool nt) {
   switch (unroll * 2 + (nt ? 1 : 0)) {
-    case 4 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 4, false>;
-    case 4 * 2 + 1: return b2p_integrate_kernel<MODE, NPO, 4, true>;
-    case 16 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 16, false>;
-    case 16 * 2 + 1: return b2p_integrate_kernel<MODE, NPO, 16, true>;
-    case 8 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 8, false>;
-    default: return b2p_integrate_kernel<MODE, NPO, 8, true>;
+    case 4 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 4, false, MULTI>;
+    case 4 * 2 + 1: return b2p_integrate_kernel<MODE, NPO, 4, true, MULTI>;
+    case 16 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 16, false, MULTI>;
+    case 16 * 2 + 1: return b2p_integrate_kernel<MODE, NPO, 16, true, MULTI>;
+    case 8 * 2 + 0: return b2p_integrate_kernel<MODE, NPO, 8, false, MULTI>;
+    default: return b2p_integrate_kernel<MODE, NPO, 8, true, MULTI>;
   }
 }
 
-static IntegrateFn pick(int mode, int npol_out, int unroll, bool nt) {
+template <bool MULTI>
+static IntegrateFn pick_m(int mode, int npol_out, int unroll, bool nt) {
   switch (mode * 2 + (npol_out - 1)) {
-    case kI8 * 2 + 0: return pick_t<kI8, 1>(unroll, nt);
-    case kI8 * 2 + 1: return pick_t<kI8, 2>(unroll, nt);
-    case kI16LE * 2 + 0: return pick_t<kI16LE, 1>(unroll, nt);
-    case kI16LE * 2 + 1: return pick_t<kI16LE, 2>(unroll, nt);
-    case kI16BE * 2 + 0: return pick_t<kI16BE, 1>(unroll, nt);
-    case kI16BE * 2 + 1: return pick_t<kI16BE, 2>(unroll, nt);
+    case kI8 * 2 + 0: return pick_t<kI8, 1, MULTI>(unroll, nt);
+    case kI8 * 2 + 1: return pick_t<kI8, 2, MULTI>(unroll, nt);
+    case kI16LE * 2 + 0: return pick_t<kI16LE, 1, MULTI>(unroll, nt);
+    case kI16LE * 2 + 1: return pick_t<kI16LE, 2, MULTI>(unroll, nt);
+    case kI16BE * 2 + 0: return pick_t<kI16BE, 1, MULTI>(unroll, nt);
+    case kI16BE * 2 + 1: return pick_t<kI16BE, 2, MULTI>(unroll, nt);
   }
   return nullptr;
 }
 
+static IntegrateFn pick(int mode, int npol_out, int unroll, bool nt, bool multi) {
+  return multi ? pick_m<true>(mode, npol_out, unroll, nt) : pick_m<false>(mode, npol_out, unroll, nt);
+}
+
 hipError_t launch_integrate(const IntegrateArgs &a, const KernelChoice &k, uint32_t threads,
                             uint32_t grid, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-  IntegrateFn f = pick(k.mode, k.npol_out, k.unroll, k.nt);
+  // a.blk is read only by the MULTI instantiation, a.data only by the other
+  IntegrateFn f = pick(k.mode, k.npol_out, k.unroll, k.nt, a.nblk > 1);
   if (!f) return hipErrorInvalidValue;
   const size_t lds = (size_t)a.nout * sizeof(unsigned long long);
   IntegrateArgs arg = a;
@@ -499,7 +510,7 @@ hipError_t launch_integrate(const IntegrateArgs &a, const KernelChoice &k, uint3
 }
 
 hipError_t occupancy_integrate(const KernelChoice &k, uint32_t threads, size_t lds, int *blocks) {
-  IntegrateFn f = pick(k.mode, k.npol_out, k.unroll, k.nt);
+  IntegrateFn f = pick(k.mode, k.npol_out, k.unroll, k.nt, false);  // both shapes: the same resources
   if (!f) return hipErrorInvalidValue;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void *>(f),
                                                       (int)threads, lds);

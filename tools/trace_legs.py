@@ -27,6 +27,7 @@ def legs(trace_path: str, line: dict) -> dict:
     rows = [r for r in csv.DictReader(open(trace_path)) if KERNEL in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]  # us
+    names = [r["Kernel_Name"] for r in rows]
     rf = line["roofline"]
     phases = rf.get("launch_phases") or []
     want = sum(c for _, c in phases)
@@ -35,10 +36,11 @@ def legs(trace_path: str, line: dict) -> dict:
     i = 0
     for name, c in phases:
         d = dur[i:i + c]
+        kn = sorted(set(names[i:i + c]))
         i += c
         if not d:
             continue
-        out["legs"][name] = {"launches": len(d), "avg_us": round(statistics.fmean(d), 2),
+        out["legs"][name] = {"launches": len(d), "kernels": kn, "avg_us": round(statistics.fmean(d), 2),
                              "median_us": round(statistics.median(d), 2),
                              "min_us": round(min(d), 2), "max_us": round(max(d), 2)}
     h = out["legs"].get("headline")
