@@ -84,3 +84,43 @@ def test_port_rejects_ragged():
     g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=16)
     with pytest.raises(ValueError):
         co.port_integrate(g, np.zeros(g.frame_bytes + 4, np.uint8))
+
+
+def test_cpu_leg_deals_threads_over_every_l3(monkeypatch):
+    """bench.py's CPU leg (oracle/cpu_baseline.pick_cpus): one core per L3
+    domain before any domain gets a second, idlest core of each first, CPUs
+    listed in order so the first threads sit on node 0 (a host of 2 nodes x
+    4 CCDs x 4 cores, SMT siblings at +32, stands in for the 9575F)"""
+    import cpu_baseline as cb
+    l3 = {c: str((c % 32) // 4) for c in range(64)}          # CCD of each logical CPU
+    node = {0: set(range(0, 16)) | set(range(32, 48)), 1: set(range(16, 32)) | set(range(48, 64))}
+    busy = {c: (0.9 if c in (0, 4) else 0.0) for c in range(64)}  # the first core of CCDs 0, 1 busy
+    monkeypatch.setattr(cb, "allowed_cpus", lambda: list(range(64)))
+    monkeypatch.setattr(cb, "busy_fraction", lambda cpus, s=0.25: {c: busy[c] for c in cpus})
+    monkeypatch.setattr(cb, "l3_domain", lambda c: l3[c])
+    monkeypatch.setattr(cb, "numa_nodes", lambda: node)
+    topo = {}
+    for c in range(64):
+        topo[f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"] = "0" if c % 32 < 16 else "1"
+        topo[f"/sys/devices/system/cpu/cpu{c}/topology/core_id"] = str(c % 32)
+    monkeypatch.setattr(cb, "_read", lambda p: topo.get(p))
+    p = cb.pick_cpus(8, 0.0)
+    assert p["cpus"] == [1, 5, 8, 12, 16, 20, 24, 28]        # one per CCD, busy cores skipped
+    assert p["l3_domains"] == 8 and p["l3_domains_allowed"] == 8 and p["nodes"] == [0, 1]
+    p = cb.pick_cpus(12, 0.0)
+    assert len(p["cpus"]) == 12 and len(set(p["cpus"])) == 12 and all(c < 32 for c in p["cpus"])
+    per = {}
+    for c in p["cpus"]:
+        per[l3[c]] = per.get(l3[c], 0) + 1
+    assert sorted(per.values()) == [1, 1, 1, 1, 2, 2, 2, 2]   # dealt: no CCD gets a third first
+    p = cb.pick_cpus(40, 0.0)                                 # more threads than cores: SMT siblings
+    assert len(set(p["cpus"])) == 40
+
+
+def test_cpu_leg_reports_other_tenants_load():
+    """others_busy: the mean load of the CPUs a leg did not run on"""
+    import cpu_baseline as cb
+    a = {0: (0, 0), 1: (0, 0), 2: (0, 0)}
+    b = {0: (0, 100), 1: (50, 100), 2: (100, 100)}            # (idle ticks, total ticks)
+    assert cb.others_busy(a, b, {0}) == 0.25                  # cpu 1 half busy, cpu 2 idle
+    assert cb.others_busy(a, b, {0, 1, 2}) is None
