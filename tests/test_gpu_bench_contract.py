@@ -153,3 +153,42 @@ def test_configs4_eight_subbands_full_size(gpu):
     assert d["verification"]["gather"] == "rank 0 holds every rank's K spectra"
     assert "2 distinct block" in d["verification"]["what"]
     assert len(d["per_rank_ms_per_step"]) == 8
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("split", ["subband", "time"])
+def test_bench_rccl_world1_under_torchrun(gpu, split):
+    """The driver's multi-GPU launch shape, torch.distributed.run + bench.py,
+    with the RCCL ("nccl") group forced at world size 1 (--force-dist): the
+    communicator set-up, the gather of the spectra to rank 0 (or, time split,
+    the exact uint64 reduce of the partial sums), the identity all_gather,
+    the max-over-ranks all_reduce and the barriers all run over RCCL, and the
+    spectra are verified against the oracle.  RCCL refuses two ranks on one
+    GPU, so world 1 is as far as a one-GPU box takes this path."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--steps", "8", "--warmup", "2", "--cpu-seconds", "0",
+           "--min-seconds", "0.2", "--bpl1-seconds", "0.1", "--force-dist", "--dist-timeout", "180"]
+    if split == "time":
+        cmd += ["--split", "time"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=500, cwd=REPO, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["dist_backend"] == "nccl" and d["rccl_ranks"] == 1 and d["ranks"] == 1
+    assert d["config"]["launcher"] == "torch.distributed.run"
+    assert d["verified"] is True and d["distinct_gpus"] == 1
+    assert [x["rank"] for x in d["rank_devices"]] == [0]
+    if split == "time":
+        assert d["scaling"] == "strong" and d["config"]["blocks_per_launch"] == 1
+    else:
+        assert d["verification"]["gather"] == "rank 0 holds every rank's K spectra"
+        assert d["config"]["blocks_per_launch"] == 4 and d["one_per_launch"]["verified"] is True
