@@ -6,7 +6,7 @@
 #   steps: smoke tests contract bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained
+#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -118,6 +118,7 @@ for s in $STEPS; do
          run pmc_write_asm 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_asm" -o run \
             -- python3 tools/bench_assemble.py --steps 4 --warmup 1 --order tm ;;
     matrix) run perf_matrix 600 python3 tools/perf_matrix.py --steps 20 ;;
+    matrix4) run perf_matrix_m4 600 python3 tools/perf_matrix.py --steps 40 --multi 4 ;;
     multi) run multi_1 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "int8 64ch" &&
            run multi_8 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "int8 64ch" --multi 8 &&
            run multi_tf1 300 python3 tools/perf_matrix.py --steps 40 --npol-out 1 --only "TFTFP 8x8" &&
