@@ -307,7 +307,8 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
     ln = leg(r_n, el_n, thr_n)
     return {
         "value": ln["value"], "unit": "Msamples/s", "cores": threads,
-        "kind": "port-tuned",
+        "kind": "port",          # the contract's two kinds: "reference" | "port"
+        "port": "tuned (oracle/b2p_cpu_port.c), not the scalar checker",
         "isa": used,
         "sample": (f"tuned port ({used}, OpenMP time tiles): {len(r_n)} passes ({el_n:.1f} s) at "
                    f"{threads} threads and {len(r_1)} passes ({el_1:.1f} s) at 1 thread over one "

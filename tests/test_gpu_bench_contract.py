@@ -49,7 +49,7 @@ def test_bench_prints_one_contract_line(gpu):
     assert one["blocks_per_launch"] == 1 and one["verified"] is True and one["value"] > 0
     assert one["timed_regions"] >= 1 and 0.3 < one["frac_of_value"] < 1.0
     cb = d["cpu_baseline"]
-    assert cb["unit"] == d["unit"] and cb["kind"] == "port-tuned" and cb["cores"] >= 1
+    assert cb["unit"] == d["unit"] and cb["kind"] == "port" and cb["port"].startswith("tuned") and cb["cores"] >= 1
     assert d["value"] > 0 and cb["value"] > 0 and cb["value_1thread"] > 0
     assert cb["equals_oracle"] is True and cb["oracle_value"] > 0
     lo, hi = cb["iqr"]
