@@ -8,7 +8,7 @@ so that a rare ordering fault would show as a wrong spectrum:
 * the replica banks that alternate between batched launches;
 * the finalize that one launch carries for the previous one;
 * the fences that release ring blocks;
-* the gathered rounds of `-n 2`.
+* the gathered rounds of `-n 2`, and the time-split reduce of `-t 2`.
 
 Small blocks (16 KiB, a 5 us kernel) put the semaphore / fence / launch
 machinery at its highest rate, on device rings and on a host ring.
@@ -31,7 +31,7 @@ from test_gpu_device_ring import BIN, HDR, SEED, _wait, fresh_key
 pytestmark = pytest.mark.gpu
 
 
-def _soak(tmp_path, g, nbufs, nrep, nsub=1, timeout=300, device=0):
+def _soak(tmp_path, g, nbufs, nrep, nsub=1, timeout=300, device=0, stage_args=()):
     base, kout = fresh_key(), fresh_key()
     kins = [base + 0x10 * q for q in range(nsub)]
     for k in kins:
@@ -44,7 +44,8 @@ def _soak(tmp_path, g, nbufs, nrep, nsub=1, timeout=300, device=0):
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{base:x}", "-b", f"{kout:x}",
                                    "-c", str(tmp_path), "-d", "0", "-f", f"int8:{g.nchan_chunk}"]
-                                  + (["-n", str(nsub)] if nsub > 1 else []), stderr=subprocess.PIPE)]
+                                  + (["-n", str(nsub)] if nsub > 1 else []) + list(stage_args),
+                                  stderr=subprocess.PIPE)]
         procs += [subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{k:x}", "-b", HDR, "-R", str(nrep),
                                     "-f", f"int8:{g.nchan_chunk}", "-r", str(SEED + q)], stderr=subprocess.PIPE)
                   for q, k in enumerate(kins)]
@@ -83,6 +84,14 @@ def test_soak_small_blocks_host_ring(gpu, tmp_path):
     buffered staging, each one released only after its copy"""
     g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
     _soak(tmp_path, g, nbufs=4, nrep=50000, device=-1)
+
+
+def test_soak_time_split_host_ring(gpu, tmp_path):
+    """-t 2: 20 000 host-ring blocks, each cut by time over two contexts
+    (both on the one test GPU) whose exact partial sums are reduced"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
+    log = _soak(tmp_path, g, nbufs=4, nrep=20000, device=-1, stage_args=["-t", "2"])
+    assert "reduce of 2 time shares" in log
 
 
 def test_soak_full_size_configs1_blocks(gpu, tmp_path):
