@@ -101,3 +101,66 @@ def test_soak_full_size_configs1_blocks(gpu, tmp_path):
     log = _soak(tmp_path, g, nbufs=8, nrep=10000)
     m = re.search(r"(\d+) integrate launches for (\d+) integrations", log)
     assert m and int(m.group(2)) == 10000 and int(m.group(1)) <= 10000
+
+
+def test_soak_udp_capture_many_blocks(gpu, tmp_path):
+    """paf_dfsend -> loopback UDP on 3 ports -> paf_capture (GPU assembly into
+    a device ring) -> paf_baseband2power, 120 blocks of 64 frames x 8 chunks
+    with arrival shuffled within 1.5 blocks and the 27-s frame-counter wrap
+    crossed: every spectrum equals the oracle of the block assembled from the
+    same stream, and no frame is lost"""
+    import time
+    from test_capture import make_stream
+    nchunk, block_ndf, nblk = 8, 64, 120
+    g, payload, df, ck = make_stream(tmp_path, nchunk=nchunk, nblk=nblk, block_ndf=block_ndf,
+                                     window=block_ndf * nchunk * 3 // 2, seed=29)
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text(f"HDR_SIZE 4096\nNBIT 16\nNDIM 2\nNPOL 2\nNCHAN {nchunk * 7}\nNCHUNK {nchunk}\n"
+                   "NCHAN_CHUNK 7\nNSAMP_DF 128\nBYTE_ORDER BE\nTSAMP 0.84375\n")
+    kin, kout = fresh_key(), fresh_key()
+    dada.create_ring(kin, 4, g.block_bytes, device=0)
+    dada.create_ring(kout, 8, g.nout * 4)
+    port = 26000 + (os.getpid() % 500) * 8
+    out = tmp_path / "power.dada"
+    procs = []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
+                                   f"{kout:x}", "-c", str(tmp_path), "-d", "0"], stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([os.path.join(BIN, "paf_capture"), "-a", f"{kin:x}", "-f", str(hdr),
+                                   "-c", str(block_ndf), "-n", str(nblk), "-P", str(port), "-N", "3",
+                                   "-m", "freq:1300", "-x", "249990", "-s", "54", "-t", "1", "-d", "0"],
+                                  stderr=subprocess.PIPE, text=True)]
+        time.sleep(3)  # capture opens its context and binds before the sender starts
+        snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-P",
+                              str(port), "-N", "3", "-r", "200"], capture_output=True, text=True)
+        assert snd.returncode == 0, snd.stderr
+        errs = []
+        for p in procs[::-1]:
+            _, e = p.communicate(timeout=180)
+            errs.append(e)
+            assert p.returncode == 0, e[-800:]
+        cap_log = errs[0]
+        _, data = dada.read_dada_file(str(out))
+        sp = data.view(np.float32).reshape(-1, g.nout)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+    assert "0.000% lost" in cap_log, cap_log[-600:]
+    assert sp.shape[0] == nblk, cap_log[-600:]
+    dfs = np.fromfile(df, np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, np.uint8)
+    idf, sec = 249990, 54
+    want = np.zeros(g.block_bytes, np.uint8)
+    for b in range(nblk):
+        want[:] = 0
+        co.assemble(dfs, chunk, idf, sec, want, block_ndf, nchunk)
+        assert np.array_equal(want, payload[b * g.block_bytes:(b + 1) * g.block_bytes]), b
+        assert np.array_equal(sp[b].view(np.uint32), co.power(g, want).view(np.uint32)), b
+        gi = idf + block_ndf
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27
