@@ -272,8 +272,8 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
 
     def timed(fn, nt: int, budget: float, min_passes: int = 3):
         warm = buf[: g.frame_bytes * max(1, (64 << 20) // g.frame_bytes)]
-        (co.port_integrate(g, warm, nthreads=nt, isa=isa) if fn is port
-         else co.integrate(g, warm, nthreads=nt))
+        (co.integrate(g, warm, nthreads=nt) if fn is oracle
+         else co.port_integrate(g, warm, nthreads=nt, isa=isa))
         st0, tk0 = cpu_stat(), _idle_ticks()
         rates, t_all = [], time.perf_counter()
         while len(rates) < min_passes or time.perf_counter() - t_all < budget:
@@ -298,7 +298,17 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
         r_n, el_n, thr_n = timed(port, threads, seconds)
         return {"threads": threads, **leg(r_n, el_n, thr_n), "isa": used, "binding": binding}
     r_n, el_n, thr_n = timed(port, threads, seconds * 0.6)
-    r_1, el_1, thr_1 = timed(port, 1, seconds * 0.25)
+    # the 1-thread leg streams a copy first-touched by that thread (the main
+    # thread, bound to the first place): the block's own pages are spread
+    # over both nodes by the threads that filled it, and half of them would
+    # be remote to one thread
+    buf1 = np.empty_like(buf)
+    np.copyto(buf1, buf)
+
+    def port1(nt):
+        return co.port_integrate(g, buf1, nthreads=nt, isa=isa)
+    r_1, el_1, thr_1 = timed(port1, 1, seconds * 0.25)
+    del buf1
     r_o, el_o, _ = timed(oracle, threads, seconds * 0.15)
     # the port is a baseline, not the checker: its sums must equal the oracle's
     equal = bool(np.array_equal(port(threads), oracle(threads)))
