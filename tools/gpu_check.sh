@@ -6,7 +6,7 @@
 #   steps: smoke tests contract bench benchdrv benchnf bench5 benchbmf bench3 bench2gloo bench4gloo benchdist1 distcost benchsplit cpunproc
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
-#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4
+#          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4 pmc1
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -163,6 +163,11 @@ for s in $STEPS; do
             -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
             -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 ;;
+    pmc1) # the one-block launch shape (MULTI=false) of configs[1]
+         run pmc_fetch_bpl1 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_bpl1" -o run \
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --blocks-per-launch 1 &&
+         run pmc_write_bpl1 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_bpl1" -o run \
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --blocks-per-launch 1 ;;
     pmc5) run pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run \
             -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run \

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--blocks-per-launch", type=int, default=1,
                     help="integrations per integrate launch in the profiled run (bench.py's)")
     ap.add_argument("--kernel", default=KERNEL)
+    ap.add_argument("--name", help="file stem instead of the config (e.g. c2_bpl1 for the one-block "
+                                    "launch shape; bench.py reads pmc_<config>.json only)")
     ap.add_argument("--bench-log", help="stdout of a profiled bench.py run (its JSON line names the "
                                         "kernel sources' sha256 it ran)")
     a = ap.parse_args()
@@ -75,8 +77,9 @@ def main():
     fetch_kib, write_kib = statistics.median(f), statistics.median(w)
     hbm = int(fetch_kib * 1024 * 2 + write_kib * 1024)
     alg = a.algorithmic_bytes or ALGORITHMIC.get(a.config, 0) * a.blocks_per_launch
-    fetch_dst = f"profiles/{a.round}_{a.config}_pmc_fetch.csv"
-    write_dst = f"profiles/{a.round}_{a.config}_pmc_write.csv"
+    name = a.name or a.config
+    fetch_dst = f"profiles/{a.round}_{name}_pmc_fetch.csv"
+    write_dst = f"profiles/{a.round}_{name}_pmc_write.csv"
     out = {
         "kernel": a.kernel,
         "config": a.config,
@@ -96,11 +99,11 @@ def main():
         "kernel_sources_commit": git("log", "-1", "--format=%H", "--", *bench.KERNEL_SOURCES),
     }
     os.makedirs(os.path.join(REPO, "profiles"), exist_ok=True)
-    json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{a.config}.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(REPO, "profiles", f"pmc_{name}.json"), "w"), indent=1)
     shutil.copy(a.fetch, os.path.join(REPO, fetch_dst))
     shutil.copy(a.write, os.path.join(REPO, write_dst))
     if a.stats:
-        shutil.copy(a.stats, os.path.join(REPO, "profiles", f"{a.round}_{a.config}_kernel_stats.csv"))
+        shutil.copy(a.stats, os.path.join(REPO, "profiles", f"{a.round}_{name}_kernel_stats.csv"))
     print(json.dumps(out, indent=1))
 
 
