@@ -134,7 +134,7 @@ def test_soak_udp_capture_many_blocks(gpu, tmp_path):
                                   stderr=subprocess.PIPE, text=True)]
         time.sleep(3)  # capture opens its context and binds before the sender starts
         snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-P",
-                              str(port), "-N", "3", "-r", "200"], capture_output=True, text=True)
+                              str(port), "-N", "3", "-r", "100"], capture_output=True, text=True)
         assert snd.returncode == 0, snd.stderr
         errs = []
         for p in procs[::-1]:
