@@ -4,9 +4,11 @@ counts, 1..N samples per frame, 1 or 2 output pols, sum or mean -- plus a
 random split of the integration into pushes, and checks the HIP result
 against the oracle bit for bit.  One Integrator per example, all in this
 one process (the GPU box allows few processes)."""
+import os
+
 import numpy as np
 import pytest
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, given, seed, settings
 from hypothesis import strategies as st
 
 import b2p_oracle as npo
@@ -14,6 +16,16 @@ import oracle_c as co
 import paf_b2p
 
 pytestmark = pytest.mark.gpu
+
+# a longer bug hunt on request: B2P_HYPOTHESIS_SCALE=k runs k times the
+# examples, B2P_HYPOTHESIS_SEED=n draws a different (seeded) set of them;
+# by default the same derandomized set runs every time
+_SCALE = int(os.environ.get("B2P_HYPOTHESIS_SCALE", "1"))
+_SEED = os.environ.get("B2P_HYPOTHESIS_SEED")
+
+
+def _hunt(f):
+    return seed(int(_SEED))(f) if _SEED else f
 
 
 @st.composite
@@ -41,7 +53,8 @@ def layouts(draw):
     return g, cuts, seed
 
 
-@settings(max_examples=120, deadline=None, derandomize=True,
+@_hunt
+@settings(max_examples=120 * _SCALE, deadline=None, derandomize=_SEED is None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
                                  HealthCheck.function_scoped_fixture])
 @given(layouts())
@@ -59,7 +72,8 @@ def test_random_layouts_match_oracle(gpu, case):
     assert np.array_equal(out.view(np.uint32), want.view(np.uint32)), (g, cuts, seed)
 
 
-@settings(max_examples=40, deadline=None, derandomize=True,
+@_hunt
+@settings(max_examples=40 * _SCALE, deadline=None, derandomize=_SEED is None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
                                  HealthCheck.function_scoped_fixture])
 @given(layouts(), st.integers(1, 8))
