@@ -103,3 +103,78 @@ def test_assembly_opens_a_timing_region(gpu):
     moved = block_ndf * nchunk * (7232 + 7168)
     assert moved / (us * 1e-6) / 1e9 < 8000.0, us
     assert us > 50, us
+
+
+# ---- property: random streams ---------------------------------------------------
+import os  # noqa: E402
+
+from hypothesis import HealthCheck, given, seed, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_SCALE = int(os.environ.get("B2P_HYPOTHESIS_SCALE", "1"))
+_SEED = os.environ.get("B2P_HYPOTHESIS_SEED")
+
+
+@st.composite
+def streams(draw):
+    """a shuffled, lossy frame stream around one block: frames of the block
+    (some lost, some sent twice with the same payload), frames of the blocks
+    before and after it, bad chunk ids, and references that put the block
+    across the 27-s frame-counter wrap"""
+    nchunk = draw(st.integers(1, 48))
+    block_ndf = draw(st.integers(1, 48))
+    ref_idf = draw(st.sampled_from([0, 1000, 249_999 - block_ndf // 2, 249_990]))
+    ref_sec = 27 * draw(st.integers(0, 3000))
+    keep = draw(st.floats(0.5, 1.0))
+    n_early = draw(st.integers(0, 2 * nchunk))
+    n_late = draw(st.integers(0, 2 * nchunk))
+    n_dup = draw(st.integers(0, 8))
+    n_bad = draw(st.integers(0, 3))
+    s = draw(st.integers(0, 2 ** 32 - 1))
+    return nchunk, block_ndf, ref_idf, ref_sec, keep, n_early, n_late, n_dup, n_bad, s
+
+
+@(seed(int(_SEED)) if _SEED else (lambda f: f))
+@settings(max_examples=60 * _SCALE, deadline=None, derandomize=_SEED is None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(streams())
+def test_assemble_random_streams_match_oracle(gpu, case):
+    """GPU placement and per-chunk counts equal the oracle's sequential
+    placement (capture.c:527-547) for random streams; duplicates carry the
+    same payload, so their (unordered) GPU writes are indistinguishable"""
+    nchunk, block_ndf, ref_idf, ref_sec, keep, n_early, n_late, n_dup, n_bad, s = case
+    rng = np.random.default_rng(s)
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=128 * block_ndf)
+    block = npo.fill_synthetic(g, g.block_bytes, s, 0, 1)
+    n = block_ndf * nchunk
+    order = rng.permutation(n)[: max(1, int(round(n * keep)))]
+    if n_dup:
+        order = np.concatenate([order, rng.choice(order, n_dup)])
+    dfs, chunk = npo.df_stream(block, nchunk, ref_idf, ref_sec, order)
+    parts, chunks = [dfs], [chunk]
+    if n_early and (ref_idf >= 2 or ref_sec >= 27):  # the 2 frame times before the block
+        e, ec = npo.df_stream(block[: nchunk * 7168 * 2], nchunk, ref_idf - 2 + 250_000 * (ref_idf < 2),
+                              ref_sec - 27 * (ref_idf < 2))
+        parts.append(e[: n_early])
+        chunks.append(ec[: n_early])
+    if n_late:
+        l_, lc = npo.df_stream(block[: nchunk * 7168 * 2], nchunk, (ref_idf + block_ndf) % 250_000,
+                               ref_sec + 27 * ((ref_idf + block_ndf) // 250_000))
+        parts.append(l_[: n_late])
+        chunks.append(lc[: n_late])
+    dfs, chunk = np.concatenate(parts), np.concatenate(chunks)
+    perm = rng.permutation(len(dfs))
+    dfs, chunk = np.ascontiguousarray(dfs[perm]), np.ascontiguousarray(chunk[perm])
+    if n_bad:
+        chunk[rng.choice(len(chunk), min(n_bad, len(chunk)), replace=False)] = 200 + nchunk % 50
+    init = np.full(block.size, 0x5A, np.uint8)
+    want = init.copy()
+    want_cnt = co.assemble(dfs, chunk, ref_idf, ref_sec, want, block_ndf, nchunk)
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict())) as it:
+        got, cnt, bufs = _run_gpu(it, dfs, chunk, ref_idf, ref_sec, init, block_ndf, nchunk)
+        for b in bufs:
+            b.free()
+    assert np.array_equal(got, want), case
+    assert cnt.tolist() == want_cnt.tolist(), case
