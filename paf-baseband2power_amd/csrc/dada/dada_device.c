@@ -97,6 +97,8 @@ static void report(int fd, const char *what, int code) {
   if (n > 0) (void)!write(fd, msg, (size_t)n < sizeof msg ? (size_t)n : sizeof msg - 1);
 }
 
+#define DEV_ALLOC_ALIGN (2ull << 20)
+
 /* the holder: owns the blocks until SIGTERM/SIGINT or the ring is removed */
 static void holder(ipcbuf_t *id, int device, int wfd) {
   int rc;
@@ -115,9 +117,13 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
     report(wfd, "hipSetDevice", rc);
     _exit(1);
   }
+  /* each block its own allocation of whole 2 MiB pages: HIP serves small
+   * requests (a 29 952-B block did) from a shared sub-allocated chunk, and
+   * hipIpcGetMemHandle refuses a pointer inside one ("invalid argument") */
+  const uint64_t alloc = (bufsz + DEV_ALLOC_ALIGN - 1) / DEV_ALLOC_ALIGN * DEV_ALLOC_ALIGN;
   for (uint64_t i = 0; i < n; i++) {
     ipc_handle_t h;
-    if ((rc = hip.malloc_(&blk[i], bufsz)) != 0 || (rc = hip.memset_(blk[i], 0, bufsz)) != 0 ||
+    if ((rc = hip.malloc_(&blk[i], alloc)) != 0 || (rc = hip.memset_(blk[i], 0, alloc)) != 0 ||
         (rc = hip.get_handle(&h, blk[i])) != 0) {
       report(wfd, "hipMalloc/hipIpcGetMemHandle", rc);
       for (uint64_t j = 0; j <= i; j++)

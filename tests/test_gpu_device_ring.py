@@ -54,16 +54,19 @@ def _wait(procs, timeout=300):
     return errs
 
 
-def test_device_ring_bytes_cross_processes(gpu, tmp_path):
+# 29 952 B (12 frames of 2496 B) once failed in the holder: HIP served the
+# block from a sub-allocated chunk and hipIpcGetMemHandle refused it
+@pytest.mark.parametrize("bufsz", [1 << 16, 29952, 1040, (3 << 20) + 48])
+def test_device_ring_bytes_cross_processes(gpu, tmp_path, bufsz):
     key = fresh_key()
-    dada.create_ring(key, 3, 1 << 16, device=0)
+    dada.create_ring(key, 3, bufsz, device=0)
     try:
         out = tmp_path / "o.dada"
         rd = subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{key:x}", "-o", str(out)],
                               stderr=subprocess.PIPE)
         rng = np.random.default_rng(1)
-        blocks = [rng.integers(0, 256, 1 << 16, dtype=np.uint8).tobytes() for _ in range(5)]
-        blocks.append(rng.integers(0, 256, 1000, dtype=np.uint8).tobytes())  # short = EOD
+        blocks = [rng.integers(0, 256, bufsz, dtype=np.uint8).tobytes() for _ in range(5)]
+        blocks.append(rng.integers(0, 256, bufsz // 3, dtype=np.uint8).tobytes())  # short = EOD
         with dada.Hdu(key, "W") as w:
             assert w.device == 0
             w.write_header("HDR_SIZE 4096\nNBIT 8\n")

@@ -10,7 +10,7 @@ so that a rare ordering fault would show as a wrong spectrum:
 * the fences that release ring blocks;
 * the gathered rounds of `-n 2`, and the time-split reduce of `-t 2`.
 
-Small blocks (16 KiB, a 5 us kernel) put the semaphore / fence / launch
+Small blocks (16 MiB, a 2-3 us kernel) put the semaphore / fence / launch
 machinery at its highest rate, on device rings and on a host ring.
 Full-size configs[1] blocks (1 GiB) run the production launch shape. `paf_dfdb -R` fills ring buffer i with synthetic
 block i once and re-hands it, so output k must equal the oracle of block
@@ -66,7 +66,7 @@ def _soak(tmp_path, g, nbufs, nrep, nsub=1, timeout=300, device=0, stage_args=()
 
 
 def test_soak_small_blocks_one_subband(gpu, tmp_path):
-    """300 000 blocks of 16 KiB through an 8-block device ring"""
+    """300 000 blocks of 16 MiB through an 8-block device ring"""
     g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
     log = _soak(tmp_path, g, nbufs=8, nrep=300000)
     m = re.search(r"FINISH PAF_PROCESS: (\d+) integrations", log)
@@ -80,7 +80,7 @@ def test_soak_small_blocks_gathered(gpu, tmp_path):
 
 
 def test_soak_small_blocks_host_ring(gpu, tmp_path):
-    """a host ring: 50 000 blocks copied H2D through the stage's double-
+    """a host ring: 50 000 16-MiB blocks copied H2D through the stage's double-
     buffered staging, each one released only after its copy"""
     g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)
     _soak(tmp_path, g, nbufs=4, nrep=50000, device=-1)
