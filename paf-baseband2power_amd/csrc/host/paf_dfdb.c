@@ -12,11 +12,18 @@
  *
  *   paf_dfdb -a key -b header_file -c df_file -k chunk_file [-n nchunk]
  *            [-x ref_idf] [-s ref_sec] [-d device] [-Z] [-e dir]
- *     Frames arrive in batches of one block's worth; block b is assembled
- *     from batches b-1, b and b+1, so a frame may arrive up to one block
- *     early or late (the reference keeps late frames in its temp buffer,
- *     capture.c:525-531).  The block is zeroed first unless -Z (the
- *     reference leaves lost frames' slots stale).
+ *     Frames are read in batches of one block's worth.  The host decodes
+ *     every frame's header as the batch arrives and records which blocks
+ *     the batch touches; block b is assembled from every batch that holds
+ *     frames of it, once a batch that lies wholly past block b+1 has been
+ *     read (so a frame may arrive up to about one block early or late, as
+ *     the reference's temp buffer allows, capture.c:525-531).  Blocks
+ *     follow the frames' timestamps, not the batch count, so a lossy stream
+ *     (fewer frames than blocks x frames per block) still yields every
+ *     block it has frames for.  A frame more than 2 blocks past the latest
+ *     block seen so far is taken as corrupt and left out (capture.c:491-508
+ *     drops far-future frames likewise).  The block is zeroed first unless
+ *     -Z (the reference leaves lost frames' slots stale).
  *
  *   paf_dfdb -a key -b header_file -R nblocks [-f layout] [-r seed] [-d device]
  *     Replay: fill each ring block once with the synthetic generator, then
@@ -58,21 +65,38 @@ static int parse_layout(const char *lay, b2p_geom_t *g) {
   return g->nchan_chunk ? 0 : -1;
 }
 
+#define NSLOT 6 /* batches held on the GPU at once */
+
 typedef struct batch_t {
   void *frames;  /* device: n x 7232 B */
   void *chunks;  /* device: n chunk indices */
   uint64_t n;
+  int64_t lo, hi; /* blocks (from the first reference) its frames fall in; hi < 0: none */
 } batch_t;
 
-/* next batch of up to cap frames from the stream files, via host staging */
+/* next batch of up to cap frames from the stream files, via host staging;
+ * the headers are decoded on the host for the blocks the batch touches,
+ * leaving out frames before block 0 and past block `limit` (corrupt) */
 static int load_batch(b2p_ctx_t *ctx, FILE *fd, FILE *fc, batch_t *b, uint64_t cap, unsigned char *hf,
-                      unsigned char *hc) {
+                      unsigned char *hc, const b2p_df_hdr_t *ref0, uint64_t block_ndf, int64_t limit) {
   const size_t got = fread(hf, B2P_DF_BYTES, cap, fd);
   b->n = got;
+  b->lo = INT64_MAX;
+  b->hi = -1;
   if (!got) return 0;
   if (fread(hc, 1, got, fc) != got) {
     fprintf(stderr, "paf_dfdb: chunk file shorter than the frame file\n");
     return -1;
+  }
+  for (size_t i = 0; i < got; i++) {
+    b2p_df_hdr_t h;
+    b2p_df_decode(hf + i * B2P_DF_BYTES, &h);
+    const int64_t rel = b2p_df_index(&h, ref0);
+    if (rel < 0) continue;
+    const int64_t k = rel / (int64_t)block_ndf;
+    if (k > limit) continue;
+    if (k < b->lo) b->lo = k;
+    if (k > b->hi) b->hi = k;
   }
   if (b2p_memcpy(ctx, b->frames, hf, got * B2P_DF_BYTES, 1) != B2P_OK ||
       b2p_memcpy(ctx, b->chunks, hc, got, 1) != B2P_OK)
@@ -126,7 +150,7 @@ int main(int argc, char **argv) {
   b2p_ctx_t *ctx = NULL;
   FILE *fd = NULL, *fc = NULL;
   unsigned char *hf = NULL, *hc = NULL;
-  batch_t bt[3] = {{0}};
+  batch_t bt[NSLOT] = {{0}};
   unsigned long long *d_cnt = NULL;
   void *stage = NULL; /* replay into a host ring: blocks generated on the GPU, copied down */
   int locked = 0;
@@ -202,28 +226,52 @@ int main(int argc, char **argv) {
     hc = malloc(cap);
     if (!hf || !hc) goto done;
     b2p_register_host(ctx, hf, cap * B2P_DF_BYTES); /* pinned: full PCIe rate */
-    for (int k = 0; k < 3; k++)
+    for (int k = 0; k < NSLOT; k++)
       if (b2p_dev_alloc(ctx, &bt[k].frames, cap * B2P_DF_BYTES) != B2P_OK ||
           b2p_dev_alloc(ctx, &bt[k].chunks, cap) != B2P_OK)
         goto done;
     if (b2p_dev_alloc(ctx, (void **)&d_cnt, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK)
       goto done;
-    b2p_df_hdr_t ref = {1, ref_idf, ref_sec, 0, 0, 0.0};
-    /* window: slot (b+2)%3 = batch b-1, b%3 = batch b, (b+1)%3 = batch b+1 */
-    if (load_batch(ctx, fd, fc, &bt[0], cap, hf, hc) < 0 ||
-        load_batch(ctx, fd, fc, &bt[1], cap, hf, hc) < 0)
-      goto done;
-    uint64_t placed_all = 0, sent_all = 0;
-    for (uint64_t b = 0; bt[b % 3].n; b++) {
+    const b2p_df_hdr_t ref0 = {1, ref_idf, ref_sec, 0, 0, 0.0};
+    b2p_df_hdr_t ref = ref0;
+    /* live batches: slots head, head+1, ... (mod NSLOT), oldest first */
+    int head = 0, live = 0, eof = 0;
+    int64_t seen_hi = 0; /* latest block any accepted frame fell in */
+    uint64_t placed_all = 0, sent_all = 0, dropped = 0;
+    for (int64_t b = 0;; b++) {
+      /* read on until a batch lies wholly past block b+1: no later frame is
+       * for block b any more */
+      while (!eof) {
+        if (live) {
+          const batch_t *nw = &bt[(head + live - 1) % NSLOT];
+          if (nw->hi >= 0 && nw->lo > b + 1) break;
+        }
+        if (live == NSLOT) { /* out of slots: the oldest batch goes */
+          if (bt[head].hi >= b) dropped += bt[head].n;
+          head = (head + 1) % NSLOT;
+          live--;
+        }
+        batch_t *x = &bt[(head + live) % NSLOT];
+        if (load_batch(ctx, fd, fc, x, cap, hf, hc, &ref0, block_ndf, seen_hi + 2) < 0) goto done;
+        if (!x->n) {
+          eof = 1;
+          break;
+        }
+        sent_all += x->n;
+        if (x->hi > seen_hi) seen_hi = x->hi;
+        live++;
+      }
+      int any = 0;
+      for (int j = 0; j < live; j++) any |= bt[(head + j) % NSLOT].hi >= b;
+      if (!any) break; /* no frame of block b or later is left */
       uint64_t bid;
       char *blk = ipcio_open_block_write(hdu->data_block, &bid);
       if (!blk) goto done;
       if (!nozero && b2p_memset(ctx, blk, 0, bufsz) != B2P_OK) goto done;
       if (b2p_memset(ctx, d_cnt, 0, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) goto done;
-      const int slots[3] = {(int)((b + 2) % 3), (int)(b % 3), (int)((b + 1) % 3)};
-      for (int j = 0; j < 3; j++) {
-        batch_t *x = &bt[slots[j]];
-        if ((j == 0 && b == 0) || !x->n) continue;
+      for (int j = 0; j < live; j++) {
+        batch_t *x = &bt[(head + j) % NSLOT];
+        if (x->hi < b || x->lo > b) continue;
         if (b2p_assemble(ctx, x->frames, x->n, B2P_DF_BYTES, x->chunks, ref.idf, ref.sec, blk,
                          block_ndf, (uint32_t)nchunk, d_cnt) != B2P_OK) {
           multilog(log, LOG_ERR, "assemble: %s", b2p_last_error(ctx));
@@ -237,16 +285,21 @@ int main(int argc, char **argv) {
       uint64_t placed = 0;
       for (int c = 0; c < nchunk; c++) placed += cnt[c];
       placed_all += placed;
-      sent_all += bt[b % 3].n;
       ipcio_close_block_write(hdu->data_block, bufsz);
       nblk++;
-      multilog(log, LOG_INFO, "block %" PRIu64 ": %" PRIu64 " of %" PRIu64 " frames placed (%.3f%% lost), "
+      multilog(log, LOG_INFO, "block %" PRId64 ": %" PRIu64 " of %" PRIu64 " frames placed (%.3f%% lost), "
                "%llu with a bad chunk", b, placed, cap, 100.0 * (double)(cap - placed) / (double)cap,
                cnt[nchunk + 2]);
       b2p_df_ref_advance(&ref, block_ndf);
-      /* batch b-1 is done with: its slot takes batch b+2 */
-      if (load_batch(ctx, fd, fc, &bt[(b + 2) % 3], cap, hf, hc) < 0) goto done;
+      /* batches whose frames all fell in blocks <= b are done with */
+      while (live && bt[head].hi <= b) {
+        head = (head + 1) % NSLOT;
+        live--;
+      }
     }
+    if (dropped)
+      multilog(log, LOG_WARNING, "%" PRIu64 " frames of batches dropped for want of slots (arrival "
+               "more than %d blocks out of order)", dropped, NSLOT - 2);
     multilog(log, LOG_INFO, "%" PRIu64 " frames read, %" PRIu64 " placed", sent_all, placed_all);
   }
   const double el = now_s() - t0;
@@ -258,7 +311,7 @@ done:
   if (locked) dada_hdu_unlock_write(hdu); /* ends the transfer (EOD) */
   dada_hdu_destroy(hdu);
   if (ctx) {
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < NSLOT; k++) {
       if (bt[k].frames) b2p_dev_free(ctx, bt[k].frames);
       if (bt[k].chunks) b2p_dev_free(ctx, bt[k].chunks);
     }

@@ -204,3 +204,55 @@ def test_stage_random_time_split(gpu, tmp_path_factory, case, nsplit):
         assert np.array_equal(sp[b, 0], co.power(g, blocks[b], nthreads=8).view(np.uint32)), (case, b)
     assert dada.header_get(ohdr, "NSPLIT", "%d") == nsplit
     assert f"reduce of {nsplit} time shares" in log
+
+
+@(seed(int(_SEED)) if _SEED else (lambda f: f))
+@settings(max_examples=8 * _SCALE, deadline=None, derandomize=_SEED is None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(st.integers(1, 64), st.integers(1, 8), st.integers(2, 5), st.floats(0.0, 0.3),
+       st.floats(0.05, 1.0), st.sampled_from([0, 249_990, 249_999]), st.integers(0, 2 ** 31))
+def test_dfdb_random_streams_to_spectra(gpu, tmp_path_factory, block_ndf, nblk, nbufs, loss, shuffle,
+                                        ref_idf, s):
+    """paf_dfgen stream (0-30 % of frames lost, arrival shuffled within up
+    to one block, the 27-s wrap near the start or not) -> paf_dfdb (GPU
+    assembly into a device ring, block by block) -> paf_baseband2power:
+    every block the stream has frames for comes out, and output b is the
+    oracle's spectrum of block b as the oracle places the stream's frames
+    (lost frames read as zeros).  Before paf_dfdb followed the frames'
+    timestamps, a lossy stream lost its last blocks and, further in, frames
+    drifted out of the batches assembled into their block."""
+    tmp = tmp_path_factory.mktemp("dfdb")
+    nchunk = 48
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=block_ndf * 128)
+    per_block = block_ndf * nchunk
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, s, 2, 5)
+    src = tmp / "bmf.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    df, ck = tmp / "s.df", tmp / "s.chunks"
+    ref_sec = 27 * 40
+    lost = int(loss * 1000)  # paf_dfgen -l: frames lost per mille
+    window = max(1, int(shuffle * per_block))
+    subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(nchunk),
+                    "-c", str(ck), "-x", str(ref_idf), "-s", str(ref_sec), "-r", str(s % 1000),
+                    "-w", str(window), "-l", str(lost)], check=True, capture_output=True)
+    kin, kout = fresh_key(), fresh_key()
+    from test_gpu_device_ring import HDR, _run_chain
+    sp, log = _run_chain(tmp, kin, kout,
+                         [os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-c", str(df),
+                          "-k", str(ck), "-n", str(nchunk), "-x", str(ref_idf), "-s", str(ref_sec)],
+                         "bmf", g.nout, nbufs, g.block_bytes)
+    dfs = np.fromfile(df, dtype=np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, dtype=np.uint8)
+    h = npo.df_decode(dfs)
+    rel = np.trunc(h["idf"].astype(np.float64) + (h["sec"].astype(np.float64) - ref_sec) / 1.08e-4 - ref_idf)
+    assert sp.shape[0] == int(rel.max()) // block_ndf + 1, log[-600:]    # every block with frames
+    idf, sec = ref_idf, ref_sec
+    for b in range(sp.shape[0]):
+        want = np.zeros(g.block_bytes, np.uint8)
+        co.assemble(dfs, chunk, idf, sec, want, block_ndf, nchunk)
+        assert np.array_equal(sp[b].view(np.uint32), co.power(g, want, nthreads=8).view(np.uint32)), \
+            (block_ndf, nblk, nbufs, lost, window, ref_idf, s, b)
+        gi = idf + block_ndf
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""How often does creating a GPU-resident ring (dada_db -g) fail, and where?
+
+Creates and destroys device rings of assorted block sizes and depths, N
+times each, one after another (as the stage property tests do), and prints
+one JSON line: attempts, failures and IPC-export retries per (block size,
+depth), and the holder's error text of each distinct failure.
+
+  python3 tools/devring_probe.py [ROUNDS] [use]   (use: open and write every ring)
+"""
+import collections
+import json
+import os
+import re
+import subprocess
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "paf-baseband2power_amd"))
+from paf_b2p import dada  # noqa: E402
+
+SIZES = [1040, 29952, 1 << 16, 1032192, 3096576, (3 << 20) + 48, 16 << 20]
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    use = len(sys.argv) > 2 and sys.argv[2] == "use"
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="devring_probe_")
+    key = 0x7e40
+    fails, retries, errs, attempts = collections.Counter(), collections.Counter(), {}, 0
+    for r in range(rounds):
+        for sz in SIZES:
+            for nb in (2, 4, 6):
+                attempts += 1
+                dada.destroy_ring(key)
+                try:
+                    p = subprocess.run([os.path.join(dada.BIN_DIR, "dada_db"), "-k", f"{key:x}", "-b", str(sz),
+                                        "-n", str(nb), "-g", "0"], capture_output=True, text=True, timeout=120)
+                    m = re.search(r"(\d+) IPC export retr", p.stderr)
+                    if m:
+                        retries[f"{sz}x{nb}"] += int(m.group(1))
+                    if p.returncode != 0:
+                        fails[f"{sz}x{nb}"] += 1
+                        e = p.stderr.strip()[-200:]
+                        errs[e] = errs.get(e, 0) + 1
+                    if p.returncode == 0 and use:
+                        # use the ring as the tests do: a reader process and
+                        # a writer here open every block's IPC handle
+                        sink = os.path.join(tmp, "sink.dada")
+                        if os.path.exists(sink):
+                            os.remove(sink)
+                        rd = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_dbdisk"), "-k", f"{key:x}",
+                                               "-o", sink], stderr=subprocess.DEVNULL)
+                        with dada.Hdu(key, "W") as w:
+                            w.write_header("HDR_SIZE 4096\n")
+                            for _ in range(nb + 1):
+                                w.write_block(b"\1" * sz)
+                        rd.wait(60)
+                        print(json.dumps({"used": f"{sz}x{nb}"}), flush=True)
+                finally:
+                    dada.destroy_ring(key)
+        print(json.dumps({"round": r, "attempts": attempts, "failures": sum(fails.values()),
+                          "retries": sum(retries.values())}), flush=True)
+    print(json.dumps({"attempts": attempts, "failures": sum(fails.values()), "by_case": fails,
+                      "retries": sum(retries.values()), "retries_by_case": retries, "errors": errs}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
