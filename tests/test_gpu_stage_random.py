@@ -256,3 +256,98 @@ def test_dfdb_random_streams_to_spectra(gpu, tmp_path_factory, block_ndf, nblk, 
             (block_ndf, nblk, nbufs, lost, window, ref_idf, s, b)
         gi = idf + block_ndf
         idf, sec = gi % 250000, sec + (gi // 250000) * 27
+
+
+@(seed(int(_SEED)) if _SEED else (lambda f: f))
+@settings(max_examples=6 * _SCALE, deadline=None, derandomize=_SEED is None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large, HealthCheck.filter_too_much,
+                                 HealthCheck.function_scoped_fixture])
+@given(st.integers(1, 48), st.integers(1, 64), st.integers(1, 6), st.floats(0.0, 0.3), st.floats(0.05, 1.5),
+       st.sampled_from([1000, 249_990]), st.integers(0, 2 ** 31))
+def test_capture_random_streams_to_spectra(gpu, tmp_path_factory, nchunk, block_ndf, nblk, loss, shuffle,
+                                           ref_idf, s):
+    """UDP (3 loopback ports) -> paf_capture (host sort by timestamp, GPU
+    assembly into a device ring) -> paf_baseband2power, for random chunk
+    counts, block lengths, 0-30 % of frames lost at the source and arrival
+    shuffled within up to 1.5 blocks (less than the temp buffer's 256 frame
+    times, so nothing arrives too late to be placed): every output is the
+    oracle's spectrum of its block as the oracle places the sent stream.
+    A run where the loopback itself dropped a frame says nothing about the
+    capture and is discarded (hypothesis.assume)."""
+    import threading
+    import time
+    from hypothesis import assume
+    tmp = tmp_path_factory.mktemp("cap")
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=block_ndf * 128)
+    per_block = block_ndf * nchunk
+    window = max(1, min(int(shuffle * per_block), 200 * nchunk))
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, s, 4, 2)
+    src = tmp / "in.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    df, ck = tmp / "s.df", tmp / "s.chunks"
+    ref_sec = 27 * 54
+    subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(nchunk),
+                    "-c", str(ck), "-x", str(ref_idf), "-s", str(ref_sec), "-f", "1300", "-r", str(s % 997),
+                    "-w", str(window), "-l", str(int(loss * 1000))], check=True, capture_output=True)
+    dfs = np.fromfile(df, dtype=np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, dtype=np.uint8)
+    hdr = tmp / "hdr.txt"
+    hdr.write_text(f"HDR_SIZE 4096\nNBIT 16\nNDIM 2\nNPOL 2\nNCHAN {nchunk * 7}\nNCHUNK {nchunk}\n"
+                   "NCHAN_CHUNK 7\nNSAMP_DF 128\nBYTE_ORDER BE\nTSAMP 0.84375\n")
+    kin, kout = fresh_key(), fresh_key()
+    dada.create_ring(kin, 4, g.block_bytes, device=0)
+    dada.create_ring(kout, 8, g.nout * 4)
+    port = 27000 + (os.getpid() % 400) * 8
+    out = tmp / "power.dada"
+    procs, cap_err = [], []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
+                                   f"{kout:x}", "-c", str(tmp), "-d", "0"], stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([os.path.join(BIN, "paf_capture"), "-a", f"{kin:x}", "-f", str(hdr),
+                                   "-c", str(block_ndf), "-n", str(nblk), "-P", str(port), "-N", "3",
+                                   "-m", "freq:1300", "-x", str(ref_idf), "-s", str(ref_sec), "-t", "1",
+                                   "-d", "0"], stderr=subprocess.PIPE, text=True)]
+        ready = threading.Event()
+
+        def drain():  # the capture's log; ready once its receive threads run
+            for ln in procs[2].stderr:
+                cap_err.append(ln)
+                if "receive thread(s) over" in ln:
+                    ready.set()
+        th = threading.Thread(target=drain, daemon=True)
+        th.start()
+        assert ready.wait(60), "".join(cap_err)[-800:]
+        snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-P",
+                              str(port), "-N", "3", "-r", "100"], capture_output=True, text=True)
+        assert snd.returncode == 0, snd.stderr
+        assert procs[2].wait(120) == 0, "".join(cap_err)[-800:]
+        th.join(10)
+        for p in procs[1::-1]:
+            _, e = p.communicate(timeout=120)
+            assert p.returncode == 0, e[-800:]
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+    log = "".join(cap_err)
+    import re
+    m = re.search(r"capture: (\d+) frames received", log)
+    assert m, log[-800:]
+    assume(int(m.group(1)) == len(dfs))      # the loopback delivered every frame sent
+    sp = data.view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == nblk, log[-800:]
+    idf, sec = ref_idf, ref_sec
+    for b in range(nblk):
+        want = np.zeros(g.block_bytes, np.uint8)
+        co.assemble(dfs, chunk, idf, sec, want, block_ndf, nchunk)
+        assert np.array_equal(sp[b], co.power(g, want, nthreads=8).view(np.uint32)), \
+            (nchunk, block_ndf, nblk, loss, window, ref_idf, s, b, log[-600:])
+        gi = idf + block_ndf
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27
