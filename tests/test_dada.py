@@ -503,3 +503,32 @@ def test_dbdisk_overwrites_only_with_W(tmp_path, ring):
             assert "-W overwrites" in err and out.read_bytes() == b"old"
     h, data = dada.read_dada_file(str(out))
     assert h.decode() == TEMPLATE and data.tobytes() == b"\5" * 1024
+
+
+def test_ascii_header_matches_a_dict_model():
+    """ascii_header_set / _get / _del against a dict: random sequences of
+    sets (new keys appended, existing keys replaced in place), deletes and
+    lookups of keys that share prefixes and suffixes with each other"""
+    from hypothesis import given, settings, strategies as st
+    keys = st.sampled_from(["NCHAN", "NCHAN_CHUNK", "XNCHAN", "NCH", "FREQ", "UTC_START", "A", "AB", "B_A"])
+    vals = st.one_of(st.integers(-10 ** 6, 10 ** 9).map(str),
+                     st.text(alphabet="abcdefXYZ0123456789.-:_", min_size=1, max_size=24))
+    ops = st.lists(st.tuples(st.sampled_from(["set", "del", "get"]), keys, vals), max_size=40)
+
+    @settings(max_examples=200, deadline=None, derandomize=True)
+    @given(ops)
+    def run(seq):
+        model = {}
+        h = b"HDR_SIZE 4096\n"
+        for op, k, v in seq:
+            if op == "set":
+                h = dada.header_set(h, k, v)
+                model[k] = v
+            elif op == "del":
+                h = dada.header_del(h, k)
+                model.pop(k, None)
+            assert dada.header_get(h, k) == model.get(k), (op, k, h)
+        for k in ("NCHAN", "NCHAN_CHUNK", "XNCHAN", "NCH", "FREQ", "UTC_START", "A", "AB", "B_A"):
+            assert dada.header_get(h, k) == model.get(k), (k, h)
+        assert dada.header_get(h, "HDR_SIZE", "%d") == 4096
+    run()

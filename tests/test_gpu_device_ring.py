@@ -103,7 +103,7 @@ def test_pipeline_with_device_input_ring(gpu, tmp_path):
     assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log
 
 
-def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz, device=0):
+def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz, device=0, stage_args=()):
     dada.create_ring(kin, nbufs, bufsz, device=device)
     dada.create_ring(kout, 4, nout * 4)
     try:
@@ -111,8 +111,8 @@ def _run_chain(tmp_path, kin, kout, producer, layout, nout, nbufs, bufsz, device
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}",
-                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", layout],
-                                  stderr=subprocess.PIPE),
+                                   "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0", "-f", layout]
+                                  + list(stage_args), stderr=subprocess.PIPE),
                  subprocess.Popen(producer, stderr=subprocess.PIPE)]
         msgs = _wait(procs)
         _, data = dada.read_dada_file(str(out))

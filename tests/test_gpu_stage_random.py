@@ -351,3 +351,39 @@ def test_capture_random_streams_to_spectra(gpu, tmp_path_factory, nchunk, block_
             (nchunk, block_ndf, nblk, loss, window, ref_idf, s, b, log[-600:])
         gi = idf + block_ndf
         idf, sec = gi % 250000, sec + (gi // 250000) * 27
+
+
+@(seed(int(_SEED)) if _SEED else (lambda f: f))
+@settings(max_examples=10 * _SCALE, deadline=None, derandomize=_SEED is None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(cases(), st.floats(0.0, 0.99))
+def test_diskdb_random_files_to_spectra(gpu, tmp_path_factory, case, tail):
+    """paf_diskdb (a DADA file: 4096-B header skipped, the template's header
+    passed on, diskdb.cu:69,79-93) -> host or GPU-resident ring -> the stage:
+    random layouts, ring depths and block counts, and a file that ends part-
+    way through a block (that partial integration is skipped)"""
+    g, nblk = case["g"], case["nblk"]
+    tmp = tmp_path_factory.mktemp("diskdb")
+    frames_tail = int(tail * (g.nsamp_int // g.nsamp_df))
+    payload = co.fill_synthetic(g, g.block_bytes * nblk + frames_tail * g.frame_bytes, case["seed"], 6, 1)
+    src = tmp / "obs.dada"
+    dada.write_dada_file(str(src), "FILE_HEADER_IS_SKIPPED 1\n", payload)
+    hdr = tmp / "header.txt"
+    hdr.write_text(f"HDR_SIZE 4096\nNBIT {g.nbit}\nNDIM 2\nNPOL 2\nNCHAN {g.nchunk * g.nchan_chunk}\n"
+                   f"NCHUNK {g.nchunk}\nNCHAN_CHUNK {g.nchan_chunk}\nNSAMP_DF {g.nsamp_df}\n"
+                   f"BYTE_ORDER {'BE' if g.big_endian else 'LE'}\nTSAMP 0.84375\n")
+    kin, kout = fresh_key(), fresh_key()
+    from test_gpu_device_ring import _run_chain
+    args = ["-p", str(g.npol_out)] + (["-m"] if g.mean else [])
+    sp, log = _run_chain(tmp, kin, kout,
+                         [os.path.join(BIN, "paf_diskdb"), "-a", f"{kin:x}", "-b", str(tmp), "-c", "obs.dada",
+                          "-d", str(hdr), "-e", "1"],
+                         "header", g.nout, case["nbufs"], g.block_bytes,
+                         device=0 if case["device"] else -1, stage_args=args)
+    assert sp.shape[0] == nblk, log[-600:]
+    for b in range(nblk):
+        blk = payload[b * g.block_bytes:(b + 1) * g.block_bytes]
+        assert np.array_equal(sp[b].view(np.uint32), co.power(g, blk, nthreads=8).view(np.uint32)), (case, b)
+    stage_log = open(str(tmp / "paf_baseband2power.log")).read()
+    assert ("partial integration skipped" in stage_log) == (frames_tail > 0), stage_log[-600:]
