@@ -549,6 +549,8 @@ static size_t pend_bytes(const b2p_ctx_t *c) {
   return (size_t)c->pend.nblk * c->nout * (c->pend.raw ? sizeof(unsigned long long) : sizeof(float));
 }
 
+static int flush_pending(b2p_ctx_t *c);
+
 // Enqueue one integrate launch over a device span (frame-aligned).  With
 // fused_out set, the launch also emits the integration (last workgroup).
 static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out,
@@ -586,6 +588,19 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
   a.fin_out = nullptr;
   a.fin_raw = 0;
   a.fin_nblk = 0;
+  // A deferred finalize rides on this launch in its own extra workgroup,
+  // which runs at no fixed point against the workgroup that emits a fused
+  // integration.  If both would write the same output (a caller reusing an
+  // output buffer before b2p_sync), the older spectrum could land last: run
+  // the deferred one first, on its own (found by tests/test_gpu_api_model.py).
+  if (fused_out && c->pend.valid) {
+    const char *f0 = reinterpret_cast<const char *>(fused_out), *f1 = f0 + (size_t)c->nout * sizeof(float);
+    const char *p0 = reinterpret_cast<const char *>(c->pend.dev_out), *p1 = p0 + pend_bytes(c);
+    if (f0 < p1 && p0 < f1) {
+      int rf = flush_pending(c);
+      if (rf != B2P_OK) return rf;
+    }
+  }
   const bool carry = c->pend.valid;
   if (carry) {
     a.fin_rep = c->pend.rep;

@@ -94,3 +94,27 @@ def test_integrate_n_refusals(gpu):
         out = it.integrate_n([d, d])
         assert same(out[0], out[1])
         d.free()
+
+
+def test_fused_integrate_into_an_output_still_pending(gpu):
+    """launch variant fuse=1: b2p_integrate emits its spectrum from the last
+    workgroup of its own launch, while the extra workgroup of that launch
+    finalizes the previous, deferred integration.  With both aimed at the
+    same output (reused before b2p_sync) the newer spectrum must win -- the
+    older one once landed last (tests/test_gpu_api_model.py found it)."""
+    g = npo.Geom(nbit=16, nchunk=2, nsamp_df=2, nchan_chunk=12, nsamp_int=4)
+    hosts = [co.fill_synthetic(g, g.block_bytes, SEED, 9, b) for b in range(2)]
+    want = [co.power(g, h).view(np.uint32) for h in hosts]
+    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict()), tuning={"fuse": 1}) as it:
+        ds = [it.upload(h) for h in hosts]
+        out = it.alloc(6 * g.nout * 4)
+        for _ in range(20):
+            it.integrate_n([ds[0]] * 6, out.ptr, True)      # deferred: slots 0..5 <- block 0
+            it.integrate(ds[1], out.ptr, True)               # fused: slot 0 <- block 1
+            it.sync()
+            got = it.download(out).view(np.uint32).reshape(6, g.nout)
+            assert np.array_equal(got[0], want[1])
+            for s in range(1, 6):
+                assert np.array_equal(got[s], want[0])
+        for d in ds + [out]:
+            d.free()
