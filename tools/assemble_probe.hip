@@ -14,6 +14,8 @@
 //   nt_512     512-thread workgroups
 //   pipe       software pipelined: frame i+1's loads issued before frame
 //              i's stores
+//   sw*        small grids (256-1024 workgroups): the whole grid sweeps the
+//              stream front to back with few frames in flight per CU
 // Prints one JSON line per variant: median GB/s of (read + write) bytes.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -143,6 +145,14 @@ int main(int argc, char **argv) {
       {"pipe", copy_kernel<1, 0, true>, 256, 2048},
       {"pipe_g4096", copy_kernel<1, 0, true>, 256, 4096},
       {"pipe_sc1", copy_kernel<1, 2, true>, 256, 2048},
+      // sweeps with few frames in flight per CU (the read_pattern_probe
+      // copy_sweep_u4 shape: ~32 KiB in flight per CU, grid front to back)
+      {"sw_g256_t512", copy_kernel<1, 0, false>, 512, 256},
+      {"sw_g512_t512", copy_kernel<1, 0, false>, 512, 512},
+      {"sw_g512_t256", copy_kernel<1, 0, false>, 256, 512},
+      {"sw_g1024_t256", copy_kernel<1, 0, false>, 256, 1024},
+      {"sw2_g256_t512", copy_kernel<2, 0, false>, 512, 256},
+      {"sw2_g512_t256", copy_kernel<2, 0, false>, 256, 512},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
