@@ -21,9 +21,11 @@
  *     follow the frames' timestamps, not the batch count, so a lossy stream
  *     (fewer frames than blocks x frames per block) still yields every
  *     block it has frames for.  A frame more than 2 blocks past the latest
- *     block seen so far is taken as corrupt and left out (capture.c:491-508
- *     drops far-future frames likewise).  The block is zeroed first unless
- *     -Z (the reference leaves lost frames' slots stale).
+ *     block seen so far is taken as corrupt and left out; the reference's
+ *     capture stops at such a frame (capture.c:491-508), and here a stream
+ *     whose frames jump that far ends its blocks at the jump as well.  The
+ *     block is zeroed first unless -Z (the reference leaves lost frames'
+ *     slots stale).
  *
  *   paf_dfdb -a key -b header_file -R nblocks [-f layout] [-r seed] [-d device]
  *     Replay: fill each ring block once with the synthetic generator, then
