@@ -7,12 +7,14 @@ a holder process (dada_db -g) and shared through HIP IPC handles.
   matches the oracle;
 * paf_dfdb assembles a raw data-frame stream (paf_dfgen) on the GPU straight
   into the ring block, and the spectra match the oracle of the original
-  blocks, with and without lost frames;
+  blocks, with and without lost frames; a corrupt far-future frame is left
+  out, and a stream that jumps blocks ahead ends at the jump;
 * replay mode hands out re-used blocks, spectra match the oracle;
 * blocks already queued when the stage gets to them are integrated in one
   launch (b2p_integrate_n), spectra bit-equal to the oracle.
 """
 import os
+import re
 import subprocess
 import time
 
@@ -154,6 +156,52 @@ def test_dfdb_assembles_stream_into_device_ring(gpu, tmp_path, lost):
         gi = idf + block_ndf
         idf, sec = gi % 250000, sec + (gi // 250000) * 27
     assert ("0.000% lost" in log) == (lost == 0)
+
+
+@pytest.mark.parametrize("case", ["corrupt_frame", "jump"])
+def test_dfdb_far_future_frames(gpu, tmp_path, case):
+    """A frame more than 2 blocks past the latest block seen is taken as
+    corrupt (paf_dfdb.c header; capture.c:491-508 stops the capture at one):
+    a single such frame is left out and every block still comes out; a
+    stream whose timestamps jump 4 blocks ahead ends its blocks at the jump."""
+    nchunk, block_ndf, nblk = 48, 16, 4
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=block_ndf * 128)
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, SEED, 6, 1)
+    ref_idf, ref_sec = 249_990, 27 * 40  # across a 27-s period
+    dfs, chunk = npo.df_stream(payload, nchunk, ref_idf, ref_sec)
+    t = np.arange(dfs.shape[0]) // nchunk
+    c = np.arange(dfs.shape[0]) % nchunk
+    if case == "corrupt_frame":
+        sel = np.array([(block_ndf + 3) * nchunk + 5])  # one frame of block 1
+        ahead = 5 * block_ndf
+    else:
+        sel = np.nonzero(t >= 2 * block_ndf)[0]  # blocks 2.. stamped 4 blocks later
+        ahead = 4 * block_ndf
+    gidf = ref_idf + t[sel] + ahead
+    dfs[sel, :npo.DF_HDR] = npo.df_encode(gidf % 250000, ref_sec + (gidf // 250000) * 27, 1, 0, 0, 1300 + c[sel])
+    df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
+    dfs.tofile(df)
+    chunk.tofile(ck)
+    kin, kout = fresh_key(), fresh_key()
+    sp, log = _run_chain(tmp_path, kin, kout,
+                         [os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-c", str(df),
+                          "-k", str(ck), "-n", str(nchunk), "-x", str(ref_idf), "-s", str(ref_sec)],
+                         "bmf", g.nout, 3, g.block_bytes)
+    want_blocks = nblk if case == "corrupt_frame" else 2
+    assert sp.shape[0] == want_blocks, log[-600:]
+    idf, sec = ref_idf, ref_sec
+    for b in range(want_blocks):
+        want = np.zeros(g.block_bytes, np.uint8)
+        co.assemble(dfs, chunk, idf, sec, want, block_ndf, nchunk)
+        if case == "corrupt_frame" and b == 1:  # the corrupt frame's slot stays zero
+            s0 = (3 * nchunk + 5) * npo.DF_PAYLOAD
+            assert not want[s0:s0 + npo.DF_PAYLOAD].any()
+        assert np.array_equal(sp[b].view(np.uint32), co.power(g, want, nthreads=8).view(np.uint32)), (case, b)
+        gi = idf + block_ndf
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27
+    placed = sum(int(x) for x in re.findall(r"block \d+: (\d+) of", log))
+    assert placed == (nblk * block_ndf * nchunk - 1 if case == "corrupt_frame" else 2 * block_ndf * nchunk), log
 
 
 @pytest.mark.parametrize("device", [0, -1])  # GPU-resident ring, and a host ring for contrast
