@@ -135,17 +135,21 @@ def header_block(text: bytes | str, size: int = HDR_SIZE) -> bytes:
 # ---- rings --------------------------------------------------------------------------
 
 def create_ring(key: int, nbufs: int, bufsz: int, nreaders: int = 1, hdr_nbufs: int = 8,
-                hdr_bufsz: int = HDR_SIZE, device: int = -1) -> None:
+                hdr_bufsz: int = HDR_SIZE, device: int = -1, page: bool = False) -> None:
     """device >= 0: data blocks in that GPU's memory (dada_db -g).  That ring
     is made by the dada_db executable, never in this process: its holder is
-    forked, and forking a process that runs threads (torch) is not safe."""
-    if device >= 0:
+    forked, and forking a process that runs threads (torch) is not safe.
+    page=True: the host blocks' pages are allocated now (dada_db -p, as the
+    reference's launcher creates its rings, paf-baseband2power.py:114-115),
+    not by the first write of the first block."""
+    if device >= 0 or page:
         import subprocess
         r = subprocess.run([os.path.join(BIN_DIR, "dada_db"), "-k", f"{key:x}", "-b", str(bufsz),
-                            "-n", str(nbufs), "-r", str(nreaders), "-H", str(hdr_bufsz),
-                            "-g", str(device)], capture_output=True, text=True, timeout=300)
+                            "-n", str(nbufs), "-r", str(nreaders), "-H", str(hdr_bufsz)]
+                           + (["-g", str(device)] if device >= 0 else ["-p"]),
+                           capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
-            raise OSError(f"dada_db -g {device} {key:x}: {r.stderr.strip()}")
+            raise OSError(f"dada_db {'-g %d' % device if device >= 0 else '-p'} {key:x}: {r.stderr.strip()}")
         return
     if dlib().dada_db_create(key, nbufs, bufsz, nreaders, hdr_nbufs, hdr_bufsz) != 0:
         raise OSError(C.get_errno(), f"dada_db_create {key:x}")

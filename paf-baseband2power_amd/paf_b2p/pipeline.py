@@ -97,8 +97,10 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
                     f.write(f"key {k:x}\n")
             dada.destroy_ring(kin)
             dada.destroy_ring(kout)
+            # dada_db -p, as the reference's launcher (paf-baseband2power.py:114;
+            # its -l needs CAP_IPC_LOCK and is left out)
             dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"],
-                             device=_ring_device(gpu, r) if device_ring else -1)
+                             device=_ring_device(gpu, r) if device_ring else -1, page=not device_ring)
             keys.append(kin)
             obytes = c["b2p_rbufsz"] * npol_out
             dada.create_ring(kout, c["b2p_nbuf"], obytes, c["b2p_nreader"])
@@ -191,8 +193,10 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
         for r in range(nsub):
             kin = c["diskdb_key"] + 0x10 * r
             dada.destroy_ring(kin)
+            # dada_db -p, as the reference's launcher (paf-baseband2power.py:114;
+            # its -l needs CAP_IPC_LOCK and is left out)
             dada.create_ring(kin, c["diskdb_nbuf"], c["diskdb_rbufsz"], c["diskdb_nreader"],
-                             device=_ring_device(gpu, r) if device_ring else -1)
+                             device=_ring_device(gpu, r) if device_ring else -1, page=not device_ring)
             keys.append(kin)
         out = os.path.join(directory, "power.dada")
         procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],

@@ -273,9 +273,10 @@ def test_dada_db_tool_create_destroy():
 
 # ---- executables: diskdb -> ring -> dbdisk (byte-exact) -------------------------------
 
-def run_diskdb(key, path, hdr_path, sod=1):
+def run_diskdb(key, path, hdr_path, sod=1, threads=None):
     return subprocess.Popen([f"{BIN}/paf_diskdb", "-a", f"{key:x}", "-b", os.path.dirname(path),
-                             "-c", os.path.basename(path), "-d", hdr_path, "-e", str(sod)],
+                             "-c", os.path.basename(path), "-d", hdr_path, "-e", str(sod)]
+                            + ([] if threads is None else ["-T", str(threads)]),
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE)
 
 
@@ -298,6 +299,45 @@ def test_diskdb_to_dbdisk_bytes(tmp_path, ring, payload_blocks):
     h, data = dada.read_dada_file(str(out))
     assert h.decode() == TEMPLATE                # diskdb.cu:79-93: the template header
     assert np.array_equal(data, payload)         # diskdb.cu:69,103-121: payload only
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+@pytest.mark.parametrize("payload_blocks", [2.0, 2.37, 0.4, 0.0])
+def test_diskdb_parallel_readers_same_bytes(tmp_path, ring, threads, payload_blocks):
+    """-T N: each block is read as N contiguous slices in parallel (2 MiB
+    pieces); the ring sees the same blocks as one fread per block gives --
+    whole blocks, then the short (or empty) one that ends the transfer"""
+    bufsz = (5 << 20) + 4096  # not a whole number of 2 MiB pieces
+    k = ring(3, bufsz)
+    payload = np.random.default_rng(int(payload_blocks * 100) + threads).integers(
+        0, 256, int(bufsz * payload_blocks), dtype=np.uint8)
+    src = tmp_path / "obs.dada"
+    dada.write_dada_file(str(src), "FILE_HEADER_IS_SKIPPED 1\n", payload)
+    hdr = tmp_path / "header.txt"
+    hdr.write_text(TEMPLATE)
+    seen = []
+
+    def consumer():
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            while (b := r.read_block()) is not None:
+                seen.append(bytes(b))
+
+    t = threading.Thread(target=consumer)
+    t.start()
+    p = run_diskdb(k, str(src), str(hdr), threads=threads)
+    assert p.wait(60) == 0, p.stderr.read()
+    t.join(60)
+    nfull = len(payload) // bufsz
+    assert [len(b) for b in seen[:nfull]] == [bufsz] * nfull
+    assert b"".join(seen) == payload.tobytes()
+    assert f"{threads} reader" in p.stderr.read().decode()
+
+
+def test_diskdb_rejects_bad_thread_count(tmp_path):
+    r = subprocess.run([f"{BIN}/paf_diskdb", "-a", "dada", "-c", "x", "-d", "y", "-T", "0"],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "-T takes 1..64" in r.stderr
 
 
 def test_dbdisk_default_file_name(tmp_path, ring):

@@ -32,6 +32,10 @@ PSRDADA_SUBSET = {
     "multilog_open", "multilog_add", "multilog_close", "multilog",
     "dada_hdu_lock_read", "dada_hdu_unlock_read", "ipcbuf_get_next_read", "ipcbuf_mark_cleared",
     "ipcio_open_block_read", "ipcio_close_block_read", "ipcbuf_eod", "ascii_header_get",
+    # paf_diskdb -T pre-maps the ring's blocks: the block count, from the
+    # libpsrdada linked into the reference's own paf_diskdb (0x4053b0,
+    # tests/golden/psrdada_abi.json)
+    "ipcbuf_get_nbufs",
 }
 DADA_PREFIX = re.compile(r"^(dada_|ipcbuf_|ipcio_|ascii_header_|multilog|fileread)")
 

@@ -14,7 +14,7 @@ The file (--nint integrations, 1 GiB each, synthetic) is written first and
 read once before the legs, so it is served from the page cache.  Prints one
 JSON line per leg.
 
-  python tools/bench_diskdb.py [--nint 4] [--legs sink,cpu,gpu] [--threads 16]
+  python tools/bench_diskdb.py [--nint 4] [--legs sink,cpu,gpu] [--threads 16] [--readers 1,8] [--page 0,1]
 """
 from __future__ import annotations
 
@@ -42,12 +42,12 @@ HDR = os.path.join(os.path.dirname(BIN), "conf", "header_baseband2power.txt")
 SEED = 20181105
 
 
-def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str) -> dict:
+def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str, readers: int, page: bool) -> dict:
     kin, kout = 0x7d00, 0x7d10
     for k in (kin, kout):
         dada.destroy_ring(k)
     bufsz = g.block_bytes
-    dada.create_ring(kin, 2, bufsz)
+    dada.create_ring(kin, 2, bufsz, page=page)  # dada_db -p: the reference launcher's ring
     procs, out = [], {}
     try:
         seen, acc = [], np.zeros(g.nout, dtype=np.uint64)
@@ -66,7 +66,7 @@ def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str) -> di
 
         if leg == "gpu":
             dada.create_ring(kout, 8, g.nout * 4)
-            procs.append(subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o",
+            procs.append(subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-W", "-o",
                                            os.path.join(workdir, "power.dada")], stderr=subprocess.PIPE))
             procs.append(subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b",
                                            f"{kout:x}", "-c", workdir, "-d", "0", "-f", f"int8:{g.nchan}"],
@@ -76,7 +76,7 @@ def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str) -> di
             th.start()
         t0 = time.perf_counter()
         dk = subprocess.Popen([os.path.join(BIN, "paf_diskdb"), "-a", f"{kin:x}", "-b", os.path.dirname(path),
-                               "-c", os.path.basename(path), "-d", HDR, "-e", "1"],
+                               "-c", os.path.basename(path), "-d", HDR, "-e", "1", "-T", str(readers)],
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE)
         procs.append(dk)
         dk_out, dk_err = dk.communicate(timeout=600)
@@ -85,11 +85,26 @@ def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str) -> di
         m = re.search(r"diskdb: (\d+) B in \d+ blocks, ([0-9.]+) s", (dk_out + dk_err).decode(errors="replace"))
         diskdb = {"diskdb_s": float(m.group(2)), "diskdb_GBps": round(int(m.group(1)) / float(m.group(2)) / 1e9, 2)} \
             if m and float(m.group(2)) > 0 else {}
+        m = re.search(r"([0-9.]+) s reading \(([0-9.]+) GB/s; ([0-9.]+) s of it in the first pass over the (\d+) "
+                      r"ring blocks\), ([0-9.]+) s waiting", (dk_out + dk_err).decode(errors="replace"))
+        if m:
+            rest_s, rest_b = float(m.group(1)) - float(m.group(3)), (nint - int(m.group(4))) * bufsz
+            diskdb.update({"diskdb_read_s": float(m.group(1)), "diskdb_read_GBps": float(m.group(2)),
+                           "diskdb_first_pass_s": float(m.group(3)), "diskdb_wait_s": float(m.group(5)),
+                           "diskdb_read_GBps_after_first_pass": round(rest_b / rest_s / 1e9, 2) if rest_s > 0 else None})
+        m = re.search(r"([0-9.]+) s mapping the ring", (dk_out + dk_err).decode(errors="replace"))
+        if m:
+            diskdb["diskdb_map_s"] = float(m.group(1))
         if leg == "gpu":
+            errs = {}
             for p in procs:
-                p.wait(600)
+                if p is dk:
+                    errs[p] = dk_err
+                else:
+                    _, errs[p] = p.communicate(timeout=600)
             if any(p.returncode for p in procs):
-                raise RuntimeError("\n".join(p.stderr.read().decode(errors="replace")[-800:] for p in procs))
+                raise RuntimeError("\n".join(f"{os.path.basename(p.args[0])} rc={p.returncode}: "
+                                             + errs[p].decode(errors="replace")[-800:] for p in procs))
             wall = time.perf_counter() - t0
             log = open(os.path.join(workdir, "paf_baseband2power.log")).read()
             m = re.search(r"FINISH PAF_PROCESS: (\d+) integrations.* ([0-9.]+) s from the first", log)
@@ -120,6 +135,8 @@ def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str) -> di
             "GBps_wall": round(nint * bufsz / wall / 1e9, 2),
             "Msamples_s_wall": round(nint * samples / wall / 1e6, 1),
             "threads": threads if leg == "cpu" else None,
+            "diskdb_readers": readers,
+            "ring_paged": page,
         })
         return out
     finally:
@@ -137,6 +154,8 @@ def main():
     ap.add_argument("--legs", default="sink,cpu,gpu")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--nchan", type=int, default=256)
+    ap.add_argument("--readers", default="8", help="paf_diskdb -T values, comma-separated (one set of legs each)")
+    ap.add_argument("--page", default="1", help="ring created with dada_db -p (1) or not (0); comma-separated")
     a = ap.parse_args()
     g = npo.Geom(nbit=8, nchan_chunk=a.nchan)
     workdir = tempfile.mkdtemp(prefix="bench_diskdb_")
@@ -149,8 +168,10 @@ def main():
         while f.read(64 << 20):
             pass
     try:
-        for leg in a.legs.split(","):
-            print(json.dumps(run_leg(leg, path, a.nint, g, a.threads, workdir)), flush=True)
+        for page in (x == "1" for x in a.page.split(",")):
+            for readers in (int(x) for x in a.readers.split(",")):
+                for leg in a.legs.split(","):
+                    print(json.dumps(run_leg(leg, path, a.nint, g, a.threads, workdir, readers, page)), flush=True)
     finally:
         os.unlink(path)
     return 0
