@@ -165,10 +165,11 @@ static void *populate_span(void *arg) {
 }
 
 /* Before the first block: the ring's blocks mapped writable in this process,
- * nthread spans at a time.  Measured on the GPU box's host (DESIGN.md
- * section 7): a ring block's first pass took 3-4x as long as later ones,
- * the page faults of the freshly attached segment, which now happen here
- * in parallel and before any data moves. */
+ * nthread spans at a time, so that no page fault lands in the data path.
+ * On the GPU box's host (profiles/r04_diskdb_readers_paging.jsonl) this took
+ * 0.16-0.19 s for a ring of 2 x 1 GiB made with dada_db -p, and 0.33-0.68 s
+ * for one that was not (its pages are allocated here); the reads after it
+ * ran at 65-92 GB/s with 8-16 threads against 18-22 GB/s with one. */
 static void populate_ring(const conf_t *conf) {
   ipcbuf_t *db = (ipcbuf_t *)conf->hdu->data_block;
 #ifndef B2P_PSRDADA

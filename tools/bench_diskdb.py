@@ -65,6 +65,9 @@ def run_leg(leg: str, path: str, nint: int, g, threads: int, workdir: str, reade
                     r.release_block(len(b))
 
         if leg == "gpu":
+            stage_log = os.path.join(workdir, "paf_baseband2power.log")
+            if os.path.exists(stage_log):  # appended to by every run: this leg's lines only
+                os.unlink(stage_log)
             dada.create_ring(kout, 8, g.nout * 4)
             procs.append(subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-W", "-o",
                                            os.path.join(workdir, "power.dada")], stderr=subprocess.PIPE))
