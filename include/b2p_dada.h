@@ -158,6 +158,10 @@ int ipcbuf_get_device(ipcbuf_t *id);
  * kind (memcpy, or a synchronous hipMemcpy for a device ring) */
 int ipcbuf_copy_in(ipcbuf_t *id, char *block, const void *src, uint64_t n);
 int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n);
+/* extension: why this thread's last device-ring call failed (hipMemcpy,
+ * hipIpcOpenMemHandle ...: the HIP call, its error string and code); ""
+ * when none has */
+const char *dada_device_error(void);
 /* Extension: make every ring wait of this process (a reader waiting for a
  * block, a writer waiting for a free one) give up -- the call fails, e.g.
  * ipcio_open_block_read returns NULL -- instead of resuming, once a signal

@@ -90,6 +90,16 @@ static int hip_load(void) {
   return hip.loaded > 0 ? 0 : -1;
 }
 
+/* this thread's last device-ring failure (dada_device_error) */
+static __thread char dev_err[200];
+
+const char *dada_device_error(void) { return dev_err; }
+
+static void dev_fail(const char *what, int code) {
+  snprintf(dev_err, sizeof dev_err, "%s: %s (%d)", what, code >= 0 && hip.err_str ? hip.err_str(code) : "unavailable",
+           code);
+}
+
 static void report(int fd, const char *what, int code) {
   char msg[240];
   int n = snprintf(msg, sizeof msg, "E%s: %s", what,
@@ -252,8 +262,20 @@ int dev_stop_holder(dev_seg_t *seg0) {
 
 int dev_open_blocks(ipcbuf_t *id) {
   const dev_seg_t *seg0 = id->shm_addr[0];
-  if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) != 1 || hip_load() < 0 ||
-      hip.set_device(id->sync->on_device_id) != 0) {
+  int rc;
+  if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) != 1) {
+    snprintf(dev_err, sizeof dev_err, "device ring: no live holder (state %d)",
+             __atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE));
+    errno = ENODEV;
+    return -1;
+  }
+  if (hip_load() < 0) {
+    dev_fail("dlopen libamdhip64.so.7", -1);
+    errno = ENODEV;
+    return -1;
+  }
+  if ((rc = hip.set_device(id->sync->on_device_id)) != 0) {
+    dev_fail("hipSetDevice", rc);
     errno = ENODEV;
     return -1;
   }
@@ -261,7 +283,15 @@ int dev_open_blocks(ipcbuf_t *id) {
     ipc_handle_t h;
     void *p = NULL;
     memcpy(&h, id->shm_addr[i], DEV_HANDLE_BYTES);
-    if (hip.open_handle(&p, h, 1 /* hipIpcMemLazyEnablePeerAccess */) != 0) {
+    if ((rc = hip.open_handle(&p, h, 1 /* hipIpcMemLazyEnablePeerAccess */)) != 0) {
+      char w[80];
+      snprintf(w, sizeof w, "hipIpcOpenMemHandle (block %llu of %llu)", (unsigned long long)i,
+               (unsigned long long)id->sync->nbufs);
+      dev_fail(w, rc);
+      for (uint64_t j = 0; j < i; j++) { /* none of them stays open */
+        hip.close_handle(id->buffer[j]);
+        id->buffer[j] = NULL;
+      }
       errno = ENODEV;
       return -1;
     }
@@ -281,13 +311,32 @@ void dev_close_blocks(ipcbuf_t *id) {
 
 int dev_copy(void *dst, const void *src, uint64_t n) {
   if (!n) return 0;
-  if (hip_load() < 0) return -1;
-  return hip.memcpy_(dst, src, n, 4 /* hipMemcpyDefault */) == 0 ? 0 : -1;
+  if (hip_load() < 0) {
+    dev_fail("dlopen libamdhip64.so.7", -1);
+    return -1;
+  }
+  const int rc = hip.memcpy_(dst, src, n, 4 /* hipMemcpyDefault */);
+  if (rc != 0) {
+    char w[96];
+    snprintf(w, sizeof w, "hipMemcpy of %llu B (%p <- %p)", (unsigned long long)n, dst, src);
+    dev_fail(w, rc);
+    return -1;
+  }
+  return 0;
 }
 
 /* zero n bytes of a device block, finished on return (ipc_zero_buffer_cuda) */
 int dev_zero(void *dst, uint64_t n) {
   if (!n) return 0;
-  if (hip_load() < 0) return -1;
-  return hip.memset_(dst, 0, n) == 0 && hip.sync() == 0 ? 0 : -1;
+  if (hip_load() < 0) {
+    dev_fail("dlopen libamdhip64.so.7", -1);
+    return -1;
+  }
+  int rc = hip.memset_(dst, 0, n);
+  if (rc == 0) rc = hip.sync();
+  if (rc != 0) {
+    dev_fail("hipMemset", rc);
+    return -1;
+  }
+  return 0;
 }

@@ -64,6 +64,8 @@ def dlib():
         L.ipcbuf_get_device.argtypes = [P]
         L.ipcbuf_set_read_depth.argtypes = [P, C.c_int]
         L.ipcbuf_copy_in.argtypes = [P, P, P, C.c_uint64]
+        L.dada_device_error.restype = C.c_char_p
+        L.dada_device_error.argtypes = []
         L.ipcbuf_copy_out.argtypes = [P, P, P, C.c_uint64]
         for n in ("ipcbuf_get_nfull", "ipcbuf_get_nclear", "ipcbuf_get_sodack", "ipcbuf_get_eodack"):
             getattr(L, n).restype = C.c_uint64
@@ -155,6 +157,11 @@ def create_ring(key: int, nbufs: int, bufsz: int, nreaders: int = 1, hdr_nbufs: 
         raise OSError(C.get_errno(), f"dada_db_create {key:x}")
 
 
+def device_error() -> str:
+    """why this thread's last device-ring call failed (dada_device_error)"""
+    return (dlib().dada_device_error() or b"").decode(errors="replace")
+
+
 def destroy_ring(key: int) -> bool:
     return dlib().dada_db_destroy(key) == 0
 
@@ -171,7 +178,8 @@ class Hdu:
         L.dada_hdu_set_key(self.h, key)
         if L.dada_hdu_connect(self.h) != 0:
             L.dada_hdu_destroy(self.h)
-            raise OSError(f"no ring at key {key:x}")
+            why = device_error()
+            raise OSError(f"no ring at key {key:x}" + (f" ({why})" if why else ""))
         lock = {"W": L.dada_hdu_lock_write, "R": L.dada_hdu_lock_read, "r": L.dada_hdu_open_view}[mode]
         if lock(self.h) != 0:
             L.dada_hdu_destroy(self.h)
@@ -203,7 +211,7 @@ class Hdu:
             raise ValueError("block too large")
         src = bytes(data)
         if L.ipcbuf_copy_in(self.data, p, src, n) != 0:  # hipMemcpy for a device ring
-            raise OSError("copy into block")
+            raise OSError(f"copy into block: {device_error()}")
         L.ipcio_close_block_write(self.data, n)
 
     # reader ----------------------------------------------------------------------
