@@ -4,7 +4,10 @@
 Creates and destroys device rings of assorted block sizes and depths, N
 times each, one after another (as the stage property tests do), and prints
 one JSON line: attempts, failures and IPC-export retries per (block size,
-depth), and the holder's error text of each distinct failure.
+depth), and the holder's error text of each distinct failure.  With `use`,
+each used ring's line also carries this process's open file descriptors
+and mapped size after the ring was closed, so a per-import leak in the HIP
+runtime's IPC path shows as steady growth.
 
   python3 tools/devring_probe.py [ROUNDS] [use]   (use: open and write every ring)
 """
@@ -22,7 +25,19 @@ from paf_b2p import dada  # noqa: E402
 SIZES = [1040, 29952, 1 << 16, 1032192, 3096576, (3 << 20) + 48, 16 << 20]
 
 
+def _vm() -> dict:
+    out = {}
+    for line in open("/proc/self/status"):
+        k, _, v = line.partition(":")
+        if k in ("VmSize", "VmRSS"):
+            out[k] = v.strip()
+    return out
+
+
 def main():
+    import resource
+    print(json.dumps({"rlimit_nofile": resource.getrlimit(resource.RLIMIT_NOFILE),
+                      "fds": len(os.listdir("/proc/self/fd"))}), flush=True)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     use = len(sys.argv) > 2 and sys.argv[2] == "use"
     import tempfile
@@ -52,12 +67,19 @@ def main():
                             os.remove(sink)
                         rd = subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_dbdisk"), "-k", f"{key:x}",
                                                "-o", sink], stderr=subprocess.DEVNULL)
-                        with dada.Hdu(key, "W") as w:
-                            w.write_header("HDR_SIZE 4096\n")
-                            for _ in range(nb + 1):
-                                w.write_block(b"\1" * sz)
+                        try:
+                            with dada.Hdu(key, "W") as w:
+                                w.write_header("HDR_SIZE 4096\n")
+                                for _ in range(nb + 1):
+                                    w.write_block(b"\1" * sz)
+                        except OSError as e:  # the device-ring error text, then stop
+                            rd.kill()
+                            print(json.dumps({"error": str(e), "case": f"{sz}x{nb}",
+                                              "fds": len(os.listdir("/proc/self/fd"))}), flush=True)
+                            raise
                         rd.wait(60)
-                        print(json.dumps({"used": f"{sz}x{nb}"}), flush=True)
+                        print(json.dumps({"used": f"{sz}x{nb}", "fds": len(os.listdir("/proc/self/fd")),
+                                          "vm": _vm()}), flush=True)
                 finally:
                     dada.destroy_ring(key)
         print(json.dumps({"round": r, "attempts": attempts, "failures": sum(fails.values()),
