@@ -55,6 +55,13 @@
 #define DEVICE_RINGS 1
 #endif
 
+/* why the last device-ring call of this thread failed ("" for host rings) */
+#if DEVICE_RINGS
+#define RING_WHY() dada_device_error()
+#else
+#define RING_WHY() ""
+#endif
+
 #define MSTR_LEN 512 /* paf_baseband2power.cuh:4 */
 #define TSAMP_BMF_US (27.0 / 32.0) /* README.md:2 */
 #define MAX_SUB 64
@@ -992,7 +999,7 @@ int main(int argc, char *argv[]) {
     s->in = dada_hdu_create(log);
     dada_hdu_set_key(s->in, s->key);
     if (dada_hdu_connect(s->in) < 0 || dada_hdu_lock_read(s->in) < 0) {
-      multilog(log, LOG_ERR, "cannot attach/lock input ring %x", (unsigned)s->key);
+      multilog(log, LOG_ERR, "cannot attach/lock input ring %x %s", (unsigned)s->key, RING_WHY());
       goto done;
     }
     s->locked = 1;

@@ -451,7 +451,7 @@ int main(int argc, char **argv) {
     c.hdu = dada_hdu_create(c.log);
     dada_hdu_set_key(c.hdu, key);
     if (dada_hdu_connect(c.hdu) < 0 || dada_hdu_lock_write(c.hdu) < 0) {
-      multilog(c.log, LOG_ERR, "cannot attach/lock ring %x", (unsigned)key);
+      multilog(c.log, LOG_ERR, "cannot attach/lock ring %x %s", (unsigned)key, dada_device_error());
       goto done;
     }
     locked = 1;

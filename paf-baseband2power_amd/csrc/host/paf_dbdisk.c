@@ -71,7 +71,7 @@ int main(int argc, char **argv) {
   dada_hdu_t *hdu = dada_hdu_create(log);
   dada_hdu_set_key(hdu, key);
   if (dada_hdu_connect(hdu) < 0 || dada_hdu_lock_read(hdu) < 0) {
-    fprintf(stderr, "paf_dbdisk: cannot attach/lock ring %x\n", (unsigned)key);
+    fprintf(stderr, "paf_dbdisk: cannot attach/lock ring %x %s\n", (unsigned)key, dada_device_error());
     return EXIT_FAILURE;
   }
   if (dada_hdu_open_read(hdu) < 0) {

@@ -157,7 +157,7 @@ int main(int argc, char **argv) {
   void *stage = NULL; /* replay into a host ring: blocks generated on the GPU, copied down */
   int locked = 0;
   if (dada_hdu_connect(hdu) < 0 || dada_hdu_lock_write(hdu) < 0) {
-    multilog(log, LOG_ERR, "cannot attach/lock ring %x for writing", (unsigned)key);
+    multilog(log, LOG_ERR, "cannot attach/lock ring %x for writing %s", (unsigned)key, dada_device_error());
     goto done;
   }
   locked = 1;

@@ -92,7 +92,11 @@ static int init_diskdb(conf_t *conf) {
   dada_hdu_set_key(conf->hdu, conf->key);
   if (dada_hdu_connect(conf->hdu) < 0) {
     multilog(conf->log, LOG_ERR, "could not connect to hdu");
+#ifdef B2P_PSRDADA
     fprintf(stderr, "Can not connect to hdu %x\n", (unsigned)conf->key);
+#else
+    fprintf(stderr, "Can not connect to hdu %x %s\n", (unsigned)conf->key, dada_device_error());
+#endif
     return EXIT_FAILURE;
   }
   ipcbuf_t *db = (ipcbuf_t *)conf->hdu->data_block; /* diskdb.cu:33 */
@@ -283,7 +287,7 @@ static int do_diskdb(conf_t *conf) {
     const size_t n = (size_t)got;
 #ifndef B2P_PSRDADA
     if (stage && ipcbuf_copy_in(db, curbuf, stage, n) < 0) {
-      multilog(conf->log, LOG_ERR, "copy into device block failed");
+      multilog(conf->log, LOG_ERR, "copy into device block failed: %s", dada_device_error());
       free(stage);
       return EXIT_FAILURE;
     }
