@@ -572,3 +572,15 @@ def test_ascii_header_matches_a_dict_model():
             assert dada.header_get(h, k) == model.get(k), (k, h)
         assert dada.header_get(h, "HDR_SIZE", "%d") == 4096
     run()
+
+
+def test_device_error_is_empty_until_a_device_ring_call_fails():
+    # dada_device_error: per thread, "" until a device-ring call fails (host
+    # rings never set it); the Python OSErrors carry it (paf_b2p.dada)
+    import threading
+    assert dada.device_error() == ""
+    got = []
+    t = threading.Thread(target=lambda: got.append(dada.device_error()))
+    t.start()
+    t.join()
+    assert got == [""]
