@@ -7,6 +7,7 @@
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 #          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4 pmc1
+#          devleak
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -180,6 +181,9 @@ for s in $STEPS; do
             -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_bmf 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_bmf" -o run \
             -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
+    devleak) # a few hundred device-ring create / write / destroy cycles in one process:
+             # open fds and mapped size per ring
+             run devring_leak 600 python3 tools/devring_probe.py 10 use ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
