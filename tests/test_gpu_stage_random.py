@@ -1,5 +1,6 @@
 """Property test of the stage end to end: `paf_baseband2power` between a
-PSRDADA writer (this process) and `paf_dbdisk`, on layouts the input header
+PSRDADA writer (this process for host rings, `paf_diskdb` processes for
+GPU-resident rings) and `paf_dbdisk`, on layouts the input header
 describes (NBIT, NCHAN, NCHUNK, NCHAN_CHUNK, NSAMP_DF, BYTE_ORDER; the
 reference's TFTFP family), with random ring depths, block counts, output
 pols, sum or mean, GPU-resident or host rings, pipelined or one block at a
@@ -49,6 +50,21 @@ def cases(draw):
                 seed=draw(st.integers(0, 2 ** 32 - 1)))
 
 
+def _diskdb_writer(tmp, key, hdr, blocks, short_bytes=None):
+    """write blocks (plus an optional short tail) to a DADA file and start a
+    paf_diskdb process that feeds it into ring `key`: GPU-resident rings are
+    written from their own process, as in production, so this test process
+    never imports a ring block's IPC handle"""
+    name = f"in_{key:x}.dada"
+    parts = [b.reshape(-1).view(np.uint8) for b in blocks]
+    if short_bytes is not None:
+        parts.append(parts[0][:short_bytes])
+    dada.write_dada_file(str(tmp / name), "FILE_HEADER_IS_SKIPPED 1\n", np.concatenate(parts))
+    (tmp / f"hdr_{key:x}.txt").write_text(hdr)
+    return subprocess.Popen([os.path.join(BIN, "paf_diskdb"), "-a", f"{key:x}", "-b", str(tmp), "-c", name,
+                             "-d", str(tmp / f"hdr_{key:x}.txt"), "-e", "1"], stderr=subprocess.PIPE)
+
+
 @(seed(int(_SEED)) if _SEED else (lambda f: f))
 @settings(max_examples=24 * _SCALE, deadline=None, derandomize=_SEED is None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
@@ -73,12 +89,15 @@ def test_stage_random_layouts_rings_and_flags(gpu, tmp_path_factory, case):
                                    "-c", str(tmp), "-d", "0", "-f", "header", "-p", str(g.npol_out)]
                                   + (["-m"] if g.mean else []) + (["-S"] if case["sync"] else []),
                                   stderr=subprocess.PIPE)]
-        with dada.Hdu(kin, "W") as w:
-            w.write_header(hdr)
-            for b in blocks:
-                w.write_block(b.tobytes())
-            if case["short"]:  # end of data part-way through an integration
-                w.write_block(blocks[0][: g.frame_bytes].tobytes())
+        if case["device"]:  # end of data part-way through an integration: a short tail
+            procs.append(_diskdb_writer(tmp, kin, hdr, blocks, g.frame_bytes if case["short"] else None))
+        else:
+            with dada.Hdu(kin, "W") as w:
+                w.write_header(hdr)
+                for b in blocks:
+                    w.write_block(b.tobytes())
+                if case["short"]:  # end of data part-way through an integration
+                    w.write_block(blocks[0][: g.frame_bytes].tobytes())
         _wait(procs, timeout=120)
         ohdr, data = dada.read_dada_file(str(out))
     finally:
@@ -133,7 +152,11 @@ def _run_stage(tmp, g, keys, rings_blocks, stage_args, device, nbufs, out_nsub, 
                         w.write_block(blocks[0][: g.frame_bytes].tobytes())
             except Exception as e:  # noqa: BLE001 -- reported below
                 errs.append(e)
-        ths = [threading.Thread(target=writer, args=(k, bl, k in short)) for k, bl in zip(keys, rings_blocks)]
+        if device:  # GPU-resident rings: one paf_diskdb process per ring
+            procs += [_diskdb_writer(tmp, k, hdr, bl, g.frame_bytes if k in short else None)
+                      for k, bl in zip(keys, rings_blocks)]
+        ths = [] if device else [threading.Thread(target=writer, args=(k, bl, k in short))
+                                 for k, bl in zip(keys, rings_blocks)]
         for t in ths:
             t.start()
         for t in ths:
