@@ -11,10 +11,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "b2p.h"
 #include "b2p_internal.h"
+#include "b2p_plan.h"
 
 using namespace b2p;
 
@@ -32,6 +34,20 @@ struct EvPair {
   uint64_t bytes;
   int kind;  // 0 integrate, 1 finalize
 };
+
+// Host memory registered through b2p_register_host, process-wide (HIP's
+// registration is): which context registered each range, so that b2p_close
+// releases what its context registered and a register that overlaps a live
+// registration is refused up front.  A range left registered after its
+// owner freed it is the hazard: HIP would keep serving copies of that
+// address from the stale pinned mapping ("Host memory").
+struct HostReg {
+  const char *base;
+  size_t bytes;
+  const b2p_ctx *owner;
+};
+std::mutex g_reg_mu;
+std::vector<HostReg> g_regs;
 
 }  // namespace
 
@@ -79,7 +95,9 @@ struct b2p_ctx {
   hipEvent_t ev_copied[2] = {nullptr, nullptr};
   hipEvent_t ev_consumed[2] = {nullptr, nullptr};
   uint32_t stage_next = 0;
+  int staging_ready = 0;        // both buffers, their events and the copy stream exist
   uint64_t samples = 0;
+  unsigned long long *d_dbg = nullptr;  // B2P_DEBUG builds: out-of-bounds records (b2p_kernels.hip)
   // timing: 1 = per-launch dispatch-packet events, 2 = one event pair
   // around a region of launches (no per-launch packets)
   int timing = 0;
@@ -103,6 +121,7 @@ struct b2p_ctx {
   b2p_tuning_t tun{};           // launch variant (b2p_open_tuned); defaults otherwise
 #ifdef B2P_TEST_HOOKS
   long inject_push_fail = -1;  // test build only: b2p_test_inject_push_fail
+  long dbg_shrink = 0;         // debug + test build only: b2p_test_debug_shrink_bound
 #endif
   char err[256] = {0};
 };
@@ -130,15 +149,6 @@ static int set_err(b2p_ctx_t *c, int code, const char *fmt, ...) {
       return set_err((c), B2P_EHIP, "%s failed at %s:%d: %s", #call, __FILE__, \
                      __LINE__, hipGetErrorString(e_));                         \
   } while (0)
-
-static uint32_t gcd_u(uint32_t a, uint32_t b) {
-  while (b) {
-    uint32_t t = a % b;
-    a = b;
-    b = t;
-  }
-  return a;
-}
 
 static uint64_t word_bytes(const b2p_geom_t *g) {
   return (uint64_t)g->npol * g->ndim * (g->nbit / 8);
@@ -221,81 +231,25 @@ int b2p_device_count(int *count) {
   return B2P_OK;
 }
 
-// Choose the workgroup shape (DESIGN.md "integrate kernel / launch shape").
+// The workgroup shape (b2p_plan.h plan_shape, shared with the CPU address
+// model of tests/c/plan_model.cpp).
 static int plan_launch(b2p_ctx_t *c, int ncu) {
   const b2p_geom_t *g = &c->g;
-  const b2p_tuning_t &t = c->tun;
-  const uint32_t wb = (uint32_t)word_bytes(g);
-  c->VW = 16 / wb;
-  c->IV = g->nsamp_df * g->nchan_chunk / c->VW;
-  c->FV = g->nchunk * c->IV;
-  const uint32_t P = g->nchan_chunk / gcd_u(g->nchan_chunk, c->VW);
-  c->CP = g->nchunk == 1 ? P : c->FV;
-  uint32_t maxT = g->nbit == 8 ? 512 : 448;
-  if (t.max_threads) maxT = (uint32_t)t.max_threads;
-  const uint32_t L = c->CP / gcd_u(c->CP, 64) * 64;  // lcm(CP, 64)
-  uint32_t colB = 0;  // whole-wave divisor of L for a row split into columns
-  if (c->CP <= maxT && L > maxT && g->nchunk == 1)
-    for (uint32_t b = maxT / 64 * 64; b >= 256 && !colB; b -= 64)
-      if (L % b == 0) colB = b;
-  if (c->CP <= maxT && !colB) {
-    c->B = L <= maxT ? (maxT / L) * L : (maxT / c->CP) * c->CP;
-    c->S = c->B;
-    c->NC = 1;
-  } else if (colB) {
-    // the channel period fits a workgroup but not in whole waves (e.g. 336
-    // int8 channels = 84 vectors): a row of lcm(period, 64) vectors split
-    // into whole-wave columns keeps every lane on fixed channels without a
-    // partial wave (504 threads measured 6.3 TB/s, tools/perf_matrix.py)
-    c->B = colB;
-    c->S = L;
-    c->NC = L / colB;
-  } else {
-    // the frame is split into NC = CP / B columns: the largest whole-wave B
-    // (multiple of 64) that divides the frame -- partial waves straddle
-    // 1-KiB lines and measured 10-15 % slower (BMF: 168 or 336 threads)
-    uint32_t best = 0;
-    for (uint32_t b = maxT / 64 * 64; b >= 64; b -= 64)
-      if (c->CP % b == 0) { best = b; break; }
-    // a power-of-two frame (TFTFP 8x8 int16: 4096 vectors) divides into 256
-    // under the int16 cap; 512-thread columns, one per CU, measured 2-4 %
-    // faster there (8 KiB contiguous per row and workgroup), while BMF keeps
-    // 448 (512 measured 2.7 % slower; profiles/r03_tune_frame_split.jsonl)
-    if (!t.max_threads && best && best <= 256 && maxT < 512 && c->CP % 512 == 0) best = 512;
-    if (t.threads) {  // tuning: an exact whole-wave divisor of the frame
-      if (c->CP % (uint32_t)t.threads)
-        return set_err(c, B2P_EINVAL, "tuning threads %d does not divide the %u-vector frame",
-                       t.threads, c->CP);
-      best = (uint32_t)t.threads;
-    }
-    if (best) {
-      c->B = best;
-      c->S = c->CP;
-      c->NC = c->CP / c->B;
-    } else {
-      // no whole-wave divisor (e.g. 61 chunks x 11 vectors): rows of
-      // lcm(frame, 64) vectors, split into whole-wave columns (64 always
-      // divides), so every lane still keeps its channels
-      const uint64_t rowv = (uint64_t)c->CP / gcd_u(c->CP, 64) * 64;
-      if (rowv > 0x7fffffffull) return set_err(c, B2P_EINVAL, "frame of %u vectors too large", c->CP);
-      uint32_t b = maxT / 64 * 64;
-      while (b > 64 && rowv % b) b -= 64;
-      c->B = b;
-      c->S = (uint32_t)rowv;
-      c->NC = (uint32_t)(rowv / b);
-    }
-  }
-  c->Bpad = (c->B + 63) / 64 * 64;
-  // one workgroup per CU: with ~32 KiB of loads in flight per CU more
-  // resident waves only cost bandwidth (tools/tune.py sweep)
-  // ... counted as ~8 waves: a narrower workgroup (a frame that only
-  // divides into 256-thread columns) gets two per CU
-  uint32_t per_cu = std::max<uint32_t>(1, 512 / c->Bpad);
-  if (t.wg_per_cu) per_cu = (uint32_t)t.wg_per_cu;
-  const uint32_t target = (uint32_t)ncu * per_cu;
-  c->G = std::max<uint32_t>(1, (target + c->NC / 2) / c->NC);
-  if (t.row_groups) c->G = (uint32_t)t.row_groups;  // e.g. long per-lane runs in tests
-  c->nrep = t.replicas ? (uint32_t)t.replicas : 16;
+  const ShapeKnobs k{c->tun.max_threads, c->tun.threads, c->tun.wg_per_cu, c->tun.row_groups, c->tun.replicas};
+  Shape sh;
+  char msg[160];
+  if (plan_shape(g->nbit, g->nchunk, g->nsamp_df, g->nchan_chunk, k, ncu, &sh, msg, sizeof msg) != 0)
+    return set_err(c, B2P_EINVAL, "%s", msg);
+  c->VW = sh.VW;
+  c->IV = sh.IV;
+  c->FV = sh.FV;
+  c->CP = sh.CP;
+  c->B = sh.B;
+  c->Bpad = sh.Bpad;
+  c->S = sh.S;
+  c->NC = sh.NC;
+  c->G = sh.G;
+  c->nrep = sh.nrep;
   return B2P_OK;
 }
 
@@ -414,6 +368,11 @@ int b2p_open_tuned(b2p_ctx_t **out, const b2p_geom_t *g, int device, const b2p_t
   // sized for uint64 sums too (b2p_finish_partial_async to host)
   if (hipMalloc(&c->d_out, (size_t)c->nout * sizeof(unsigned long long)) != hipSuccess)
     return fail(set_err(c, B2P_ENOMEM, "hipMalloc out"));
+#ifdef B2P_DEBUG
+  if (hipMalloc(&c->d_dbg, 8 * sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_dbg, 0, 8 * sizeof(unsigned long long)) != hipSuccess)
+    return fail(set_err(c, B2P_ENOMEM, "hipMalloc debug record"));
+#endif
   if (hipMemsetAsync(c->d_rep, 0, rep_bytes, c->stream) != hipSuccess ||
       hipStreamSynchronize(c->stream) != hipSuccess)
     return fail(set_err(c, B2P_EHIP, "zero replicas"));
@@ -464,6 +423,17 @@ int b2p_close(b2p_ctx_t *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   drain_timing(c);
+  {  // what this context registered and the caller did not release
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (auto it = g_regs.begin(); it != g_regs.end();) {
+      if (it->owner == c) {
+        (void)hipHostUnregister(const_cast<char *>(it->base));
+        it = g_regs.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 2; ++i) {
     if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
@@ -474,6 +444,7 @@ int b2p_close(b2p_ctx_t *c) {
   if (c->d_out) (void)hipFree(c->d_out);
   if (c->d_mrep) (void)hipFree(c->d_mrep);
   if (c->d_mout) (void)hipFree(c->d_mout);
+  if (c->d_dbg) (void)hipFree(c->d_dbg);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   for (auto e : c->fence_ev)
     if (e) (void)hipEventDestroy(e);
@@ -512,16 +483,40 @@ int b2p_set_stream(b2p_ctx_t *c, void *s) {
 
 int b2p_register_host(b2p_ctx_t *c, void *base, size_t bytes) {
   if (!c || !base || !bytes) return B2P_EINVAL;
+  const char *b = static_cast<const char *>(base);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (const HostReg &r : g_regs)
+    if (b < r.base + r.bytes && r.base < b + bytes)
+      return set_err(c, B2P_EINVAL, "host range %p+%zu overlaps the registered range %p+%zu", base, bytes,
+                     (const void *)r.base, r.bytes);
   CK(c, hipSetDevice(c->device));
   CK(c, hipHostRegister(base, bytes, hipHostRegisterDefault));
+  g_regs.push_back(HostReg{b, bytes, c});
+  return B2P_OK;
+}
+
+// Release a registration once no copy of this context can still read or
+// write the range: the context's streams are drained first (a host finish
+// may still be landing in it; a failed push's copies were drained by
+// b2p_push).  Work the caller enqueued on other contexts or streams that
+// touches the range must be complete before this call.
+static int unregister_locked(b2p_ctx_t *c, const char *base) {
+  if (c->stream) CK(c, hipStreamSynchronize(c->stream));
+  if (c->copy_stream) CK(c, hipStreamSynchronize(c->copy_stream));
+  CK(c, hipHostUnregister(const_cast<char *>(base)));
   return B2P_OK;
 }
 
 int b2p_unregister_host(b2p_ctx_t *c, void *base) {
   if (!c || !base) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));
-  CK(c, hipHostUnregister(base));
-  return B2P_OK;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  const char *b = static_cast<const char *>(base);
+  int rc = unregister_locked(c, b);
+  if (rc == B2P_OK)
+    g_regs.erase(std::remove_if(g_regs.begin(), g_regs.end(), [b](const HostReg &r) { return r.base == b; }),
+                 g_regs.end());
+  return rc;
 }
 
 static hipEvent_t pool_event(b2p_ctx_t *c) {
@@ -551,6 +546,22 @@ static size_t pend_bytes(const b2p_ctx_t *c) {
 
 static int flush_pending(b2p_ctx_t *c);
 
+#ifdef B2P_DEBUG
+// Debug build: read the kernels' out-of-bounds record (b2p_kernels.hip
+// dbg_record) once the stream is idle; a record fails the call with the
+// access that would have been made, and the context.
+static int dbg_check(b2p_ctx_t *c) {
+  CK(c, hipStreamSynchronize(c->stream));
+  unsigned long long r[5] = {0, 0, 0, 0, 0};
+  CK(c, hipMemcpy(r, c->d_dbg, sizeof r, hipMemcpyDeviceToHost));
+  if (r[0] == 0) return B2P_OK;
+  c->failed = 1;
+  return set_err(c, B2P_EHIP,
+                 "B2P_DEBUG: %llu out-of-bounds %s; first: index %llu of %llu, workgroup %llu thread %llu", r[0],
+                 r[1] == 1 ? "span loads" : "output slots", r[2], r[3], r[4] >> 32, r[4] & 0xffffffffull);
+}
+#endif
+
 // Enqueue one integrate launch over a device span (frame-aligned).  With
 // fused_out set, the launch also emits the integration (last workgroup).
 static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *fused_out,
@@ -578,6 +589,26 @@ static int enqueue_span(b2p_ctx_t *c, const void *dev, uint64_t nbytes, float *f
     for (uint32_t b = 0; b < nblk; ++b) a.blk[b] = (const uint4 *)blocks[b];
   }
   a.out = fused_out;
+  a.dbg = c->d_dbg;
+  a.dbg_bound = a.nvec;
+#if defined(B2P_DEBUG) && defined(B2P_TEST_HOOKS)
+  if (c->dbg_shrink) a.dbg_bound = a.nvec > (uint64_t)c->dbg_shrink ? a.nvec - (uint64_t)c->dbg_shrink : 0;
+#endif
+#ifdef B2P_DEBUG
+  // the launch invariants the kernel's indexing assumes
+  {
+    const unsigned long long *r0 = c->d_rep, *r1 = c->d_rep + 2 * (size_t)c->nrep * c->nout;
+    if (blocks) r0 = c->d_mrep, r1 = c->d_mrep + 2 * (size_t)kMaxBlk * c->nrep * c->nout;
+    const unsigned long long *a0 = a.rep, *a1 = a.rep + (size_t)a.nblk * a.set_words;
+    if (nbytes % c->frame_bytes || nbytes % 16 || (uint64_t)c->NC * c->B > c->S || a0 < r0 || a1 > r1 ||
+        (size_t)c->nout * sizeof(unsigned long long) > 65536 || !c->d_dbg)
+      return set_err(c, B2P_EINVAL,
+                     "B2P_DEBUG: launch invariants: span %llu B (frame %llu), NC %u x B %u vs S %u, replicas "
+                     "[%p,%p) in [%p,%p)",
+                     (unsigned long long)nbytes, (unsigned long long)c->frame_bytes, c->NC, c->B, c->S,
+                     (const void *)a0, (const void *)a1, (const void *)r0, (const void *)r1);
+  }
+#endif
   a.ticket = c->d_ticket + c->cur;
   a.mean = c->g.mean;
   a.nsamp = (double)c->g.nsamp_int;
@@ -663,14 +694,29 @@ static int flush_pending(b2p_ctx_t *c) {
   return B2P_OK;
 }
 
-static int ensure_staging(b2p_ctx_t *c) {
-  if (c->d_stage[0]) return B2P_OK;
+// The staging pair, its events and the copy stream: all or nothing (a
+// half-made set would hand push_host a null buffer or stream).
+static void release_staging(b2p_ctx_t *c) {
+  for (int i = 0; i < 2; ++i) {
+    if (c->d_stage[i]) (void)hipFree(c->d_stage[i]);
+    if (c->ev_copied[i]) (void)hipEventDestroy(c->ev_copied[i]);
+    if (c->ev_consumed[i]) (void)hipEventDestroy(c->ev_consumed[i]);
+    c->d_stage[i] = nullptr;
+    c->ev_copied[i] = c->ev_consumed[i] = nullptr;
+  }
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  c->copy_stream = nullptr;
+}
+
+static int make_staging(b2p_ctx_t *c) {
   const uint64_t want = (uint64_t)(c->tun.stage_mib ? c->tun.stage_mib : 256) << 20;
-  uint64_t sb = want / c->frame_bytes * c->frame_bytes;
-  if (sb == 0) sb = c->frame_bytes;
+  const uint64_t sb = stage_bytes_for(want, c->frame_bytes);
   c->stage_bytes = sb;
   for (int i = 0; i < 2; ++i) {
-    if (hipMalloc(&c->d_stage[i], sb) != hipSuccess) return set_err(c, B2P_ENOMEM, "hipMalloc staging");
+    if (hipMalloc(&c->d_stage[i], sb) != hipSuccess) {
+      c->d_stage[i] = nullptr;
+      return set_err(c, B2P_ENOMEM, "hipMalloc staging");
+    }
     CK(c, hipEventCreateWithFlags(&c->ev_copied[i], hipEventDisableTiming));
     CK(c, hipEventCreateWithFlags(&c->ev_consumed[i], hipEventDisableTiming));
   }
@@ -679,17 +725,60 @@ static int ensure_staging(b2p_ctx_t *c) {
   return B2P_OK;
 }
 
+static int ensure_staging(b2p_ctx_t *c) {
+  if (c->staging_ready) return B2P_OK;
+  const int rc = make_staging(c);
+  if (rc != B2P_OK) {
+    (void)hipStreamSynchronize(c->stream);  // the consumed-event records
+    release_staging(c);
+    return rc;
+  }
+  c->staging_ready = 1;
+  return B2P_OK;
+}
+
+#ifdef B2P_DEBUG
+// Debug build: the invariants push_host relies on, checked per chunk; a
+// violation fails the push with its text instead of reaching the GPU.
+#define DBG_REQUIRE(c, cond, ...)                                                           \
+  do {                                                                                       \
+    if (!(cond)) return set_err((c), B2P_EINVAL, "B2P_DEBUG: " __VA_ARGS__);                 \
+  } while (0)
+
+// A host range inside a registration must end inside it: a copy that ran
+// past the registered pages would read memory HIP never mapped.
+static int dbg_check_host_range(b2p_ctx_t *c, const uint8_t *h, uint64_t n) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  const char *p = reinterpret_cast<const char *>(h);
+  for (const HostReg &r : g_regs)
+    if (p >= r.base && p < r.base + r.bytes)
+      DBG_REQUIRE(c, p + n <= r.base + r.bytes, "host chunk %p+%llu runs past its registration %p+%zu",
+                  (const void *)p, (unsigned long long)n, (const void *)r.base, r.bytes);
+  return B2P_OK;
+}
+#endif
+
 // A host span through the two staging buffers: chunk k is copied on the
 // copy stream while chunk k-1 is integrated.  Returns once every copy has
 // landed (the caller may release the span).  A failure after the first
-// chunk leaves part of the span summed.
+// chunk leaves part of the span summed, and copies from the span may still
+// be in flight: b2p_push drains them before it returns.
 static int push_host(b2p_ctx_t *c, const uint8_t *h, uint64_t nbytes) {
   if (int rm = region_mark(c)) return rm;  // the region holds the copies as well
   int last = -1;
   long k = 0;
   for (uint64_t off = 0; off < nbytes; off += c->stage_bytes, ++k) {
-    const uint64_t n = std::min<uint64_t>(c->stage_bytes, nbytes - off);
+    const uint64_t n = stage_chunk(nbytes, c->stage_bytes, off);
     const int i = (int)(c->stage_next++ & 1);
+#ifdef B2P_DEBUG
+    DBG_REQUIRE(c, c->staging_ready && c->d_stage[i] && c->copy_stream && c->ev_copied[i] && c->ev_consumed[i],
+                "staging set incomplete at chunk %ld", k);
+    DBG_REQUIRE(c, n > 0 && n <= c->stage_bytes && n % c->frame_bytes == 0 && off + n <= nbytes,
+                "chunk %ld: %llu B at %llu of a %llu-B span, staging %llu B, frame %llu B", k,
+                (unsigned long long)n, (unsigned long long)off, (unsigned long long)nbytes,
+                (unsigned long long)c->stage_bytes, (unsigned long long)c->frame_bytes);
+    if (int rd = dbg_check_host_range(c, h + off, n)) return rd;
+#endif
 #ifdef B2P_TEST_HOOKS
     if (k == c->inject_push_fail)
       return set_err(c, B2P_EHIP, "injected failure at staging chunk %ld (test build)", k);
@@ -735,10 +824,19 @@ int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
     if ((rc = ensure_staging(c)) != B2P_OK) return rc;
     rc = push_host(c, (const uint8_t *)buf, nbytes);
     if (rc != B2P_OK) {
-      // part of the span may already be summed: the integration is unknown
+      // part of the span may already be summed: the integration is unknown.
+      // Copies from the span may still be in flight: drain them, so that the
+      // caller can release (unregister, free, close its DADA block) the span
+      // as soon as this returns -- a copy still reading memory its owner
+      // has released is a GPU page fault
+      (void)hipStreamSynchronize(c->copy_stream);
+      (void)hipStreamSynchronize(c->stream);
       c->failed = 1;
       return rc;
     }
+#ifdef B2P_DEBUG
+    if ((rc = dbg_check(c)) != B2P_OK) return rc;
+#endif
   }
   c->samples += samples;
   return B2P_OK;
@@ -865,6 +963,9 @@ int b2p_sync(b2p_ctx_t *c) {
   int rc = flush_pending(c);
   if (rc != B2P_OK) return rc;
   CK(c, hipStreamSynchronize(c->stream));
+#ifdef B2P_DEBUG
+  if ((rc = dbg_check(c)) != B2P_OK) return rc;
+#endif
   return B2P_OK;
 }
 
@@ -1081,6 +1182,22 @@ int b2p_test_inject_push_fail(b2p_ctx_t *c, long chunk) {
   c->inject_push_fail = chunk;
   return B2P_OK;
 }
+#endif
+
+#ifdef B2P_DEBUG
+// Debug build only (lib/debug/libpafb2p.so, -DB2P_DEBUG): 1.
+int b2p_debug_build(void) { return 1; }
+#ifdef B2P_TEST_HOOKS
+// Debug + test build: the bound the kernels check span loads against is
+// lowered by `vectors` on later launches, so the last rows of a span read
+// as out-of-bounds loads -- the detector is exercised without any access
+// outside real memory (tests/debug_build_checks.py).
+int b2p_test_debug_shrink_bound(b2p_ctx_t *c, long vectors) {
+  if (!c || vectors < 0) return B2P_EINVAL;
+  c->dbg_shrink = vectors;
+  return B2P_OK;
+}
+#endif
 #endif
 
 }  // extern "C"

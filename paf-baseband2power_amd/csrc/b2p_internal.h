@@ -50,6 +50,10 @@ struct IntegrateArgs {
   uint32_t fin_nblk;
   uint64_t set_words;           // nrep * nout
   const uint4 *blk[kMaxBlk];
+  // debug build only (B2P_DEBUG): where out-of-bounds accesses are recorded
+  // (b2p_kernels.hip dbg_record); null and unused in the release library
+  unsigned long long *dbg;
+  uint64_t dbg_bound;           // the bound loads are checked against (nvec)
 };
 
 struct FinalizeArgs {

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include "b2p_internal.h"
+#include "b2p_plan.h"
 
 namespace b2p {
 
@@ -128,6 +129,39 @@ __device__ __forceinline__ u32x4 stream_load(const u32x4 *p) {
   return *p;
 }
 
+#ifdef B2P_DEBUG
+// Debug build (make B2P_DEBUG=1 -> lib/debug/libpafb2p.so): every access the
+// launch would make outside its span or its outputs is recorded in a.dbg
+// instead of being made -- [0] count, [1] kind (1 load, 2 output slot),
+// [2] offending index, [3] its bound, [4] workgroup << 32 | thread -- and the
+// host turns a non-zero count into an error naming the access (b2p_ctx.hip
+// dbg_check).  Plain vector-memory atomics and stores.
+__device__ __noinline__ void dbg_record(unsigned long long *dbg, uint64_t kind, uint64_t idx, uint64_t bound) {
+  if (atomicAdd(&dbg[0], 1ull) == 0) {
+    dbg[1] = kind;
+    dbg[2] = idx;
+    dbg[3] = bound;
+    dbg[4] = ((unsigned long long)blockIdx.x << 32) | threadIdx.x;
+  }
+}
+#endif
+
+// A load of the span: in a debug build, checked against the span's nvec
+// vectors (an out-of-span load is recorded and not made).
+template <bool NT>
+__device__ __forceinline__ u32x4 checked_load(const IntegrateArgs &a, const u32x4 *data, const u32x4 *p) {
+#ifdef B2P_DEBUG
+  const uint64_t idx = (uint64_t)(p - data);
+  if (idx >= a.dbg_bound) {
+    dbg_record(a.dbg, 1, idx, a.dbg_bound);
+    return u32x4{0u, 0u, 0u, 0u};
+  }
+#else
+  (void)a, (void)data;
+#endif
+  return stream_load<NT>(p);
+}
+
 __device__ __forceinline__ float to_output(unsigned long long tot, uint32_t mean, double nsamp) {
   // tot < 2^53: the double is exact, the float conversion is the one RNE
   const double d = (double)tot;
@@ -190,28 +224,12 @@ b2p_integrate_kernel(IntegrateArgs a) {
 
   // channels of this lane's VW word slots (fixed for the whole launch)
   uint32_t ch[VW];
-  {
-    // a row may hold several frames (B a multiple of the frame): fold first
-    const uint32_t fpos = a.nchunk == 1 ? pos : pos % a.FV;
-    const uint32_t chunk = a.nchunk == 1 ? 0u : fpos / a.IV;
-    const uint32_t q = a.nchunk == 1 ? pos : fpos % a.IV;
-#pragma unroll
-    for (int w = 0; w < VW; ++w)
-      ch[w] = chunk * a.nchan_chunk + (q * VW + w) % a.nchan_chunk;
-  }
+  lane_channels<VW>(pos, a.nchunk, a.FV, a.IV, a.nchan_chunk, ch);
 
   const uint64_t full = a.nvec / a.S;  // rows with every vector valid
   // this group's rows: rstart + i * rstep, i < rcount
   uint64_t rstart, rstep, rcount;
-  if (a.interleave) {
-    rstart = grp;
-    rstep = a.G;
-    rcount = full > grp ? (full - grp + a.G - 1) / a.G : 0;
-  } else {
-    rstart = (uint64_t)grp * full / a.G;
-    rstep = 1;
-    rcount = (uint64_t)(grp + 1) * full / a.G - rstart;
-  }
+  group_rows(full, grp, a.G, a.interleave, &rstart, &rstep, &rcount);
   // one integration per block: the rows of block b stream through the same
   // lanes (same channels), then the workgroup's sums go to block b's set
   const uint32_t nblk = MULTI ? a.nblk : 1u;
@@ -233,18 +251,18 @@ b2p_integrate_kernel(IntegrateArgs a) {
       for (; i + UNROLL <= iend; i += UNROLL) {
         u32x4 v[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = stream_load<NT>(p + u * stepv);
+        for (int u = 0; u < UNROLL; ++u) v[u] = checked_load<NT>(a, data, p + u * stepv);
         p += UNROLL * stepv;
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) acc.add(v[u]);
       }
-      for (; i < iend; ++i, p += stepv) acc.add(stream_load<NT>(p));
+      for (; i < iend; ++i, p += stepv) acc.add(checked_load<NT>(a, data, p));
       acc.flush();
     }
     // ragged last row (span not a whole number of rows): the last group of
     // every column takes it, its lanes keep their channels
-    if (grp == a.G - 1 && full * a.S + pos < a.nvec) {
-      acc.add(data[full * a.S + pos]);
+    if (takes_ragged_row(grp, a.G, full, a.S, pos, a.nvec)) {
+      acc.add(checked_load<false>(a, data, data + full * a.S + pos));
       acc.flush();
     }
   }
@@ -255,6 +273,12 @@ b2p_integrate_kernel(IntegrateArgs a) {
 #pragma unroll
       for (int p = 0; p < NPO; ++p) {
         const unsigned long long x = acc.get(w, p);
+#ifdef B2P_DEBUG
+        if (ch[w] * NPO + p >= a.nout) {
+          dbg_record(a.dbg, 2, ch[w] * NPO + p, a.nout);
+          continue;
+        }
+#endif
         if (x) atomicAdd(&lds[ch[w] * NPO + p], x);
       }
   }

@@ -60,6 +60,7 @@ static struct {
   int (*memcpy_)(void *, const void *, size_t, int);
   int (*sync)(void);
   const char *(*err_str)(int);
+  int (*addr_range)(void **, size_t *, void *); /* hipMemGetAddressRange (diagnostics) */
 } hip;
 
 static int hip_load(void) {
@@ -82,6 +83,7 @@ static int hip_load(void) {
   SYM(memcpy_, "hipMemcpy");
   SYM(sync, "hipDeviceSynchronize");
   SYM(err_str, "hipGetErrorString");
+  SYM(addr_range, "hipMemGetAddressRange");
 #undef SYM
   hip.loaded = (hip.set_device && hip.malloc_ && hip.free_ && hip.memset_ && hip.get_handle &&
                 hip.open_handle && hip.close_handle && hip.memcpy_ && hip.sync && hip.err_str)
@@ -110,11 +112,25 @@ static void report(int fd, const char *what, int code) {
 #define DEV_ALLOC_ALIGN (2ull << 20)
 #define DEV_EXPORT_TRIES 4
 
-/* the holder: owns the blocks until SIGTERM/SIGINT or the ring is removed */
+/* processes attached to block 0's segment besides the holder and the
+ * destroyers that only wait for it: the importers (dada_internal.h) */
+static long importers_attached(int seg0_id, const dev_seg_t *seg0) {
+  struct shmid_ds ds;
+  if (shmctl(seg0_id, IPC_STAT, &ds) < 0) return 0; /* gone: nobody can be attached */
+  const long n = (long)ds.shm_nattch - 1 - __atomic_load_n(&seg0->stop_waiters, __ATOMIC_ACQUIRE);
+  return n > 0 ? n : 0;
+}
+
+/* the holder: owns the blocks until it is told to stop (SIGTERM/SIGINT/
+ * SIGHUP), the ring is removed, or DADA_HOLDER_IDLE_S seconds pass with no
+ * importer -- and in every case only once no importer is attached (the
+ * ordering rule in dada_internal.h), so no process can still have a block
+ * mapped when it is freed */
 static void holder(ipcbuf_t *id, int device, int wfd) {
   int rc;
   const uint64_t n = id->sync->nbufs, bufsz = id->sync->bufsz;
   dev_seg_t *seg0 = id->shm_addr[0];
+  const int seg0_id = id->shmid[0];
   void **blk = calloc(n, sizeof(void *));
   if (!blk) {
     report(wfd, "calloc", -1);
@@ -131,15 +147,15 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
   /* each block its own allocation of whole 2 MiB pages: HIP serves small
    * requests (a 29 952-B block did) from a shared sub-allocated chunk, and
    * hipIpcGetMemHandle refuses a pointer inside one ("invalid argument").
-   * The export also failed now and then for whole 2-4 MiB allocations in a
-   * fresh holder (a ring created right after another was destroyed,
-   * tests/test_gpu_stage_random.py); such a block is kept aside (so the
-   * next hipMalloc cannot return it), and a new one is taken, up to
-   * DEV_EXPORT_TRIES times per block.  The spares are freed once the ring
-   * is complete. */
+   * An export that still fails is retried with a fresh allocation (the
+   * failed one kept aside so hipMalloc cannot hand it back), up to
+   * DEV_EXPORT_TRIES times per block; the first failure's call, error and
+   * hipMemGetAddressRange of the pointer are reported with the retry count
+   * (the R message), so a retry is never silent. */
   const uint64_t alloc = (bufsz + DEV_ALLOC_ALIGN - 1) / DEV_ALLOC_ALIGN * DEV_ALLOC_ALIGN;
   void *spare[DEV_EXPORT_TRIES * 4];
   int nspare = 0, retries = 0;
+  char first[160] = "";
   for (uint64_t i = 0; i < n; i++) {
     ipc_handle_t h;
     const char *what = "hipMalloc";
@@ -149,6 +165,14 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
       if ((rc = hip.malloc_(&blk[i], alloc)) == 0 && (what = "hipMemset", rc = hip.memset_(blk[i], 0, alloc)) == 0 &&
           (what = "hipIpcGetMemHandle", rc = hip.get_handle(&h, blk[i])) == 0)
         break;
+      if (!first[0]) {
+        void *base = NULL;
+        size_t size = 0;
+        const int ar = blk[i] && hip.addr_range ? hip.addr_range(&base, &size, blk[i]) : -1;
+        snprintf(first, sizeof first, "%s: %s (%d) on block %llu of %llu B, range %s%+lld %llu B", what,
+                 hip.err_str(rc), rc, (unsigned long long)i, (unsigned long long)alloc, ar == 0 ? "base" : "?",
+                 ar == 0 ? (long long)((char *)blk[i] - (char *)base) : 0LL, (unsigned long long)size);
+      }
       if (t + 1 >= DEV_EXPORT_TRIES || !blk[i] || nspare == (int)(sizeof spare / sizeof spare[0])) {
         char w[160];
         snprintf(w, sizeof w, "%s (block %llu of %llu, %llu B, try %d)", what, (unsigned long long)i,
@@ -170,9 +194,9 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
   hip.sync();
   seg0->holder_pid = (int32_t)getpid();
   __atomic_store_n(&seg0->holder_state, 1, __ATOMIC_RELEASE);
-  char ready[24];
-  const int nr = snprintf(ready, sizeof ready, "R%d", retries); /* 'R' + export retries */
-  (void)!write(wfd, ready, (size_t)nr);
+  char ready[200];
+  const int nr = snprintf(ready, sizeof ready, "R%d %s", retries, first); /* 'R' + export retries */
+  (void)!write(wfd, ready, (size_t)nr < sizeof ready ? (size_t)nr : sizeof ready - 1);
   close(wfd);
 
   sigset_t set;
@@ -183,13 +207,20 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
   const char *idle_env = getenv("DADA_HOLDER_IDLE_S");
   const long idle_max = idle_env ? atol(idle_env) : 0;
   long idle = 0;
+  int stopping = 0;
   for (;;) {
-    struct timespec one = {1, 0};
-    if (sigtimedwait(&set, NULL, &one) > 0) break;
+    /* 1-s ticks while serving; 10-ms ticks while draining the importers */
+    struct timespec tick = {stopping ? 0 : 1, stopping ? 10 * 1000 * 1000 : 0};
+    if (sigtimedwait(&set, NULL, &tick) > 0) stopping = 1;
     struct shmid_ds ds;
-    if (shmctl(id->syncid, IPC_STAT, &ds) < 0 || (ds.shm_perm.mode & SHM_DEST)) break;
-    idle = ds.shm_nattch <= 1 ? idle + 1 : 0;
-    if (idle_max > 0 && idle >= idle_max) break;
+    if (shmctl(id->syncid, IPC_STAT, &ds) < 0 || (ds.shm_perm.mode & SHM_DEST)) stopping = 1; /* ring removed */
+    const long others = importers_attached(seg0_id, seg0);
+    __atomic_store_n(&seg0->importers, (int32_t)others, __ATOMIC_RELEASE);
+    if (!stopping) {
+      idle = others == 0 ? idle + 1 : 0;
+      if (idle_max > 0 && idle >= idle_max) stopping = 1;
+    }
+    if (stopping && others == 0) break;
   }
   for (uint64_t i = 0; i < n; i++) hip.free_(blk[i]);
   __atomic_store_n(&seg0->holder_state, 2, __ATOMIC_RELEASE);
@@ -239,9 +270,12 @@ int dev_create_blocks(ipcbuf_t *id, int device) {
   } while (got < 0 && errno == EINTR);
   close(fds[0]);
   if (got >= 1 && msg[0] == 'R') {
-    if (got > 1 && atoi(msg + 1) > 0)
-      fprintf(stderr, "dada device ring: %d IPC export retr%s in the holder\n", atoi(msg + 1),
-              atoi(msg + 1) == 1 ? "y" : "ies");
+    const int retries = atoi(msg + 1);
+    if (retries > 0) {
+      const char *why = strchr(msg, ' ');
+      fprintf(stderr, "dada device ring: %d IPC export retr%s in the holder (first: %s)\n", retries,
+              retries == 1 ? "y" : "ies", why ? why + 1 : "?");
+    }
     return 0;
   }
   fprintf(stderr, "dada device ring: holder failed: %s\n", got > 1 ? msg + 1 : "no reply");
@@ -251,13 +285,31 @@ int dev_create_blocks(ipcbuf_t *id, int device) {
 
 int dev_stop_holder(dev_seg_t *seg0) {
   if (seg0->holder_pid <= 0 || __atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) != 1) return 0;
-  if (kill(seg0->holder_pid, SIGTERM) < 0) return errno == ESRCH ? 0 : -1;
-  for (int i = 0; i < 1000; i++) { /* <= 10 s for the holder to free its memory */
-    if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) == 2) return 0;
-    struct timespec t = {0, 10 * 1000 * 1000};
-    nanosleep(&t, NULL);
+  /* this process stays attached to block 0's segment only to watch the
+   * holder's state: it says so, so the holder does not wait for it */
+  __atomic_add_fetch(&seg0->stop_waiters, 1, __ATOMIC_ACQ_REL);
+  int rc = 0;
+  if (kill(seg0->holder_pid, SIGTERM) < 0) {
+    rc = errno == ESRCH ? 0 : -1;
+  } else {
+    rc = -1;
+    for (int i = 0; i < 1000; i++) { /* <= 10 s for the holder to free the blocks */
+      if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) == 2) {
+        rc = 0;
+        break;
+      }
+      struct timespec t = {0, 10 * 1000 * 1000};
+      nanosleep(&t, NULL);
+    }
+    if (rc) {
+      snprintf(dev_err, sizeof dev_err,
+               "device ring holder %d: %d process(es) still have the blocks open; it frees them when they detach",
+               seg0->holder_pid, __atomic_load_n(&seg0->importers, __ATOMIC_ACQUIRE));
+      errno = EBUSY;
+    }
   }
-  return -1;
+  __atomic_sub_fetch(&seg0->stop_waiters, 1, __ATOMIC_ACQ_REL);
+  return rc;
 }
 
 int dev_open_blocks(ipcbuf_t *id) {
@@ -304,7 +356,12 @@ void dev_close_blocks(ipcbuf_t *id) {
   if (hip_load() < 0) return;
   for (uint64_t i = 0; i < id->sync->nbufs; i++)
     if (id->buffer[i]) {
-      hip.close_handle(id->buffer[i]);
+      const int rc = hip.close_handle(id->buffer[i]);
+      if (rc != 0) { /* kept for dada_device_error(); the block is dropped either way */
+        char w[80];
+        snprintf(w, sizeof w, "hipIpcCloseMemHandle (block %llu)", (unsigned long long)i);
+        dev_fail(w, rc);
+      }
       id->buffer[i] = NULL;
     }
 }

@@ -85,16 +85,29 @@ static inline size_t sync_size(uint64_t nbufs) { return sizeof(ipcsync_t) + 5 * 
 
 /* a device ring's block segment: the 64-B HIP IPC handle PSRDADA's layout
  * reserves for it; block 0's segment carries the holder process after it
- * (a libpafdada extension: the segment is larger, the handle unchanged) */
+ * (a libpafdada extension: the segment is larger, the handle unchanged).
+ *
+ * Ordering rule of a device ring (dada_device.c): every process that opened
+ * the blocks' IPC handles stays attached to block 0's segment until it has
+ * closed them (free_local: dev_close_blocks, then shmdt), and the holder
+ * frees the blocks only once no such process is attached -- counted by the
+ * kernel as shm_nattch of block 0's segment, less the holder itself and the
+ * destroyers waiting for it (stop_waiters).  A killed importer detaches
+ * when it dies, so the count needs no cooperation to come down. */
 #define DEV_HANDLE_BYTES 64
 typedef struct {
   unsigned char handle[DEV_HANDLE_BYTES];
   int32_t holder_pid;
   int32_t holder_state; /* 0 starting, 1 serving, 2 gone */
+  int32_t stop_waiters; /* destroyers attached here only to wait for the holder */
+  int32_t importers;    /* last count the holder saw (diagnostics) */
 } dev_seg_t;
 
 /* dada_device.c: HIP reached through dlopen, so libpafdada loads without ROCm */
 int dev_create_blocks(ipcbuf_t *id, int device); /* fork the holder, fill the handles */
+/* stop the holder and wait (<= 10 s) until it has freed the blocks; -1 with
+ * errno EBUSY (text in dada_device_error) while importers stay attached --
+ * the holder then frees the blocks when the last one detaches */
 int dev_stop_holder(dev_seg_t *seg0);
 int dev_open_blocks(ipcbuf_t *id);
 void dev_close_blocks(ipcbuf_t *id);

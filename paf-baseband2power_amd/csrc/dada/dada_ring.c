@@ -256,7 +256,11 @@ static void free_local(ipcbuf_t *id) {
 /* remove every segment and semaphore set a (possibly half-built) ring has */
 static void remove_ipc(ipcbuf_t *id) {
   ipcsync_t *s = id->sync;
-  if (s->on_device_id >= 0 && id->shm_addr && id->shm_addr[0]) dev_stop_holder(id->shm_addr[0]);
+  if (s->on_device_id >= 0 && id->shm_addr && id->shm_addr[0]) {
+    /* this process's own handles first (the ordering rule, dada_internal.h) */
+    if (id->buffer) dev_close_blocks(id);
+    dev_stop_holder(id->shm_addr[0]);
+  }
   for (uint64_t i = 0; id->shmid && i < s->nbufs; i++)
     if (id->shmid[i] >= 0) shmctl(id->shmid[i], IPC_RMID, NULL);
   for (unsigned r = 0; id->semid_data && r < s->n_readers; r++)
@@ -1347,7 +1351,10 @@ static int ring_remove(key_t key) {
 }
 
 int dada_db_destroy(key_t key) {
-  const int a = ring_remove(key), b = ring_remove(key + 1);
+  const int a = ring_remove(key);
+  const int e = errno; /* EBUSY: the data ring's holder still serves importers */
+  const int b = ring_remove(key + 1);
+  if (a != 0) errno = e;
   return a == 0 && b == 0 ? 0 : -1;
 }
 

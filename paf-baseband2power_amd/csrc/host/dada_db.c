@@ -11,6 +11,7 @@
  */
 #include <getopt.h>
 #include <inttypes.h>
+#include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -42,7 +43,10 @@ int main(int argc, char **argv) {
   }
   if (destroy) {
     if (dada_db_destroy(key) < 0) {
-      fprintf(stderr, "dada_db: nothing (complete) to destroy at key %x\n", (unsigned)key);
+      if (errno == EBUSY) /* a device ring's holder still serves attached processes */
+        fprintf(stderr, "dada_db: ring %x removed, %s\n", (unsigned)key, dada_device_error());
+      else
+        fprintf(stderr, "dada_db: nothing (complete) to destroy at key %x\n", (unsigned)key);
       return EXIT_FAILURE;
     }
     return EXIT_SUCCESS;

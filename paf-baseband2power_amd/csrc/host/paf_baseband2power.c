@@ -119,7 +119,8 @@ static void usage(void) {
           " -n  Number of sub-bands (rings key_in + 0x10*r, GPUs d + r), gathered to GPU d\n"
           " -t  Split each integration of the one input ring by time over N GPUs (d + r);\n"
           "     exact partial sums are reduced on GPU d (host ring: N PCIe links in parallel)\n"
-          " -G  Transport for -n / -t: rccl | copy (default: RCCL unless members share a GPU)\n"
+          " -G  Transport for -n / -t: rccl | copy (default: RCCL unless members share a GPU);\n"
+          "     -n 1 -G rccl gathers the one sub-band through a one-member RCCL group\n"
           " -T  Time limit in s for the RCCL set-up and each collective (default 60); past it\n"
           "     the communicators are aborted and the stage exits with an error\n"
           " -S  GPU-resident rings: one block per launch, each waited for before the next\n"
@@ -328,6 +329,9 @@ typedef struct shared_t {
   char *blk;
   uint64_t blk_bytes, share_bytes, nsamp_full;
   uint64_t *root_sum; /* on member 0's device */
+  /* spectra go through the group's gather (-n N > 1, or -n 1 -G rccl: one
+   * RCCL member, the collective path exercised on one GPU) */
+  int grouped;
 } shared_t;
 
 typedef struct worker_t {
@@ -384,8 +388,8 @@ static void *worker(void *arg) {
     if (s->ondev) {
       /* the block is already in HBM: one integrate launch reads it in place;
        * it must be done with the block before the block goes back to the ring */
-      rc = b2p_integrate(s->ctx, blk, bytes, 1, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
-                         sh->nsub == 1 ? 0 : 1);
+      rc = b2p_integrate(s->ctx, blk, bytes, 1, !sh->grouped ? sh->spec_host : s->spec_dev,
+                         !sh->grouped ? 0 : 1);
       if (rc == B2P_OK) rc = b2p_sync(s->ctx);
       ipcio_close_block_read(s->in->data_block, bytes);
     } else {
@@ -393,9 +397,9 @@ static void *worker(void *arg) {
       rc = b2p_push(s->ctx, blk, bytes, 0); /* returns once the block is copied */
       t_copied = now_s();
       ipcio_close_block_read(s->in->data_block, bytes);
-      if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, sh->nsub == 1 ? sh->spec_host : s->spec_dev,
-                                              sh->nsub == 1 ? 0 : 1);
-      if (rc == B2P_OK && sh->nsub == 1) rc = b2p_sync(s->ctx);
+      if (rc == B2P_OK) rc = b2p_finish_async(s->ctx, !sh->grouped ? sh->spec_host : s->spec_dev,
+                                              !sh->grouped ? 0 : 1);
+      if (rc == B2P_OK && !sh->grouped) rc = b2p_sync(s->ctx);
     }
     if (rc != B2P_OK)
       multilog(sh->log, LOG_ERR, "sub-band %d: %s (%s)", w->r, b2p_strerror(rc), b2p_last_error(s->ctx));
@@ -405,7 +409,7 @@ static void *worker(void *arg) {
       for (int r = 0; r < sh->nsub; r++)
         if (sh->mfail[r]) sh->failed = 1;
     if (w->r == 0 && !sh->failed) {
-      if (sh->nsub > 1) {
+      if (sh->grouped) {
         float *specs[MAX_SUB];
         for (int r = 0; r < sh->nsub; r++) specs[r] = sh->sub[r].spec_dev;
         rc = b2p_group_gather(sh->grp, specs, sh->root_dev);
@@ -979,6 +983,7 @@ int main(int argc, char *argv[]) {
   const int split = conf.nsplit > 1;
   const int nmem = split ? conf.nsplit : conf.nsub;
   sh.nsub = nmem;
+  sh.grouped = !split && (conf.nsub > 1 || conf.gather == 1);
   for (int r = 0; r < nmem; r++) {
     sub_t *s = &sub[r];
     s->r = r;
@@ -1122,7 +1127,7 @@ int main(int argc, char *argv[]) {
 
   sh.bmax = 1;
 #if DEVICE_RINGS
-  if (!split && conf.nsub > 1 && !conf.sync) { /* gathered batches (worker_gather_dev) */
+  if (sh.grouped && !conf.sync) { /* gathered batches (worker_gather_dev) */
     int all_dev = 1;
     uint64_t nb = UINT64_MAX;
     for (int r = 0; r < conf.nsub; r++) {
@@ -1166,7 +1171,7 @@ int main(int argc, char *argv[]) {
     }
     multilog(log, LOG_INFO, "reduce of %d time shares to GPU %d via %s", nmem, sub[0].device,
              mode ? "peer copies (shared device)" : "RCCL ncclReduce");
-  } else if (conf.nsub > 1) {
+  } else if (sh.grouped) {
     for (int r = 0; r < conf.nsub; r++)
       if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, 3 * sh.bmax * info.nout * sizeof(float)) != B2P_OK)
         goto done;
@@ -1188,7 +1193,7 @@ int main(int argc, char *argv[]) {
 
   {
 #if DEVICE_RINGS
-    if (!split && nmem == 1 && sub[0].ondev && !conf.sync) {
+    if (!split && nmem == 1 && !sh.grouped && sub[0].ondev && !conf.sync) {
       multilog(log, LOG_INFO, "GPU-resident input: two launches in flight, queued blocks integrated "
                "together (up to %d per launch)", B2P_MAX_BLOCKS);
       run_device_pipelined(&sh);

@@ -27,8 +27,9 @@
  *     block is zeroed first unless -Z (the reference leaves lost frames'
  *     slots stale).
  *
- *   paf_dfdb -a key -b header_file -R nblocks [-f layout] [-r seed] [-d device]
- *     Replay: fill each ring block once with the synthetic generator, then
+ *   paf_dfdb -a key -b header_file -R nblocks [-f layout] [-r seed] [-u subband] [-d device]
+ *     Replay: fill each ring block once with the synthetic generator (block
+ *     i of sub-band `subband`, the stream bench.py and the tests regenerate), then
  *     hand the ring's blocks out nblocks times without rewriting them -- a
  *     consumer-side throughput test of a GPU-resident ring (or, for
  *     comparison, of a host ring, whose consumer copies each block H2D).  layout:
@@ -110,8 +111,9 @@ int main(int argc, char **argv) {
   key_t key = 0;
   const char *hfile = NULL, *dfile = NULL, *cfile = NULL, *layout = "bmf", *logdir = NULL;
   uint64_t ref_idf = 0, ref_sec = 0, seed = 20181105, replay = 0;
+  uint32_t subband = 0;
   int nchunk = 48, device = 0, nozero = 0, arg, have_key = 0;
-  while ((arg = getopt(argc, argv, "a:b:c:k:n:x:s:d:ZR:f:r:e:h")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:k:n:x:s:d:ZR:f:r:u:e:h")) != -1) {
     switch (arg) {
       case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
       case 'b': hfile = optarg; break;
@@ -125,12 +127,14 @@ int main(int argc, char **argv) {
       case 'R': replay = strtoull(optarg, NULL, 10); break;
       case 'f': layout = optarg; break;
       case 'r': seed = strtoull(optarg, NULL, 10); break;
+      case 'u': subband = (uint32_t)strtoul(optarg, NULL, 10); break;
       case 'e': logdir = optarg; break;
       default:
         fprintf(stdout,
                 "paf_dfdb -a key -b header -c frames.df -k chunks.u8 [-n nchunk] [-x ref_idf] "
                 "[-s ref_sec] [-d dev] [-Z]\n"
-                "paf_dfdb -a key -b header -R nblocks [-f bmf|int8:N|int16:N[:be]] [-r seed] [-d dev]\n");
+                "paf_dfdb -a key -b header -R nblocks [-f bmf|int8:N|int16:N[:be]] [-r seed] [-u subband] "
+                "[-d dev]\n");
         return EXIT_FAILURE;
     }
   }
@@ -208,7 +212,7 @@ int main(int argc, char **argv) {
       char *blk = ipcio_open_block_write(hdu->data_block, &bid);
       if (!blk) goto done;
       if (i < nbufs) { /* first pass: synthetic block i, then re-used as is */
-        if (b2p_fill_synthetic(ctx, ondev ? (void *)blk : stage, bufsz, seed, 0, i, 0) != B2P_OK ||
+        if (b2p_fill_synthetic(ctx, ondev ? (void *)blk : stage, bufsz, seed, subband, i, 0) != B2P_OK ||
             b2p_sync(ctx) != B2P_OK || (!ondev && b2p_memcpy(ctx, blk, stage, bufsz, 2) != B2P_OK)) {
           multilog(log, LOG_ERR, "fill: %s", b2p_last_error(ctx));
           goto done;

@@ -143,8 +143,11 @@ PROTOTYPES = {
     "b2p_group_close": (C.c_int, [_P]),
 }
 
-# the test build's extra entry (lib/hooks/libpafb2p.so, -DB2P_TEST_HOOKS)
-HOOK_PROTOTYPES = {"b2p_test_inject_push_fail": (C.c_int, [_P, C.c_long])}
+# the test builds' extra entries (lib/hooks/libpafb2p.so, -DB2P_TEST_HOOKS;
+# lib/debug/libpafb2p.so, -DB2P_DEBUG -DB2P_TEST_HOOKS)
+HOOK_PROTOTYPES = {"b2p_test_inject_push_fail": (C.c_int, [_P, C.c_long]),
+                   "b2p_test_debug_shrink_bound": (C.c_int, [_P, C.c_long]),
+                   "b2p_debug_build": (C.c_int, [])}
 
 _lib = None
 

@@ -38,6 +38,7 @@ class Integrator:
         g = geom if isinstance(geom, L.Geom) else make_geom(**(geom or {}), **geom_kw)
         self.geom = g
         self._ctx = C.c_void_p()
+        self._registered: dict[int, np.ndarray] = {}  # base -> the array, kept alive while registered
         lib = L.lib()
         if tuning:
             t = L.Tuning.make(**tuning)
@@ -54,8 +55,9 @@ class Integrator:
     # ---- lifecycle ---------------------------------------------------------
     def close(self) -> None:
         if self._ctx:
-            L.check(L.lib().b2p_close(self._ctx))
+            L.check(L.lib().b2p_close(self._ctx))  # also releases what it registered
             self._ctx = C.c_void_p()
+        self._registered.clear()
 
     def __enter__(self):
         return self
@@ -157,11 +159,17 @@ class Integrator:
 
     # ---- host memory -----------------------------------------------------------
     def register_host(self, arr: np.ndarray) -> None:
+        """Pin ``arr`` for full-rate copies (b2p_register_host).  The array is
+        kept alive until unregister_host or close: memory must never be
+        freed while it is registered, or HIP would go on copying from the
+        stale pinned pages of its address."""
         L.check(L.lib().b2p_register_host(self._ctx, C.c_void_p(arr.ctypes.data), arr.nbytes),
                 self._ctx)
+        self._registered[arr.ctypes.data] = arr
 
     def unregister_host(self, arr: np.ndarray) -> None:
         L.check(L.lib().b2p_unregister_host(self._ctx, C.c_void_p(arr.ctypes.data)), self._ctx)
+        self._registered.pop(arr.ctypes.data, None)
 
     # ---- device buffers / synthetic data ----------------------------------------
     def alloc(self, nbytes: int) -> DeviceBuffer:

@@ -144,8 +144,13 @@ def test_release_library_has_no_test_hook():
     und = subprocess.run(["nm", "-D", "--undefined-only", L.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
     assert not re.search(r"\bgetenv\b", und)
+    assert not hasattr(lib, "b2p_debug_build") and not hasattr(lib, "b2p_test_debug_shrink_bound")
     hooks = os.path.join(os.path.dirname(L.LIB_PATH), "hooks", "libpafb2p.so")
     assert hasattr(C.CDLL(hooks), "b2p_test_inject_push_fail")
+    debug = C.CDLL(os.path.join(os.path.dirname(L.LIB_PATH), "debug", "libpafb2p.so"))
+    for name in ("b2p_debug_build", "b2p_test_debug_shrink_bound", "b2p_test_inject_push_fail"):
+        assert hasattr(debug, name), name
+    assert debug.b2p_debug_build() == 1
 
 
 def test_tuning_defaults_and_refusals():

@@ -16,6 +16,7 @@ a holder process (dada_db -g) and shared through HIP IPC handles.
 import os
 import re
 import subprocess
+import sys
 import time
 
 import numpy as np
@@ -23,6 +24,7 @@ import pytest
 
 import b2p_oracle as npo
 import oracle_c as co
+from conftest import REPO
 from paf_b2p import dada, pipeline
 
 pytestmark = pytest.mark.gpu
@@ -464,3 +466,60 @@ def test_real_time_spectra_do_not_wait_for_the_next_block(gpu, tmp_path, nsub):
             proc.wait()
         for k in kins + [kout]:
             dada.destroy_ring(k)
+
+
+def _holder_pids(key):
+    """pids of this ring's holder: the forked `dada_db -k KEY ... -g` process"""
+    pids = []
+    for d in os.listdir("/proc"):
+        if d.isdigit():
+            try:
+                args = open(f"/proc/{d}/cmdline", "rb").read().split(b"\0")
+            except OSError:
+                continue
+            if args and args[0].endswith(b"dada_db") and f"{key:x}".encode() in args and b"-g" in args:
+                pids.append(int(d))
+    return pids
+
+
+def test_holder_frees_blocks_only_after_importers_detach(gpu):
+    """the ordering rule of a device ring (dada_internal.h): while a process
+    still has the blocks' IPC handles open, destroying the ring does not
+    free them -- dada_db_destroy reports the attached importer (EBUSY, text
+    in dada_device_error) and the holder keeps the memory; the moment the
+    importer detaches, the holder frees the blocks and exits.  An importer
+    that is killed counts as detached (the kernel drops its attachment)."""
+    key = fresh_key()
+    dada.create_ring(key, 2, 1 << 16, device=0)
+    assert len(_holder_pids(key)) == 1
+    v = dada.Hdu(key, "r")  # a viewer: connected, every block's handle imported
+    try:
+        t0 = time.time()
+        assert not dada.destroy_ring(key)
+        assert time.time() - t0 > 5  # it waited for the holder first
+        assert "still have the blocks open" in dada.device_error(), dada.device_error()
+        assert len(_holder_pids(key)) == 1  # memory still held for the importer
+    finally:
+        v.close()
+    t_end = time.time() + 10
+    while _holder_pids(key) and time.time() < t_end:
+        time.sleep(0.05)
+    assert not _holder_pids(key), "holder did not exit once the importer detached"
+    # a killed importer: a child process attaches and is killed
+    dada.create_ring(key, 2, 1 << 16, device=0)
+    code = ("import sys, time; sys.path.insert(0, %r); from paf_b2p import dada; "
+            "h = dada.Hdu(%d, 'r'); print('attached', flush=True); time.sleep(60)") % (
+        os.path.join(REPO, "paf-baseband2power_amd"), key)
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    try:
+        assert child.stdout.readline().strip() == "attached"
+        child.kill()
+        child.wait()
+        t0 = time.time()
+        assert dada.destroy_ring(key), dada.device_error()
+        assert time.time() - t0 < 5
+    finally:
+        if child.poll() is None:
+            child.kill()
+            child.wait()
+    assert not _holder_pids(key)

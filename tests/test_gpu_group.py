@@ -149,6 +149,60 @@ def test_c_host_reports_rccl_setup_failure(gpu, tmp_path):
     assert "b2p_group_open" in log and "member 1: GPU 0 (PCI" in log
 
 
+@pytest.mark.parametrize("device", [False, True], ids=["host_ring", "device_ring"])
+def test_c_host_rccl_gather_at_world_size_one(gpu, tmp_path, device):
+    """`paf_baseband2power -n 1 -G rccl`: the C host's collective path with
+    one RCCL member -- ncclCommInitRankConfig (non-blocking, inside one group
+    call), then an ncclGather per integration (-S / host ring) or per round
+    of queued blocks (GPU-resident ring), polled against the -T limit
+    (csrc/b2p_group.hip, rccl.h:745) -- executed on the hardware, every
+    spectrum equal to the oracle's.  The one multi-rank step this box cannot
+    run is two RCCL members on distinct GPUs."""
+    import os
+    import subprocess
+    from test_gpu_device_ring import BIN, _wait, fresh_key
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 14)  # 16 MiB blocks
+    nblk = 3
+    blocks = [co.fill_synthetic(g, g.block_bytes, SEED, 0, b) for b in range(nblk)]
+    kin, kout = fresh_key(), fresh_key()
+    hdr = "HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\nTSAMP 0.84375\n"
+    (tmp_path / "hdr.txt").write_text(hdr)
+    dada.create_ring(kin, nblk + 1, g.block_bytes, device=0 if device else -1)
+    dada.create_ring(kout, 4, g.nout * 4)
+    out = tmp_path / "power.dada"
+    procs = []
+    try:
+        if device:  # the blocks and their end of data fit: the producer is done first
+            _wait([subprocess.Popen([os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b",
+                                     str(tmp_path / "hdr.txt"), "-R", str(nblk), "-f", "int8:256", "-r",
+                                     str(SEED), "-u", "0"], stderr=subprocess.PIPE)], timeout=120)
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b", f"{kout:x}",
+                                   "-c", str(tmp_path), "-d", "0", "-f", "int8:256", "-n", "1", "-G", "rccl",
+                                   "-T", "60"], stderr=subprocess.PIPE)]
+        if not device:
+            with dada.Hdu(kin, "W") as w:
+                w.write_header(hdr)
+                for b in blocks:
+                    w.write_block(b.tobytes())
+        _wait(procs, timeout=180)
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+    log = open(str(tmp_path / "paf_baseband2power.log")).read()
+    assert "gather of 1 sub-bands to GPU 0 via RCCL ncclGather" in log, log[-800:]
+    sp = data.view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == nblk, log[-800:]
+    for b in range(nblk):
+        assert np.array_equal(sp[b], co.power(g, blocks[b], nthreads=8).view(np.uint32)), b
+
+
 # ---- time-split mode (SURVEY.md 8e, second mode) -----------------------------
 
 @pytest.mark.parametrize("npol_out,mean", [(1, 0), (2, 1)])

@@ -5,6 +5,7 @@ random split of the integration into pushes, and checks the HIP result
 against the oracle bit for bit.  One Integrator per example, all in this
 one process (the GPU box allows few processes)."""
 import os
+import subprocess
 import sys
 
 import numpy as np
@@ -15,6 +16,9 @@ from hypothesis import strategies as st
 import b2p_oracle as npo
 import oracle_c as co
 import paf_b2p
+import staging_case
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -100,46 +104,51 @@ def test_random_layouts_multi_block(gpu, case, nblk):
 @settings(max_examples=30 * _SCALE, deadline=None, derandomize=_SEED is None,
           suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
                                  HealthCheck.function_scoped_fixture])
-@given(st.sampled_from([(8, 0, 1, 1024), (16, 0, 1, 512), (16, 1, 48, 7), (8, 0, 3, 100)]),
-       st.integers(1, 3), st.integers(2, 24), st.lists(st.floats(0.0, 1.0), max_size=4), st.booleans(),
-       st.integers(0, 2 ** 31))
+@given(st.sampled_from(staging_case.LAYOUTS), st.integers(1, 3), st.integers(2, 24),
+       st.lists(st.floats(0.0, 1.0), max_size=4), st.booleans(), st.integers(0, 2 ** 31))
 def test_host_spans_through_small_staging(gpu, layout, stage_mib, mib, cut_fracs, register, s):
     """host-memory pushes go through two staging buffers of stage_mib MiB,
     chunk k copied while chunk k-1 is integrated: random staging sizes
     (1-3 MiB), integrations of 2-24 MiB cut into random pushes (so a push
     spans several chunks and ends on a partial one), registered or plain
-    host memory -- the spectrum equals the oracle's bit for bit.
+    host memory -- the spectrum equals the oracle's bit for bit
+    (tests/staging_case.py run_case).
 
-    The first hunt of this test ended in one "illegal memory access" after
-    about 40 examples; 12 480 later examples (three reseeded, traced hunts)
-    and 32 cases run one per process did not show it again (DESIGN.md,
-    round 4).  B2P_TRACE_EXAMPLES=1 prints each example before it runs, so a
-    recurrence names the example that preceded it."""
-    nbit, be, nchunk, ncc = layout
+    Round 4's first hunt of this test ended in one "illegal memory access".
+    Round 5 traced the lifetime of the host memory a copy reads (DESIGN.md
+    section 1, "Host memory"): the library now drains a failed push's copies
+    before it returns, drains its streams before an unregister, refuses
+    overlapping registrations and releases at close what a context
+    registered, and the Python wrapper keeps a registered array alive.  The
+    same property also runs under the debug library, where every span load
+    and staging chunk is bounds-checked (test_host_staging_under_debug_build).
+    B2P_TRACE_EXAMPLES=1 prints each example before it runs."""
     if os.environ.get("B2P_TRACE_EXAMPLES"):
         print("staging example", layout, stage_mib, mib, cut_fracs, register, s, file=sys.stderr, flush=True)
-    word = 4 * nbit // 8
-    nsamp_df = 1
-    while (nsamp_df * ncc * word) % 16:
-        nsamp_df *= 2
-    if (nbit, be, nchunk, ncc) == (16, 1, 48, 7):
-        nsamp_df = 128
-    frame = nchunk * nsamp_df * ncc * word
-    nframes = max(1, (mib << 20) // frame)
-    g = npo.Geom(nbit=nbit, big_endian=be, nchunk=nchunk, nsamp_df=nsamp_df, nchan_chunk=ncc,
-                 nsamp_int=nframes * nsamp_df)
-    buf = co.fill_synthetic(g, g.block_bytes, s, 2, 8)
-    cuts = sorted({int(f * nframes) for f in cut_fracs} - {0, nframes})
-    bounds = [0] + [c * g.frame_bytes for c in cuts] + [g.block_bytes]
-    with paf_b2p.Integrator(paf_b2p.make_geom(**g.asdict()), tuning={"stage_mib": stage_mib}) as it:
-        if register:
-            it.register_host(buf)
-        try:
-            for a, b in zip(bounds[:-1], bounds[1:]):
-                it.push(buf[a:b])
-            out = it.finish()
-        finally:  # never leave freed memory registered for the next example
-            if register:
-                it.unregister_host(buf)
-    assert np.array_equal(out.view(np.uint32), co.power(g, buf, nthreads=8).view(np.uint32)), \
-        (layout, stage_mib, mib, cuts, register)
+    staging_case.run_case(layout, stage_mib, mib, cut_fracs, register, s)
+
+
+def test_host_staging_under_debug_build(gpu):
+    """the host-staging property (60 examples) with the DEBUG library
+    (lib/debug/libpafb2p.so, -DB2P_DEBUG) in a child process: every span
+    load of every launch checked against its span, every output slot against
+    nout, every staging chunk against the staging size, the span and its
+    host registration -- any out-of-bounds access fails the run with its
+    index, workgroup and lane instead of being made"""
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tests", "debug_build_checks.py"), "staging",
+                        "60"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "staging under debug build: 60 examples ok" in r.stdout
+
+
+def test_debug_build_checks(gpu):
+    """the debug library's own checks (tests/debug_build_checks.py): a clean
+    run of every launch-shape branch reports nothing; a lowered load bound
+    is reported with the first offending index and the context fails; a
+    push that fails part-way from registered memory, unregistered and freed
+    at once, leaves the GPU healthy (its copies were drained); close releases
+    a registration the caller left behind"""
+    r = subprocess.run([sys.executable, "-u", os.path.join(REPO, "tests", "debug_build_checks.py"), "checks"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "debug build checks: ok" in r.stdout

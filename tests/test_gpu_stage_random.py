@@ -26,6 +26,10 @@ from test_gpu_device_ring import BIN, _wait, fresh_key
 pytestmark = pytest.mark.gpu
 _SCALE = int(os.environ.get("B2P_HYPOTHESIS_SCALE", "1"))
 _SEED = os.environ.get("B2P_HYPOTHESIS_SEED")
+# B2P_STAGE_WRITER=inproc: every GPU-resident ring is written from THIS
+# process (hipIpcOpenMemHandle + hipMemcpy into the imported blocks), as in
+# round 4's seed-9090 hunt, instead of from paf_diskdb processes
+_INPROC = os.environ.get("B2P_STAGE_WRITER") == "inproc"
 
 
 @st.composite
@@ -89,7 +93,7 @@ def test_stage_random_layouts_rings_and_flags(gpu, tmp_path_factory, case):
                                    "-c", str(tmp), "-d", "0", "-f", "header", "-p", str(g.npol_out)]
                                   + (["-m"] if g.mean else []) + (["-S"] if case["sync"] else []),
                                   stderr=subprocess.PIPE)]
-        if case["device"]:  # end of data part-way through an integration: a short tail
+        if case["device"] and not _INPROC:  # end of data part-way through an integration: a short tail
             procs.append(_diskdb_writer(tmp, kin, hdr, blocks, g.frame_bytes if case["short"] else None))
         else:
             with dada.Hdu(kin, "W") as w:
@@ -119,11 +123,13 @@ def test_stage_random_layouts_rings_and_flags(gpu, tmp_path_factory, case):
     assert ("partial integration skipped" in log) == case["short"], log[-600:]
 
 
-def _run_stage(tmp, g, keys, rings_blocks, stage_args, device, nbufs, out_nsub, short=()):
+def _run_stage(tmp, g, keys, rings_blocks, stage_args, device, nbufs, out_nsub, short=(), inproc=False):
     """create one input ring per key, start paf_dbdisk and the stage, write
-    each ring's blocks from its own thread (the stage reads every ring each
-    round), and return (output header, spectra [n, out_nsub, nout] as uint32,
-    stage log)"""
+    each ring's blocks (host rings: from a thread of this process each;
+    GPU-resident rings: from a paf_diskdb process each, or with inproc from
+    a thread of this process each, through the imported IPC handles), and
+    return (output header, spectra [n, out_nsub, nout] as uint32, stage
+    log)"""
     import threading
     hdr = (f"HDR_SIZE 4096\nNBIT {g.nbit}\nNDIM 2\nNPOL 2\nNCHAN {g.nchunk * g.nchan_chunk}\n"
            f"NCHUNK {g.nchunk}\nNCHAN_CHUNK {g.nchan_chunk}\nNSAMP_DF {g.nsamp_df}\n"
@@ -152,11 +158,12 @@ def _run_stage(tmp, g, keys, rings_blocks, stage_args, device, nbufs, out_nsub, 
                         w.write_block(blocks[0][: g.frame_bytes].tobytes())
             except Exception as e:  # noqa: BLE001 -- reported below
                 errs.append(e)
-        if device:  # GPU-resident rings: one paf_diskdb process per ring
+        inproc = inproc or _INPROC
+        if device and not inproc:  # GPU-resident rings: one paf_diskdb process per ring
             procs += [_diskdb_writer(tmp, k, hdr, bl, g.frame_bytes if k in short else None)
                       for k, bl in zip(keys, rings_blocks)]
-        ths = [] if device else [threading.Thread(target=writer, args=(k, bl, k in short))
-                                 for k, bl in zip(keys, rings_blocks)]
+        ths = [] if device and not inproc else [threading.Thread(target=writer, args=(k, bl, k in short))
+                                                for k, bl in zip(keys, rings_blocks)]
         for t in ths:
             t.start()
         for t in ths:
@@ -195,6 +202,37 @@ def test_stage_random_gathered_subbands(gpu, tmp_path_factory, case, nsub, short
     # writer of a longer transfer must not wait on a reader that has left
     nbufs = case["nbufs"] if len(set(nblks)) == 1 else max(case["nbufs"], max(nblks) + 1)
     ohdr, sp, log = _run_stage(tmp, g, keys, blocks, args, case["device"], nbufs, nsub)
+    n = min(nblks)
+    assert sp.shape[0] == n, (case, nblks, log[-600:])
+    for b in range(n):
+        for r in range(nsub):
+            assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=8).view(np.uint32)), (case, b, r)
+    assert dada.header_get(ohdr, "NSUBBAND", "%d") == nsub
+
+
+@(seed(int(_SEED)) if _SEED else (lambda f: f))
+@settings(max_examples=10 * _SCALE, deadline=None, derandomize=_SEED is None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(cases(), st.integers(2, 3), st.lists(st.integers(0, 2), min_size=3, max_size=3))
+def test_stage_random_gathered_subbands_inproc_writers(gpu, tmp_path_factory, case, nsub, shorter):
+    """as test_stage_random_gathered_subbands, on GPU-resident rings only,
+    written by 2-3 threads of THIS long-lived process through the imported
+    IPC handles (dada.Hdu.write_block -> ipcbuf copy-in -> hipMemcpy into a
+    hipIpcOpenMemHandle block), concurrently with the stage reading them --
+    the pattern whose failures round 4 routed around.  Every ring is
+    destroyed after its example; the holder frees its blocks only once
+    every importer has detached (dada_internal.h, the ordering rule)"""
+    g = case["g"]
+    tmp = tmp_path_factory.mktemp("gather_inproc")
+    nblks = [max(1, case["nblk"] - shorter[r]) for r in range(nsub)]
+    base = fresh_key()
+    keys = [base + 0x10 * r for r in range(nsub)]
+    blocks = [[co.fill_synthetic(g, g.block_bytes, case["seed"], r, b) for b in range(nblks[r])]
+              for r in range(nsub)]
+    args = ["-n", str(nsub), "-p", str(g.npol_out)] + (["-m"] if g.mean else []) + (["-S"] if case["sync"] else [])
+    nbufs = case["nbufs"] if len(set(nblks)) == 1 else max(case["nbufs"], max(nblks) + 1)
+    ohdr, sp, log = _run_stage(tmp, g, keys, blocks, args, True, nbufs, nsub, inproc=True)
     n = min(nblks)
     assert sp.shape[0] == n, (case, nblks, log[-600:])
     for b in range(n):

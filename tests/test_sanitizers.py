@@ -185,3 +185,26 @@ def test_capture_receive_threads_under_tsan(tmp_path):
     n = os.path.getsize(df) // 7232
     assert re.search(rf"capture: {n} frames received \(0 not frames\)", err), err[-2000:]
     assert "3 receive thread(s) over 3 port(s)" in err
+
+
+def test_staging_and_addressing_model_under_asan(tmp_path):
+    """the library's own index arithmetic (csrc/b2p_plan.h: launch shape,
+    lane channels, row ownership, ragged row, staging chunks) compiled on
+    the CPU under ASan+UBSan and replayed over 300 random layouts, CU
+    counts, knobs, staging sizes and push cuts (tests/c/plan_model.cpp):
+    host spans and staging buffers are exact-size allocations, every load
+    is in bounds, every vector is read exactly once, every output slot is
+    < nout, and the sums equal the C oracle's"""
+    obj = tmp_path / "orc.o"
+    exe = tmp_path / "plan_model"
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"]
+    subprocess.run(["gcc", "-O1", "-g", *san, "-c", os.path.join(REPO, "oracle", "b2p_oracle.c"),
+                    "-I", os.path.join(REPO, "oracle"), "-o", str(obj)], check=True)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-Wall", "-Wextra", "-Wno-unknown-pragmas", *san,
+                    "-I", os.path.join(REPO, "oracle"), "-I", os.path.join(REPO, "paf-baseband2power_amd", "csrc"),
+                    os.path.join(REPO, "tests", "c", "plan_model.cpp"), str(obj), "-o", str(exe)], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([str(exe), "300", "20181105"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    assert "plan model: 300 cases ok" in r.stdout, r.stdout
