@@ -226,7 +226,7 @@ def parallelism_label(world: int, split: bool, dist_on: bool, rccl: bool) -> str
 # the sources that decide what the integrate kernel reads (its code and its
 # launch planner): a PMC summary measured on other sources is stale
 KERNEL_SOURCES = ("paf-baseband2power_amd/csrc/b2p_kernels.hip", "paf-baseband2power_amd/csrc/b2p_ctx.hip",
-                  "paf-baseband2power_amd/csrc/b2p_internal.h")
+                  "paf-baseband2power_amd/csrc/b2p_internal.h", "paf-baseband2power_amd/csrc/b2p_plan.h")
 
 
 def kernel_sources_sha() -> str:
@@ -283,14 +283,14 @@ def cpu_threads() -> int:
 
 def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
     """The tuned CPU port (oracle/b2p_cpu_port.c) timed in a child process
-    (its own OpenMP binding), at every CPU this job may use and at 1 thread,
-    with the scalar oracle beside it, on one full block; then,
-    when the host shows more logical CPUs than that, once more at all of
-    them (reported beside, as `all_cpus`: under a cgroup quota they only
-    time-slice the same CPUs)."""
+    (its own OpenMP binding), at the job's CPU quota less one thread
+    (cpu_baseline.baseline_threads: threads that fill the quota exactly get
+    throttled) with passive OpenMP waits, and at 1 thread, with the scalar
+    oracle beside it, on one full block.  The line reports the share of
+    throttled cgroup periods and the interquartile range beside `value`."""
     sys.path.insert(0, ORACLE)
     import cpu_baseline as cb
-    threads = cb.effective_cpus()
+    threads = cb.baseline_threads()
     picked = cb.pick_cpus(threads)
 
     def child(env, budget, *extra):
@@ -302,16 +302,13 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
             return None
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    res = child(cb.child_env(threads, cpus=picked["cpus"]), seconds)
+    res = child(cb.child_env(threads, cpus=picked["cpus"], wait="passive"), seconds)
     if res is not None:
-        res["cpus_picked"] = {**picked, "rule": "one logical CPU per physical core, dealt round-robin over "
-                                                "every L3 domain (CCD) of every NUMA node, the idlest allowed "
-                                                "core of each over the sample before the legs; CPU order, so "
-                                                "each thread's first-touched tile is on its own node"}
-    ncpu = os.cpu_count() or threads
-    if res is not None and ncpu > threads:
-        res["all_cpus"] = child(cb.child_env(ncpu, places="threads", wait="passive"),
-                                max(1.0, seconds * 0.15), "only")
+        res["cpus_picked"] = {**picked, "rule": "the cgroup quota less one thread, one logical CPU per "
+                                                "physical core, dealt round-robin over every L3 domain (CCD) "
+                                                "of every NUMA node, the idlest allowed core of each over the "
+                                                "sample before the legs; CPU order, so each thread's "
+                                                "first-touched tile is on its own node; passive OpenMP waits"}
     return res
 
 
@@ -710,6 +707,29 @@ def main(argv=None) -> int:
         if cs["launches"]:
             calib_us = cs["kernel_ms"] / cs["launches"] * 1e3
 
+    # configs[2]'s own ceiling: a bare pinned H2D stream of the same block,
+    # measured in this run after the headline (hipMemcpy from the same
+    # registered buffer into HBM, no kernel), so the line's PCIe fraction
+    # has its denominator beside it ("vs PCIe H2D ceiling and
+    # vs HBM")
+    h2d = None
+    if host_mode:
+        dst = it.alloc(bb)
+        it.upload_into(dst, blocks[0])  # untimed: first touch of the destination
+        rates = []
+        t_all = time.perf_counter()
+        while len(rates) < 3 or time.perf_counter() - t_all < 2.0:
+            t0 = time.perf_counter()
+            it.upload_into(dst, blocks[0])
+            rates.append(bb / (time.perf_counter() - t0) / 1e9)
+            if len(rates) >= 50:
+                break
+        dst.free()
+        h2d = {"gbs": round(statistics.median(rates), 2), "copies": len(rates),
+               "range": [round(min(rates), 2), round(max(rates), 2)],
+               "what": (f"hipMemcpy of the same {bb >> 20} MiB registered host block into HBM, no kernel, "
+                        "median of the copies, same process after the headline")}
+
     kern_avg_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
     bytes_per_launch = st["bytes"] / max(st["launches"], 1)
     achieved = bytes_per_launch / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
@@ -817,6 +837,27 @@ def main(argv=None) -> int:
             "provenance": {"kernel_sources_sha256": kernel_sources_sha(),
                            "kernel_sources": list(KERNEL_SOURCES)},
         }
+        if host_mode and h2d:
+            # PCIe-bound: the ceiling is the bare H2D stream measured above;
+            # the HBM fraction stays beside it as a secondary field
+            pcie_gbs = bb / (el_med / K) / 1e9
+            hbm = {k: res["roofline"][k] for k in ("achieved", "frac", "frac_of_value", "avg_launch_us",
+                                                     "launches_timed", "kernel")}
+            res["roofline"].update({
+                "bound": "pcie",
+                "achieved": round(pcie_gbs, 2),
+                "peak": h2d["gbs"],
+                "frac": round(pcie_gbs / h2d["gbs"], 4),
+                "frac_of_value": round(pcie_gbs / h2d["gbs"], 4),
+                "peak_source": h2d,
+                "traffic": None,
+                "traffic_source": "n/a: PCIe-bound (the kernel's HBM traffic is configs[4]'s, pmc_c5.json)",
+                "hbm": {**hbm, "frac_of_8tbs": round(pcie_gbs / HBM_PEAK_GBS, 4), "peak": HBM_PEAK_GBS,
+                        "note": "the block's bytes per ms_per_step against 8 TB/s (secondary)"},
+                "timing": ("achieved: the block's bytes per ms_per_step (the host-timed median region: "
+                           "pinned-host staging copies overlapped with the integrate launches); peak: "
+                           "peak_source, the bare H2D stream of the same bytes in the same run"),
+            })
         if world == 1 and a.cpu_seconds > 0 and not host_mode:
             res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)
         print(json.dumps(res), flush=True)

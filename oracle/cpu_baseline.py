@@ -9,7 +9,8 @@ a 1 GiB block does not fit).  SURVEY.md 8(d) "CPU baseline": the reference has
 no CPU path, so the baseline is the port, at 1 thread and at every CPU this
 process may use.  bench.py picks the CPUs (pick_cpus): one per physical core,
 dealt over every L3 domain (CCD) of both NUMA nodes, listed as explicit OpenMP
-places; every leg reports the cgroup's cpu.stat deltas (periods throttled, time throttled)
+places, one fewer than the cgroup quota grants and with passive OpenMP waits
+(baseline_threads: threads that fill the quota exactly are throttled); every leg reports the cgroup's cpu.stat deltas (periods throttled, time throttled)
 beside its median and interquartile range, so a slow box shows why.
 
 Run as a child process of bench.py (never imported into the GPU process), so
@@ -105,6 +106,19 @@ def effective_cpus() -> int:
     q = cgroup_cpus()
     if q is not None:
         n = min(n, max(1, int(q)))
+    return n
+
+
+def baseline_threads() -> int:
+    """threads of the timed CPU legs: every CPU the job may use, less one
+    under a cgroup quota.  The quota covers the whole job (the GPU process
+    that waits for this child, the HIP runtime's threads, this interpreter),
+    so threads that fill it exactly are throttled -- round 4's 16 threads in
+    a 16-CPU quota were throttled in 43 of 54 periods and their passes spread
+    8x; at quota - 1 with passive waits the job stays inside it."""
+    n = effective_cpus()
+    if cgroup_cpus() is not None:
+        n = min(n, max(1, int(cgroup_cpus()) - 1))
     return n
 
 
@@ -231,7 +245,7 @@ def host_cpu() -> dict:
             "cgroup": cgroup_info()}
 
 
-def child_env(threads: int, places: str = "cores", wait: str = "active", cpus=None) -> dict:
+def child_env(threads: int, places: str = "cores", wait: str = "passive", cpus=None) -> dict:
     """environment of a timed child: with `cpus`, one OpenMP place per listed
     CPU (pick_cpus), else OMP_PLACES=`places` packed from the first CPU"""
     env = dict(os.environ)
@@ -240,6 +254,13 @@ def child_env(threads: int, places: str = "cores", wait: str = "active", cpus=No
     env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES=places,
                OMP_WAIT_POLICY=wait)
     return env
+
+
+def throttled_frac(delta: dict | None) -> float | None:
+    """share of the leg's cgroup periods in which the job was throttled"""
+    if not delta or not delta.get("nr_periods"):
+        return None
+    return round(delta.get("nr_throttled", 0) / delta["nr_periods"], 4)
 
 
 def _quartiles(xs):
@@ -289,7 +310,7 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
     def leg(rates, el, thr):
         return {"value": round(statistics.median(rates), 2), "passes": len(rates), "seconds": round(el, 2),
                 "iqr": _quartiles(rates), "passes_range": [round(min(rates), 2), round(max(rates), 2)],
-                "cgroup_cpu_stat_delta": thr}
+                "cgroup_cpu_stat_delta": thr, "throttled_frac": throttled_frac(thr)}
 
     used = co.port_isa(isa)
     binding = (f"OMP_PLACES={os.environ.get('OMP_PLACES')} OMP_PROC_BIND={os.environ.get('OMP_PROC_BIND')} "
@@ -329,6 +350,10 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
         "passes": ln["passes"],
         "leg_seconds": ln["seconds"],
         "cgroup_cpu_stat_delta": thr_n,
+        # periods of the quota in which the job was throttled during the leg,
+        # and the interquartile range relative to the median
+        "throttled_frac": throttled_frac(thr_n),
+        "iqr_rel": [round(q / ln["value"] - 1, 4) for q in ln["iqr"]] if ln["value"] else None,
         "value_1thread": round(statistics.median(r_1), 2),
         "iqr_1thread": _quartiles(r_1),
         "cgroup_cpu_stat_delta_1thread": thr_1,

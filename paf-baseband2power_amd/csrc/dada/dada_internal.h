@@ -104,6 +104,9 @@ typedef struct {
 } dev_seg_t;
 
 /* dada_device.c: HIP reached through dlopen, so libpafdada loads without ROCm */
+/* a viewer's block position (dada_ring.c: the low bits of viewbuf) */
+uint64_t ipcbuf_view_position(const ipcbuf_t *id);
+
 int dev_create_blocks(ipcbuf_t *id, int device); /* fork the holder, fill the handles */
 /* stop the holder and wait (<= 10 s) until it has freed the blocks; -1 with
  * errno EBUSY (text in dada_device_error) while importers stay attached --

@@ -63,7 +63,7 @@ int64_t ipcbuf_tell_write(ipcbuf_t *id) {
 int64_t ipcbuf_tell_read(ipcbuf_t *id) {
   if (!id || ipcbuf_eod(id)) return -1;
   if (id->state == ST_READING) return (int64_t)ipcbuf_tell(id, id->sync->r_bufs[id->iread]);
-  if (id->state == ST_VIEWING) return (int64_t)ipcbuf_tell(id, id->viewbuf);
+  if (id->state == ST_VIEWING) return (int64_t)ipcbuf_tell(id, ipcbuf_view_position(id));
   return 0;
 }
 

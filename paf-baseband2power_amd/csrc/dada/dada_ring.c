@@ -505,21 +505,35 @@ int ipcbuf_mark_filled(ipcbuf_t *id, uint64_t nbytes) {  /* @0x404170 */
 /* ------------------------------------------------------------------ */
 /* ipcbuf: reader                                                       */
 
-/* read depth (extension): viewbuf, unused by a reader in PSRDADA, holds
- * this process's depth | blocks held << 8 | end-of-data block held << 16 */
-static int rd_depth(const ipcbuf_t *id) { return (int)(id->viewbuf & 0xff) ? (int)(id->viewbuf & 0xff) : 1; }
+/* read depth (extension), kept in viewbuf, which PSRDADA leaves unused for
+ * a reader: bits 56-63 hold this process's read depth, set only through
+ * ipcbuf_set_read_depth and kept by every other call; the low bits hold a
+ * reader's blocks held (8-15) and end-of-data block held (16), or a
+ * viewer's block position (0-55, view_next).  So a handle that views and
+ * then reads keeps the depth it was given, never its old view position. */
+#define VB_DEPTH_SHIFT 56
+#define VB_LOW_MASK ((UINT64_C(1) << VB_DEPTH_SHIFT) - 1)
+static int rd_depth(const ipcbuf_t *id) {
+  const int d = (int)(id->viewbuf >> VB_DEPTH_SHIFT);
+  return d ? d : 1;
+}
 static int rd_open(const ipcbuf_t *id) { return (int)((id->viewbuf >> 8) & 0xff); }
 static int rd_eod_held(const ipcbuf_t *id) { return (int)((id->viewbuf >> 16) & 1); }
 static void rd_set(ipcbuf_t *id, int open, int eod_held) {
-  id->viewbuf = (id->viewbuf & 0xff) | ((uint64_t)open << 8) | ((uint64_t)(eod_held != 0) << 16);
+  id->viewbuf = (id->viewbuf & ~VB_LOW_MASK) | ((uint64_t)open << 8) | ((uint64_t)(eod_held != 0) << 16);
 }
+/* a viewer's block position */
+static uint64_t vw_pos(const ipcbuf_t *id) { return id->viewbuf & VB_LOW_MASK; }
+static void vw_set(ipcbuf_t *id, uint64_t pos) { id->viewbuf = (id->viewbuf & ~VB_LOW_MASK) | (pos & VB_LOW_MASK); }
 
 /* before or after ipcbuf_lock_read: lock_read / unlock_read keep the depth */
 int ipcbuf_set_read_depth(ipcbuf_t *id, int depth) {
   if (!id || !id->sync || depth < 1 || depth > 255 || (uint64_t)depth > id->sync->nbufs) return -1;
-  id->viewbuf = (id->viewbuf & ~(uint64_t)0xff) | (uint64_t)depth;
+  id->viewbuf = (id->viewbuf & VB_LOW_MASK) | ((uint64_t)depth << VB_DEPTH_SHIFT);
   return 0;
 }
+
+uint64_t ipcbuf_view_position(const ipcbuf_t *id) { return id ? vw_pos(id) : 0; }
 
 int ipcbuf_lock_read(ipcbuf_t *id) {  /* @0x404360 */
   if (!id || id->state != ST_VIEWER || id->iread != -1) return -1;
@@ -546,7 +560,7 @@ int ipcbuf_lock_read(ipcbuf_t *id) {  /* @0x404360 */
   }
   id->state = s->r_states[id->iread] ? ST_READING : ST_READER;
   id->xfer = s->r_xfers[id->iread] % IPCBUF_XFERS;
-  id->viewbuf &= 0xff; /* a read depth set before the lock stays (blocks held: none) */
+  id->viewbuf &= ~VB_LOW_MASK; /* a read depth set before the lock stays (blocks held: none) */
   return 0;
 }
 
@@ -556,7 +570,7 @@ int ipcbuf_unlock_read(ipcbuf_t *id) {  /* @0x4045f0 */
   if (sem_op(id->semid_connect, SEM_READ, 1, SEM_UNDO) < 0) return -1;
   id->state = ST_VIEWER;
   id->iread = -1;
-  id->viewbuf &= 0xff; /* the read depth stays for the next lock_read */
+  id->viewbuf &= ~VB_LOW_MASK; /* the read depth stays for the next lock_read */
   return 0;
 }
 
@@ -577,23 +591,24 @@ static char *view_next(ipcbuf_t *id, uint64_t *bytes) {
   if (id->state == ST_VIEWER) {
     id->xfer = s->r_xfers[0] % IPCBUF_XFERS;
     id->state = ST_VIEWING;
-    id->viewbuf = s->s_buf[id->xfer];
-    if (s->w_buf > id->viewbuf + 1)
-      id->viewbuf = s->w_buf - 1;
+    vw_set(id, s->s_buf[id->xfer]);
+    if (s->w_buf > vw_pos(id) + 1)
+      vw_set(id, s->w_buf - 1);
     else
       start = s->s_byte[id->xfer];
   }
-  while (s->w_buf <= id->viewbuf) {
+  while (s->w_buf <= vw_pos(id)) {
     if (s->eod[id->xfer] && s->r_bufs[0] && s->r_bufs[0] == s->e_buf[id->xfer]) {
       id->state = ST_VSTOP;
       if (bytes) *bytes = 0;
-      return id->buffer[id->viewbuf % s->nbufs];
+      return id->buffer[vw_pos(id) % s->nbufs];
     }
     if (g_interrupt) return NULL;
     nanosleep(&(struct timespec){0, 100000000}, NULL);
   }
-  if (id->viewbuf + s->nbufs < s->w_buf) id->viewbuf = s->w_buf - s->nbufs + 1;
-  const uint64_t b = id->viewbuf++;
+  if (vw_pos(id) + s->nbufs < s->w_buf) vw_set(id, s->w_buf - s->nbufs + 1);
+  const uint64_t b = vw_pos(id);
+  vw_set(id, b + 1);
   const int last = s->eod[id->xfer] && s->e_buf[id->xfer] == b;
   if (bytes) *bytes = (last ? s->e_byte[id->xfer] : s->bufsz) - start;
   return id->buffer[b % s->nbufs] + start;
@@ -1002,7 +1017,7 @@ char *ipcio_open_block_read(ipcio_t *ipc, uint64_t *curbufsz, uint64_t *block_id
   ipc->curbuf = p;
   ipc->curbufsz = sz;
   if (block_id)
-    *block_id = (reader ? id->sync->r_bufs[id->iread] + (uint64_t)rd_open(id) - 1 : id->viewbuf - 1) %
+    *block_id = (reader ? id->sync->r_bufs[id->iread] + (uint64_t)rd_open(id) - 1 : vw_pos(id) - 1) %
                 id->sync->nbufs;
   if (curbufsz) *curbufsz = sz;
   ipc->bytes = 0;

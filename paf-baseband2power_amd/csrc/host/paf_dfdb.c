@@ -17,7 +17,11 @@
  *     the batch touches; block b is assembled from every batch that holds
  *     frames of it, once a batch that lies wholly past block b+1 has been
  *     read (so a frame may arrive up to about one block early or late, as
- *     the reference's temp buffer allows, capture.c:525-531).  Blocks
+ *     the reference's temp buffer allows, capture.c:525-531).  A frame that
+ *     arrives later than that -- for a block already written, or more than
+ *     one block behind the newest block seen -- is dropped, as the capture
+ *     drops it, and so a lagging source cannot hold the read-ahead back until
+ *     the batch slots overflow.  Blocks
  *     follow the frames' timestamps, not the batch count, so a lossy stream
  *     (fewer frames than blocks x frames per block) still yields every
  *     block it has frames for.  A frame more than 2 blocks past the latest
@@ -81,7 +85,8 @@ typedef struct batch_t {
  * the headers are decoded on the host for the blocks the batch touches,
  * leaving out frames before block 0 and past block `limit` (corrupt) */
 static int load_batch(b2p_ctx_t *ctx, FILE *fd, FILE *fc, batch_t *b, uint64_t cap, unsigned char *hf,
-                      unsigned char *hc, const b2p_df_hdr_t *ref0, uint64_t block_ndf, int64_t limit) {
+                      unsigned char *hc, const b2p_df_hdr_t *ref0, uint64_t block_ndf, int64_t late_before,
+                      int64_t limit) {
   const size_t got = fread(hf, B2P_DF_BYTES, cap, fd);
   b->n = got;
   b->lo = INT64_MAX;
@@ -97,7 +102,10 @@ static int load_batch(b2p_ctx_t *ctx, FILE *fd, FILE *fc, batch_t *b, uint64_t c
     const int64_t rel = b2p_df_index(&h, ref0);
     if (rel < 0) continue;
     const int64_t k = rel / (int64_t)block_ndf;
-    if (k > limit) continue;
+    /* late: a block already written, or more than one block behind the
+     * newest seen -- the capture drops such a frame (capture.c:464-531), so
+     * it neither places it nor lets it hold the read-ahead back */
+    if (k < late_before || k > limit) continue;
     if (k < b->lo) b->lo = k;
     if (k > b->hi) b->hi = k;
   }
@@ -258,7 +266,9 @@ int main(int argc, char **argv) {
           live--;
         }
         batch_t *x = &bt[(head + live) % NSLOT];
-        if (load_batch(ctx, fd, fc, x, cap, hf, hc, &ref0, block_ndf, seen_hi + 2) < 0) goto done;
+        if (load_batch(ctx, fd, fc, x, cap, hf, hc, &ref0, block_ndf, b > seen_hi - 1 ? b : seen_hi - 1,
+                       seen_hi + 2) < 0)
+          goto done;
         if (!x->n) {
           eof = 1;
           break;

@@ -57,7 +57,7 @@ typedef struct conf_t { /* diskdb.cuh:19-30 */
   char fname[2 * MSTR_LEN + 2], hfname[MSTR_LEN];
   int fd;
   int nthread;       /* -T: parallel readers per block */
-  uint64_t payload;  /* file bytes after the 4096-B header */
+  int seekable;      /* a regular file (pread slices); else a pipe / FIFO / terminal, read in order */
   dada_hdu_t *hdu;
   multilog_t *log;
   size_t hdrsz;
@@ -86,8 +86,22 @@ static int init_diskdb(conf_t *conf) {
     fprintf(stderr, "Can not open file: %s\n", conf->fname);
     return EXIT_FAILURE;
   }
-  /* the file's own header is skipped (diskdb.cu:69) */
-  conf->payload = (uint64_t)st.st_size > DADA_HDR_SIZE ? (uint64_t)st.st_size - DADA_HDR_SIZE : 0;
+  /* the file's own header is skipped (diskdb.cu:69): a regular file's
+   * reads start past it; a stream (a FIFO or a pipe) has it read
+   * and dropped.  Either way the payload is read until end of file, not up
+   * to a size taken at open (a file still growing is read to its end, as
+   * the reference's fread loop did) */
+  conf->seekable = S_ISREG(st.st_mode);
+  if (!conf->seekable) {
+    char skip[DADA_HDR_SIZE];
+    size_t got = 0;
+    while (got < sizeof skip) {
+      const ssize_t k = read(conf->fd, skip + got, sizeof skip - got);
+      if (k < 0 && errno == EINTR) continue;
+      if (k <= 0) break;
+      got += (size_t)k;
+    }
+  }
   conf->hdu = dada_hdu_create(conf->log);
   dada_hdu_set_key(conf->hdu, conf->key);
   if (dada_hdu_connect(conf->hdu) < 0) {
@@ -196,10 +210,27 @@ static void populate_ring(const conf_t *conf) {
   }
 }
 
-/* n bytes of the payload from offset off into dst, in nthread contiguous
- * slices (whole 2 MiB pieces, so a thread's copy stays on whole pages);
- * returns the bytes read before the first short slice, or -1 */
+/* up to n bytes of a stream, in order, until end of file */
+static int64_t read_stream(int fd, char *dst, size_t n) {
+  size_t got = 0;
+  while (got < n) {
+    const ssize_t k = read(fd, dst + got, n - got);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    if (k == 0) break;
+    got += (size_t)k;
+  }
+  return (int64_t)got;
+}
+
+/* up to n bytes of the payload from offset off into dst, in nthread
+ * contiguous slices (whole 2 MiB pieces, so a thread's copy stays on whole
+ * pages); returns the bytes read before the first short slice (the end of
+ * the file as it stands), or -1.  A stream is read in order instead. */
 static int64_t read_block(const conf_t *conf, char *dst, uint64_t off, size_t n) {
+  if (!conf->seekable) return read_stream(conf->fd, dst, n);
   slice_t sl[MAX_READERS];
   pthread_t th[MAX_READERS];
   const size_t piece = 2u << 20;
@@ -258,8 +289,8 @@ static int do_diskdb(conf_t *conf) {
     return EXIT_FAILURE;
   }
 #endif
-  /* ring-block-sized reads until the payload is used up; the short (or
-   * empty) last block ends the transfer, as fread's did (diskdb.cu:103-121) */
+  /* ring-block-sized reads until end of file; the short (or empty) last
+   * block ends the transfer, as fread's did (diskdb.cu:103-121) */
   double wait_s = 0, read_s = 0, first_s = 0; /* first_s: the first pass over the ring's blocks */
   const uint64_t nbufs = ipcbuf_get_nbufs((ipcbuf_t *)conf->hdu->data_block);
   for (uint64_t off = 0;;) {
@@ -271,8 +302,7 @@ static int do_diskdb(conf_t *conf) {
       return EXIT_FAILURE;
     }
     clock_gettime(CLOCK_MONOTONIC, &b);
-    const uint64_t left = conf->payload - off;
-    const int64_t got = read_block(conf, stage ? stage : curbuf, off, left < conf->rbufsz ? left : conf->rbufsz);
+    const int64_t got = read_block(conf, stage ? stage : curbuf, off, conf->rbufsz);
     clock_gettime(CLOCK_MONOTONIC, &c);
     wait_s += (double)(b.tv_sec - a.tv_sec) + (double)(b.tv_nsec - a.tv_nsec) * 1e-9;
     const double rs = (double)(c.tv_sec - b.tv_sec) + (double)(c.tv_nsec - b.tv_nsec) * 1e-9;

@@ -186,6 +186,12 @@ class Integrator:
         d.nbytes = arr.nbytes
         return d
 
+    def upload_into(self, d: DeviceBuffer, arr: np.ndarray, offset: int = 0) -> None:
+        """arr (host) -> d + offset, synchronous (b2p_memcpy: hipMemcpy)"""
+        if arr.nbytes:
+            L.check(L.lib().b2p_memcpy(self._ctx, C.c_void_p(d.ptr + offset), C.c_void_p(arr.ctypes.data),
+                                       arr.nbytes, 1), self._ctx)
+
     def download(self, d: DeviceBuffer, nbytes: int | None = None, offset: int = 0) -> np.ndarray:
         n = d.nbytes - offset if nbytes is None else nbytes
         out = np.empty(n, dtype=np.uint8)

@@ -201,11 +201,17 @@ def test_cpu_share_parsing(monkeypatch, tmp_path):
     f.write_text("1600000 100000\n")
     assert cb.cgroup_cpus() == 16.0
     assert cb.effective_cpus() == min(16, len(os.sched_getaffinity(0)))
+    # the timed legs leave one CPU of a quota to the rest of the job
+    assert cb.baseline_threads() == min(15, len(os.sched_getaffinity(0)))
     f.write_text("max 100000\n")
     assert cb.cgroup_cpus() is None
     assert cb.effective_cpus() == len(os.sched_getaffinity(0))
+    assert cb.baseline_threads() == len(os.sched_getaffinity(0))
     env = cb.child_env(16)
     assert env["OMP_NUM_THREADS"] == "16" and env["OMP_PLACES"] == "cores"
+    assert env["OMP_WAIT_POLICY"] == "passive"
+    assert cb.throttled_frac({"nr_periods": 50, "nr_throttled": 2}) == 0.04
+    assert cb.throttled_frac(None) is None
 
 
 def test_watchdog_names_the_stuck_phase_and_exits_4(tmp_path):

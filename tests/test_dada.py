@@ -8,6 +8,7 @@ every block, a short block ends the transfer.
 import os
 import subprocess
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -332,6 +333,60 @@ def test_diskdb_parallel_readers_same_bytes(tmp_path, ring, threads, payload_blo
     assert [len(b) for b in seen[:nfull]] == [bufsz] * nfull
     assert b"".join(seen) == payload.tobytes()
     assert f"{threads} reader" in p.stderr.read().decode()
+
+
+def test_diskdb_reads_a_fifo_and_a_growing_file_to_their_end(tmp_path, ring):
+    """the payload is read until end of file, not up to a size taken when the
+    file was opened (advisor, round 4): a FIFO (no size, no pread) is read
+    in order, and a file that grows after paf_diskdb opened it is read to
+    its final end -- as the reference's fread loop did (diskdb.cu:103-121)"""
+    bufsz = 1 << 16
+    hdr = tmp_path / "header.txt"
+    hdr.write_text(TEMPLATE)
+    payload = np.random.default_rng(7).integers(0, 256, 5 * bufsz + 1234, dtype=np.uint8)
+    whole = tmp_path / "whole.dada"
+    dada.write_dada_file(str(whole), "FILE_HEADER_IS_SKIPPED 1\n", payload)
+    blob = whole.read_bytes()
+
+    def consume(k, seen):
+        with dada.Hdu(k, "R") as r:
+            r.read_header()
+            while (b := r.read_block()) is not None:
+                seen.append(bytes(b))
+
+    # 1. a FIFO, written in odd pieces by another thread
+    k = ring(3, bufsz)
+    fifo = tmp_path / "obs.fifo"
+    os.mkfifo(fifo)
+    seen = []
+    t = threading.Thread(target=consume, args=(k, seen))
+    t.start()
+
+    def feed():
+        with open(fifo, "wb") as f:
+            for i in range(0, len(blob), 9999):
+                f.write(blob[i:i + 9999])
+    w = threading.Thread(target=feed)
+    w.start()
+    p = run_diskdb(k, str(fifo), str(hdr), threads=4)
+    assert p.wait(60) == 0, p.stderr.read()
+    w.join(60)
+    t.join(60)
+    assert b"".join(seen) == payload.tobytes()
+    assert [len(b) for b in seen[:5]] == [bufsz] * 5
+    # 2. a file that grows after it was opened: paf_diskdb waits on a full
+    #    ring (no reader yet) while the rest of the payload is appended
+    k2 = ring(2, bufsz)
+    grow = tmp_path / "grow.dada"
+    grow.write_bytes(blob[: 4096 + 2 * bufsz + 100])  # header + two blocks (fill the ring) + a bit
+    p = run_diskdb(k2, str(grow), str(hdr), threads=2)
+    time.sleep(0.5)                                    # both blocks written, waiting for a third
+    with open(grow, "ab") as f:
+        f.write(blob[4096 + 2 * bufsz + 100:])
+    seen2 = []
+    consume(k2, seen2)
+    assert p.wait(60) == 0, p.stderr.read()
+    assert b"".join(seen2) == payload.tobytes()
 
 
 def test_diskdb_rejects_bad_thread_count(tmp_path):

@@ -208,3 +208,21 @@ def test_staging_and_addressing_model_under_asan(tmp_path):
     r = subprocess.run([str(exe), "300", "20181105"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert "plan model: 300 cases ok" in r.stdout, r.stdout
+
+
+def test_read_depth_survives_a_view_under_asan(tmp_path):
+    """a handle that sets read depth 2, views a block (view position 1) and
+    then locks for reading still holds two blocks at once: the depth lives
+    in viewbuf's top byte, apart from the view position (advisor, round 4:
+    it used to read back as the old position's low byte;
+    tests/c/ring_depth_view.c)"""
+    exe = tmp_path / "ring_depth_view"
+    subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
+                    "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "c", "ring_depth_view.c"), *SRC, "-o", str(exe), "-pthread",
+                    "-ldl", "-lm"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([str(exe), "7c50"], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "errors 0" in r.stdout
