@@ -55,6 +55,9 @@ def main():
                     m = re.search(r"(\d+) IPC export retr", p.stderr)
                     if m:
                         retries[f"{sz}x{nb}"] += int(m.group(1))
+                        # the holder's first failed try: call, error, address range
+                        print(json.dumps({"retry": f"{sz}x{nb}", "round": r,
+                                          "holder": p.stderr.strip()[-300:]}), flush=True)
                     if p.returncode != 0:
                         fails[f"{sz}x{nb}"] += 1
                         e = p.stderr.strip()[-200:]
