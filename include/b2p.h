@@ -173,7 +173,17 @@ const char *b2p_last_error(const b2p_ctx_t *ctx); /* ctx may be NULL */
 int b2p_set_stream(b2p_ctx_t *ctx, void *hip_stream);
 
 /* ---- host memory (role of PSRDADA dada_cuda_dbregister; dada_cuda.h is
- * included at baseband2power.cuh:9) ---- */
+ * included at baseband2power.cuh:9) ----
+ * Lifetime rules (a copy that reads or writes host memory its owner has
+ * released is a GPU page fault that kills the process's HIP context):
+ *  - register: B2P_EINVAL if the range overlaps a range still registered
+ *    through any context of the process;
+ *  - the memory must stay allocated while registered;
+ *  - unregister: first drains the context's streams (a b2p_finish_async into
+ *    the range may still be landing); work the caller enqueued elsewhere on
+ *    the range must be complete; any context may release a range;
+ *  - b2p_close releases every range its context registered and the caller
+ *    left registered. */
 int b2p_register_host(b2p_ctx_t *ctx, void *base, size_t bytes);
 int b2p_unregister_host(b2p_ctx_t *ctx, void *base);
 
@@ -187,7 +197,8 @@ int b2p_unregister_host(b2p_ctx_t *ctx, void *base);
  *   kernel, and b2p_push returns once every byte has been copied, so the
  *   caller may release / close the DADA block.  If a host-span push fails
  *   after its first chunk was enqueued, the context is marked failed
- *   (B2P_EFAILED from then on, see above). */
+ *   (B2P_EFAILED from then on, see above); its copies from buf are drained
+ *   before it returns, so buf may be released on every return. */
 int b2p_push(b2p_ctx_t *ctx, const void *buf, size_t nbytes, int is_device);
 /* Emit the integration: out[nout] (host memory), blocking.  Returns B2P_OK
  * if exactly nsamp_int samples were pushed, B2P_EPARTIAL otherwise (the

@@ -126,7 +126,14 @@ static long importers_attached(int seg0_id, const dev_seg_t *seg0) {
  * importer -- and in every case only once no importer is attached (the
  * ordering rule in dada_internal.h), so no process can still have a block
  * mapped when it is freed */
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
+
 static void holder(ipcbuf_t *id, int device, int wfd) {
+  const double t_start = now_s();
   int rc;
   const uint64_t n = id->sync->nbufs, bufsz = id->sync->bufsz;
   dev_seg_t *seg0 = id->shm_addr[0];
@@ -165,6 +172,28 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
       if ((rc = hip.malloc_(&blk[i], alloc)) == 0 && (what = "hipMemset", rc = hip.memset_(blk[i], 0, alloc)) == 0 &&
           (what = "hipIpcGetMemHandle", rc = hip.get_handle(&h, blk[i])) == 0)
         break;
+      if (rc != 0 && blk[i] && !strcmp(what, "hipIpcGetMemHandle")) {
+        /* the same pointer once more after a pause: tells a transient
+         * export failure from one that sticks to the allocation */
+        struct timespec pause = {0, 20 * 1000 * 1000};
+        nanosleep(&pause, NULL);
+        const int again = hip.get_handle(&h, blk[i]);
+        if (!first[0]) {
+          void *base = NULL;
+          size_t size = 0;
+          const int ar = hip.addr_range ? hip.addr_range(&base, &size, blk[i]) : -1;
+          snprintf(first, sizeof first,
+                   "%s: %s (%d) on block %llu of %llu B, range %s%+lld %llu B, %.0f ms after start; "
+                   "same pointer 20 ms later: %s",
+                   what, hip.err_str(rc), rc, (unsigned long long)i, (unsigned long long)alloc,
+                   ar == 0 ? "base" : "?", ar == 0 ? (long long)((char *)blk[i] - (char *)base) : 0LL,
+                   (unsigned long long)size, (now_s() - t_start) * 1e3, again == 0 ? "exported" : hip.err_str(again));
+        }
+        if (again == 0) {
+          retries++;
+          break;
+        }
+      }
       if (!first[0]) {
         void *base = NULL;
         size_t size = 0;

@@ -7,7 +7,7 @@
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 #          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4 pmc1
-#          devleak
+#          devleak devleak20 replay9090 debughunt
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -181,6 +181,14 @@ for s in $STEPS; do
             -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_bmf 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_bmf" -o run \
             -- python3 bench.py --config bmf --steps 10 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify ;;
+    replay9090) # round 4's failing stage hunt, replayed after the device-ring ordering rule:
+                # seed 9090 at scale 6, every GPU-resident ring written from the test process
+                run replay9090 1100 env B2P_STAGE_WRITER=inproc B2P_HYPOTHESIS_SEED=9090 B2P_HYPOTHESIS_SCALE=6 \
+                  python3 -u -m pytest tests/test_gpu_stage_random.py -v -rf --timeout 900 --timeout-method thread \
+                  -k "layouts_rings_and_flags or gathered_subbands" --hypothesis-show-statistics ;;
+    debughunt) # the host-staging property under the debug library, 1500 examples, seed 777
+               run debug_staging_hunt 900 python3 -u tests/debug_build_checks.py staging 1500 777 ;;
+    devleak20) run devring_leak20 900 python3 tools/devring_probe.py 20 use ;;
     devleak) # a few hundred device-ring create / write / destroy cycles in one process:
              # open fds and mapped size per ring
              run devring_leak 600 python3 tools/devring_probe.py 10 use ;;
