@@ -162,7 +162,22 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
   const uint64_t alloc = (bufsz + DEV_ALLOC_ALIGN - 1) / DEV_ALLOC_ALIGN * DEV_ALLOC_ALIGN;
   void *spare[DEV_EXPORT_TRIES * 4];
   int nspare = 0, retries = 0;
-  char first[160] = "";
+  char first[240] = "";
+  /* The primer: round 5's probes (profiles/r05_devring_leak*.jsonl) found the
+   * export refusal only ever on a holder's FIRST device allocation (block
+   * 0, ~210 ms after start), about 1 ring in 100, sticky to that allocation
+   * (refused again 20 ms later) while a fresh one exported.  So the holder
+   * makes its first allocation a 2 MiB primer that no ring block uses,
+   * tries to export it, and keeps it until exit; whether the primer's
+   * export was refused is reported with the retries (the "P" count). */
+  void *primer = NULL;
+  int primer_refused = 0;
+  if (hip.malloc_(&primer, DEV_ALLOC_ALIGN) == 0) {
+    ipc_handle_t ph;
+    primer_refused = hip.memset_(primer, 0, DEV_ALLOC_ALIGN) == 0 && hip.get_handle(&ph, primer) != 0;
+  } else {
+    primer = NULL;
+  }
   for (uint64_t i = 0; i < n; i++) {
     ipc_handle_t h;
     const char *what = "hipMalloc";
@@ -223,8 +238,9 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
   hip.sync();
   seg0->holder_pid = (int32_t)getpid();
   __atomic_store_n(&seg0->holder_state, 1, __ATOMIC_RELEASE);
-  char ready[200];
-  const int nr = snprintf(ready, sizeof ready, "R%d %s", retries, first); /* 'R' + export retries */
+  char ready[300];
+  /* 'R' + export retries of ring blocks, 'P' + 1 if the primer's export was refused */
+  const int nr = snprintf(ready, sizeof ready, "R%d P%d %s", retries, primer_refused, first);
   (void)!write(wfd, ready, (size_t)nr < sizeof ready ? (size_t)nr : sizeof ready - 1);
   close(wfd);
 
@@ -252,6 +268,7 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
     if (stopping && others == 0) break;
   }
   for (uint64_t i = 0; i < n; i++) hip.free_(blk[i]);
+  if (primer) hip.free_(primer);
   __atomic_store_n(&seg0->holder_state, 2, __ATOMIC_RELEASE);
   _exit(0);
 }
@@ -300,11 +317,15 @@ int dev_create_blocks(ipcbuf_t *id, int device) {
   close(fds[0]);
   if (got >= 1 && msg[0] == 'R') {
     const int retries = atoi(msg + 1);
+    const char *pp = strstr(msg, " P");
+    const int primer_refused = pp ? atoi(pp + 2) : 0;
     if (retries > 0) {
-      const char *why = strchr(msg, ' ');
+      const char *why = pp ? strchr(pp + 1, ' ') : NULL;
       fprintf(stderr, "dada device ring: %d IPC export retr%s in the holder (first: %s)\n", retries,
               retries == 1 ? "y" : "ies", why ? why + 1 : "?");
     }
+    if (primer_refused) /* diagnostics only: no ring block is affected */
+      fprintf(stderr, "dada device ring: the holder's primer allocation was not exportable\n");
     return 0;
   }
   fprintf(stderr, "dada device ring: holder failed: %s\n", got > 1 ? msg + 1 : "no reply");

@@ -62,13 +62,18 @@ def main():
         want = sys.argv[2].split(",")
         bindings.update({k: None for k in want if k not in bindings})
         bindings = {k: bindings[k] for k in want}
+    waits = {}
     for name in list(bindings):   # "spread2:15": the first 15 CPUs of a binding, 15 threads
-        if ":" in name:
-            base, k = name.split(":")
+        if ":" in name:           # "spread2:15:active": and that OpenMP wait policy ("default": unset)
+            base, k, *w = name.split(":")
             full = bindings[base] if base != "spread2" else sorted(cb.spread_l3(sorted(every.values()), int(k)))
             bindings[name] = full[:int(k)]
+            if w:
+                waits[name] = w[0]
     for name, cpus in bindings.items():
-        env = cb.child_env(len(cpus), cpus=cpus)
+        env = cb.child_env(len(cpus), cpus=cpus, wait=waits.get(name, "passive"))
+        if waits.get(name) == "default":
+            env.pop("OMP_WAIT_POLICY", None)
         r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_baseline.py"),
                             json.dumps(GEOM), str(secs), "20181105", "only"], env=env,
                            capture_output=True, text=True, timeout=max(120, secs * 20))
@@ -77,7 +82,12 @@ def main():
                           "nodes": sorted({k for k, cs in nodes.items() for c in cpus if c in cs}),
                           "l3_domains": len({cb.l3_domain(c) for c in cpus}),
                           "l3_domains_on_node": len(doms), "threads": len(cpus),
+                          "wait": waits.get(name, "passive"),
                           "value": res.get("value"), "iqr": res.get("iqr"), "passes": res.get("passes"),
+                          "iqr_rel": ([round(q / res["value"] - 1, 4) for q in res["iqr"]]
+                                      if res.get("value") and res.get("iqr") else None),
+                          "throttled_frac": res.get("throttled_frac"),
+                          "passes_range": res.get("passes_range"),
                           "cgroup_cpu_stat_delta": res.get("cgroup_cpu_stat_delta"),
                           "error": res.get("error")}), flush=True)
 

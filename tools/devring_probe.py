@@ -44,6 +44,7 @@ def main():
     tmp = tempfile.mkdtemp(prefix="devring_probe_")
     key = 0x7e40
     fails, retries, errs, attempts = collections.Counter(), collections.Counter(), {}, 0
+    primer = collections.Counter()  # holders whose primer (first) allocation did not export
     for r in range(rounds):
         for sz in SIZES:
             for nb in (2, 4, 6):
@@ -52,6 +53,8 @@ def main():
                 try:
                     p = subprocess.run([os.path.join(dada.BIN_DIR, "dada_db"), "-k", f"{key:x}", "-b", str(sz),
                                         "-n", str(nb), "-g", "0"], capture_output=True, text=True, timeout=120)
+                    if "primer allocation was not exportable" in p.stderr:
+                        primer[f"{sz}x{nb}"] += 1
                     m = re.search(r"(\d+) IPC export retr", p.stderr)
                     if m:
                         retries[f"{sz}x{nb}"] += int(m.group(1))
@@ -86,9 +89,11 @@ def main():
                 finally:
                     dada.destroy_ring(key)
         print(json.dumps({"round": r, "attempts": attempts, "failures": sum(fails.values()),
-                          "retries": sum(retries.values())}), flush=True)
+                          "retries": sum(retries.values()), "primer_refused": sum(primer.values())}), flush=True)
     print(json.dumps({"attempts": attempts, "failures": sum(fails.values()), "by_case": fails,
-                      "retries": sum(retries.values()), "retries_by_case": retries, "errors": errs}), flush=True)
+                      "retries": sum(retries.values()), "retries_by_case": retries,
+                      "primer_refused": sum(primer.values()), "primer_refused_by_case": primer,
+                      "errors": errs}), flush=True)
 
 
 if __name__ == "__main__":

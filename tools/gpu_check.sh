@@ -189,6 +189,11 @@ for s in $STEPS; do
     debughunt) # the host-staging property under the debug library, 1500 examples, seed 777
                run debug_staging_hunt 900 python3 -u tests/debug_build_checks.py staging 1500 777 ;;
     devleak20) run devring_leak20 900 python3 tools/devring_probe.py 20 use ;;
+    cpuwait) # the CPU baseline's thread count and OpenMP wait policy: spread and throttling
+             run cpu_wait_a 300 python3 tools/cpu_spread_probe.py 5 \
+               spread2:15:passive,spread2:15:default,spread2:15:active,spread2:14:passive,spread2:12:passive &&
+             run cpu_wait_b 300 python3 tools/cpu_spread_probe.py 5 \
+               spread2:12:passive,spread2:14:passive,spread2:15:active,spread2:15:default,spread2:15:passive ;;
     devleak) # a few hundred device-ring create / write / destroy cycles in one process:
              # open fds and mapped size per ring
              run devring_leak 600 python3 tools/devring_probe.py 10 use ;;
