@@ -285,7 +285,7 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
     """The tuned CPU port (oracle/b2p_cpu_port.c) timed in a child process
     (its own OpenMP binding), at the job's CPU quota less one thread
     (cpu_baseline.baseline_threads: threads that fill the quota exactly get
-    throttled) with passive OpenMP waits, and at 1 thread, with the scalar
+    throttled) with libgomp's default wait policy, and at 1 thread, with the scalar
     oracle beside it, on one full block.  The line reports the share of
     throttled cgroup periods and the interquartile range beside `value`."""
     sys.path.insert(0, ORACLE)
@@ -302,13 +302,14 @@ def cpu_baseline(geom_dict: dict, seconds: float) -> dict | None:
             return None
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    res = child(cb.child_env(threads, cpus=picked["cpus"], wait="passive"), seconds)
+    res = child(cb.child_env(threads, cpus=picked["cpus"], wait="default"), seconds)
     if res is not None:
         res["cpus_picked"] = {**picked, "rule": "the cgroup quota less one thread, one logical CPU per "
                                                 "physical core, dealt round-robin over every L3 domain (CCD) "
                                                 "of every NUMA node, the idlest allowed core of each over the "
                                                 "sample before the legs; CPU order, so each thread's "
-                                                "first-touched tile is on its own node; passive OpenMP waits"}
+                                                "first-touched tile is on its own node; libgomp's default wait "
+                                                "policy (OMP_WAIT_POLICY unset)"}
     return res
 
 

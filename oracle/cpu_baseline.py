@@ -9,7 +9,7 @@ a 1 GiB block does not fit).  SURVEY.md 8(d) "CPU baseline": the reference has
 no CPU path, so the baseline is the port, at 1 thread and at every CPU this
 process may use.  bench.py picks the CPUs (pick_cpus): one per physical core,
 dealt over every L3 domain (CCD) of both NUMA nodes, listed as explicit OpenMP
-places, one fewer than the cgroup quota grants and with passive OpenMP waits
+places, one fewer than the cgroup quota grants, libgomp's default wait policy
 (baseline_threads: threads that fill the quota exactly are throttled); every leg reports the cgroup's cpu.stat deltas (periods throttled, time throttled)
 beside its median and interquartile range, so a slow box shows why.
 
@@ -115,7 +115,7 @@ def baseline_threads() -> int:
     that waits for this child, the HIP runtime's threads, this interpreter),
     so threads that fill it exactly are throttled -- round 4's 16 threads in
     a 16-CPU quota were throttled in 43 of 54 periods and their passes spread
-    8x; at quota - 1 with passive waits the job stays inside it."""
+    8x; at quota - 1 the job stays inside it (0 throttled periods)."""
     n = effective_cpus()
     if cgroup_cpus() is not None:
         n = min(n, max(1, int(cgroup_cpus()) - 1))
@@ -245,14 +245,23 @@ def host_cpu() -> dict:
             "cgroup": cgroup_info()}
 
 
-def child_env(threads: int, places: str = "cores", wait: str = "passive", cpus=None) -> dict:
+def child_env(threads: int, places: str = "cores", wait: str = "default", cpus=None) -> dict:
     """environment of a timed child: with `cpus`, one OpenMP place per listed
-    CPU (pick_cpus), else OMP_PLACES=`places` packed from the first CPU"""
+    CPU (pick_cpus), else OMP_PLACES=`places` packed from the first CPU.
+    wait: "default" leaves OMP_WAIT_POLICY unset (libgomp spins briefly
+    between parallel regions, then sleeps), else "passive" / "active".
+    On the GPU box at 15 threads in the 16-CPU quota (profiles/r05_cpu_wait.jsonl)
+    the default measured 2.69-2.73 x 10^5 Msamples/s with an interquartile
+    range within -8.6 / +4.9 % and no throttled period, passive 2.33-2.49 x
+    10^5 (within +-3.6 %), active 2.57-2.71 x 10^5 (within -9.0 / +4.5 %)."""
     env = dict(os.environ)
     if cpus:
         places = ",".join("{%d}" % c for c in cpus[:threads])
-    env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES=places,
-               OMP_WAIT_POLICY=wait)
+    env.update(OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES=places)
+    if wait == "default":
+        env.pop("OMP_WAIT_POLICY", None)
+    else:
+        env["OMP_WAIT_POLICY"] = wait
     return env
 
 

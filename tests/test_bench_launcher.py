@@ -209,7 +209,8 @@ def test_cpu_share_parsing(monkeypatch, tmp_path):
     assert cb.baseline_threads() == len(os.sched_getaffinity(0))
     env = cb.child_env(16)
     assert env["OMP_NUM_THREADS"] == "16" and env["OMP_PLACES"] == "cores"
-    assert env["OMP_WAIT_POLICY"] == "passive"
+    assert "OMP_WAIT_POLICY" not in env or env["OMP_WAIT_POLICY"] == os.environ.get("OMP_WAIT_POLICY")
+    assert cb.child_env(4, wait="passive")["OMP_WAIT_POLICY"] == "passive"
     assert cb.throttled_frac({"nr_periods": 50, "nr_throttled": 2}) == 0.04
     assert cb.throttled_frac(None) is None
 
