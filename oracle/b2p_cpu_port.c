@@ -23,7 +23,13 @@
  *     widened to 64 bits on every add.  All exact, so the sums equal the
  *     oracle's uint64 sums.
  *   - Threads: frames are split into equal contiguous tiles, one per OpenMP
- *     thread (the same static split that first-touched the block).
+ *     thread (the same static split that first-touched the block), each cut
+ *     into ~4 MiB pieces.  A thread takes its own tile's pieces in order,
+ *     then takes pieces left in its neighbours' tiles: on a host shared with
+ *     other jobs a thread that is preempted for a while no longer holds the
+ *     whole pass back (one slow thread set the pass time with plain static
+ *     tiles).  Sums are exact integers, so who adds a piece cannot change a
+ *     bit.
  *
  * ISA chosen at run time (__builtin_cpu_supports): avx512vnni > avx512bw >
  * avx2 > scalar; cpp_integrate's `isa` argument forces one for tests.
@@ -146,8 +152,10 @@ static void run_scalar(const orc_geom_t *g, const uint8_t *buf, uint64_t f0, uin
         }                                                                                \
       }                                                                                  \
     }                                                                                    \
-    for (uint64_t i = 0; i < (uint64_t)p->lanes * g->nchunk; i++)                        \
+    for (uint64_t i = 0; i < (uint64_t)p->lanes * g->nchunk; i++) {                      \
       acc64[i] += (uint64_t)(uint32_t)acc32[i];                                          \
+      acc32[i] = 0; /* the next call (another piece) starts from zero */                 \
+    }                                                                                    \
     (void)ZERO;                                                                          \
   }
 
@@ -268,6 +276,14 @@ int cpp_integrate(const orc_geom_t *g, const uint8_t *buf, size_t nbytes, uint64
   if (nthreads < 1) nthreads = 1;
   uint64_t *part = calloc((size_t)nthreads * nout, sizeof(uint64_t));
   if (!part) return -1;
+  /* pieces of ~4 MiB of whole frames; next[t * 8]: the next unclaimed piece
+   * of thread t's tile (one cache line per counter) */
+  const uint64_t pf = fb >= (4u << 20) ? 1 : (4u << 20) / fb;
+  uint64_t *next = calloc((size_t)nthreads * 8, sizeof(uint64_t));
+  if (!next) {
+    free(part);
+    return -1;
+  }
   int bad = 0;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads) reduction(| : bad)
@@ -278,33 +294,42 @@ int cpp_integrate(const orc_geom_t *g, const uint8_t *buf, size_t nbytes, uint64
     t = omp_get_thread_num();
     nt = omp_get_num_threads();
 #endif
-    const uint64_t f0 = nf * t / nt, f1 = nf * (t + 1) / nt;
     uint64_t *out = part + (size_t)t * nout;
-    if (isa == ISA_SCALAR) {
-      run_scalar(g, buf, f0, f1, out);
+    const size_t nl = isa == ISA_SCALAR ? 0 : (size_t)p.lanes * g->nchunk;
+    uint64_t *acc64 = nl ? aligned_alloc(64, (nl * 8 + 63) / 64 * 64) : NULL;
+    int32_t *acc32 = nl && g->nbit == 8 ? aligned_alloc(64, (nl * 4 + 63) / 64 * 64) : NULL;
+    if (nl && (!acc64 || (g->nbit == 8 && !acc32))) {
+      bad = 1;
     } else {
-      const size_t nl = (size_t)p.lanes * g->nchunk;
-      uint64_t *acc64 = aligned_alloc(64, (nl * 8 + 63) / 64 * 64);
-      int32_t *acc32 = g->nbit == 8 ? aligned_alloc(64, (nl * 4 + 63) / 64 * 64) : NULL;
-      if (!acc64 || (g->nbit == 8 && !acc32)) {
-        bad = 1;
-      } else {
-        memset(acc64, 0, nl * 8);
-        if (acc32) memset(acc32, 0, nl * 4);
-        if (g->nbit == 8) {
-          if (isa == ISA_VNNI) i8_vnni(g, &p, buf, f0, f1, acc32, acc64);
-          else if (isa == ISA_AVX512) i8_avx512(g, &p, buf, f0, f1, acc32, acc64);
-          else i8_avx2(g, &p, buf, f0, f1, acc32, acc64);
-        } else {
-          if (isa == ISA_AVX2) i16_avx2(g, &p, buf, f0, f1, acc64);
-          else i16_avx512(g, &p, buf, f0, f1, acc64);
+      if (acc64) memset(acc64, 0, nl * 8);
+      if (acc32) memset(acc32, 0, nl * 4);
+      /* own tile first, then the neighbours' tiles in thread order */
+      for (int k = 0; k < nt; k++) {
+        const int v = (t + k) % nt;
+        const uint64_t v0 = nf * v / nt, v1 = nf * (v + 1) / nt;
+        const uint64_t npieces = (v1 - v0 + pf - 1) / pf;
+        for (;;) {
+          const uint64_t i = __atomic_fetch_add(&next[(size_t)v * 8], 1, __ATOMIC_RELAXED);
+          if (i >= npieces) break;
+          const uint64_t f0 = v0 + i * pf, f1 = f0 + pf < v1 ? f0 + pf : v1;
+          if (isa == ISA_SCALAR) {
+            run_scalar(g, buf, f0, f1, out);
+          } else if (g->nbit == 8) {
+            if (isa == ISA_VNNI) i8_vnni(g, &p, buf, f0, f1, acc32, acc64);
+            else if (isa == ISA_AVX512) i8_avx512(g, &p, buf, f0, f1, acc32, acc64);
+            else i8_avx2(g, &p, buf, f0, f1, acc32, acc64);
+          } else {
+            if (isa == ISA_AVX2) i16_avx2(g, &p, buf, f0, f1, acc64);
+            else i16_avx512(g, &p, buf, f0, f1, acc64);
+          }
         }
-        fold(g, &p, acc64, out);
       }
-      free(acc64);
-      free(acc32);
+      if (acc64) fold(g, &p, acc64, out);
     }
+    free(acc64);
+    free(acc32);
   }
+  free(next);
   if (!bad)
     for (int t = 0; t < nthreads; t++)
       for (uint32_t j = 0; j < nout; j++) acc[j] += part[(size_t)t * nout + j];
