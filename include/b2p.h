@@ -176,8 +176,9 @@ int b2p_set_stream(b2p_ctx_t *ctx, void *hip_stream);
  * included at baseband2power.cuh:9) ----
  * Lifetime rules (a copy that reads or writes host memory its owner has
  * released is a GPU page fault that kills the process's HIP context):
- *  - register: B2P_EINVAL if the range overlaps a range still registered
- *    through any context of the process;
+ *  - register: B2P_EINVAL if the range shares a (4 KiB) page with a range
+ *    still registered through any context of the process (pinning is per
+ *    page);
  *  - the memory must stay allocated while registered;
  *  - unregister: first drains the context's streams (a b2p_finish_async into
  *    the range may still be landing); work the caller enqueued elsewhere on

@@ -481,14 +481,26 @@ int b2p_set_stream(b2p_ctx_t *c, void *s) {
   return B2P_OK;
 }
 
+// pages a host range touches: [first, last] page numbers (pinning is per page)
+static void page_span(const char *p, size_t n, uintptr_t *lo, uintptr_t *hi) {
+  const uintptr_t pg = 4096;
+  *lo = reinterpret_cast<uintptr_t>(p) / pg;
+  *hi = (reinterpret_cast<uintptr_t>(p) + n - 1) / pg;
+}
+
 int b2p_register_host(b2p_ctx_t *c, void *base, size_t bytes) {
   if (!c || !base || !bytes) return B2P_EINVAL;
   const char *b = static_cast<const char *>(base);
   std::lock_guard<std::mutex> lk(g_reg_mu);
-  for (const HostReg &r : g_regs)
-    if (b < r.base + r.bytes && r.base < b + bytes)
-      return set_err(c, B2P_EINVAL, "host range %p+%zu overlaps the registered range %p+%zu", base, bytes,
-                     (const void *)r.base, r.bytes);
+  uintptr_t lo, hi;
+  page_span(b, bytes, &lo, &hi);
+  for (const HostReg &r : g_regs) {  // a page may be pinned by one registration only
+    uintptr_t rlo, rhi;
+    page_span(r.base, r.bytes, &rlo, &rhi);
+    if (lo <= rhi && rlo <= hi)
+      return set_err(c, B2P_EINVAL, "host range %p+%zu shares pages with the registered range %p+%zu", base,
+                     bytes, (const void *)r.base, r.bytes);
+  }
   CK(c, hipSetDevice(c->device));
   CK(c, hipHostRegister(base, bytes, hipHostRegisterDefault));
   g_regs.push_back(HostReg{b, bytes, c});

@@ -124,7 +124,7 @@ def checks():
                 it3.register_host(host[4096:])
                 raise AssertionError("overlapping registration accepted")
             except paf_b2p.B2PError as e:
-                assert e.code == L.B2P_EINVAL and "overlaps" in str(e), e
+                assert e.code == L.B2P_EINVAL and "shares pages" in str(e), e
             it3.close()
             it2.push(host)
             out = it2.finish()

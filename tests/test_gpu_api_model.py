@@ -7,6 +7,12 @@ into device slots, b2p_integrate and b2p_integrate_n into device slots,
 b2p_flush, b2p_fence / b2p_fence_wait, b2p_sync -- with slots reused before
 a sync, pushes while an output is still pending, and calls that must be
 refused (b2p_integrate with a push pending, pushes past the integration).
+Host memory lifetime (round 5): the input blocks and a host output array
+are registered and unregistered at random; a second registration of a
+range is refused; b2p_finish_async lands spectra in the registered host
+output, and unregistering it while they may still be landing must drain
+them first; b2p_close releases what the context left registered (the same
+memory registers again in a fresh context at teardown).
 A NumPy model keeps the exact uint64 sums of the frames pushed (the C
 oracle's integrate over each span) and what every slot must hold after
 b2p_sync; every check compares bit for bit.  The geometry and the launch
@@ -48,7 +54,21 @@ class ApiModel(RuleBasedStateMachine):
         self.nframes = nframes
         self.it = paf_b2p.Integrator(paf_b2p.make_geom(**self.g.asdict()), tuning={"fuse": fuse})
         fb = self.g.frame_bytes
-        self.host = [co.fill_synthetic(self.g, self.g.block_bytes, seed, 1, b) for b in range(NBLK)]
+        # page-aligned, page-padded host arrays (a page is pinned by one
+        # registration only): the blocks, then a host output array
+        pg = 4096
+        span = (self.g.block_bytes + pg - 1) // pg * pg
+        hspan = (NSLOT * self.g.nout * 4 + pg - 1) // pg * pg
+        self._hmem = np.zeros(NBLK * span + hspan + pg, np.uint8)
+        a0 = (-self._hmem.ctypes.data) % pg
+        self.host = []
+        for b in range(NBLK):
+            v = self._hmem[a0 + b * span: a0 + b * span + self.g.block_bytes]
+            co.fill_synthetic(self.g, self.g.block_bytes, seed, 1, b, out=v)
+            self.host.append(v)
+        self.hout = self._hmem[a0 + NBLK * span: a0 + NBLK * span + NSLOT * self.g.nout * 4].view(np.float32)
+        self.registered = set()            # host blocks registered (index), "out" for the output
+        self.want_host = {}                # host slot -> expected fp32 bits (after sync)
         self.dev = [self.it.upload(h) for h in self.host]
         # per block, exact sums of each frame (the model adds them up)
         g1 = npo.Geom(**{**self.g.asdict(), "nsamp_int": layout["nsamp_df"]})
@@ -78,7 +98,51 @@ class ApiModel(RuleBasedStateMachine):
             finally:
                 for d in self.dev + [self.out, self.raw]:
                     d.free()
-                self.it.close()
+                self.it.close()   # releases what is still registered
+            if self.registered:   # ... so the same memory registers again
+                with paf_b2p.Integrator(paf_b2p.make_geom(**self.g.asdict())) as it2:
+                    for r in self.registered:
+                        arr = self.hout if r == "out" else self.host[r]
+                        it2.register_host(arr)
+                        it2.unregister_host(arr)
+
+    # ---- host memory ----------------------------------------------------------
+    @rule(r=st.sampled_from([0, 1, 2, "out"]))
+    def register(self, r):
+        CALLS["register"] = CALLS.get("register", 0) + 1
+        self.log.append(f"register {r}")
+        arr = self.hout if r == "out" else self.host[r]
+        if r in self.registered:   # a second registration of the range is refused
+            with pytest.raises(L.B2PError) as e:
+                self.it.register_host(arr)
+            assert e.value.code == L.B2P_EINVAL
+            return
+        self.it.register_host(arr)
+        self.registered.add(r)
+
+    @precondition(lambda self: bool(self.registered))
+    @rule(data=st.data())
+    def unregister(self, data):
+        CALLS["unregister"] = CALLS.get("unregister", 0) + 1
+        r = data.draw(st.sampled_from(sorted(self.registered, key=str)))
+        self.log.append(f"unregister {r}")
+        # the output may still be landing (finish_async_host): unregister drains it
+        self.it.unregister_host(self.hout if r == "out" else self.host[r])
+        self.registered.discard(r)
+        if r == "out":   # every spectrum enqueued into it has landed
+            got = self.hout.view(np.uint32).reshape(NSLOT, self.g.nout)
+            for s_, w in self.want_host.items():
+                assert np.array_equal(got[s_], w), ("host slot after unregister", s_, "\n".join(self.log[-60:]))
+
+    @precondition(lambda self: "out" in self.registered)
+    @rule(slot=st.integers(0, NSLOT - 1))
+    def finish_async_host(self, slot):
+        CALLS["finish_async_host"] = CALLS.get("finish_async_host", 0) + 1
+        self.log.append(f"finish_async_host slot={slot}")
+        rc = self.it.finish_async(self.hout.ctypes.data + slot * self.g.nout * 4, False)
+        assert rc == (L.B2P_OK if self.pend == self.nframes else L.B2P_EPARTIAL)
+        self.want_host[slot] = self._spectrum(self.acc)
+        self._reset()
 
     # ---- pushes ---------------------------------------------------------------
     @rule(data=st.data())
@@ -186,7 +250,7 @@ class ApiModel(RuleBasedStateMachine):
         self.log.append("fence " + repr({k: v for k, v in locals().items() if k not in ("self", "data")}))
         self.it.fence_wait(self.it.fence())
 
-    @precondition(lambda self: bool(self.want or self.want_raw))
+    @precondition(lambda self: bool(self.want or self.want_raw or self.want_host))
     @rule()
     def check(self):
         CALLS["check"] = CALLS.get("check", 0) + 1
@@ -198,6 +262,9 @@ class ApiModel(RuleBasedStateMachine):
         raw = self.it.download(self.raw).view(np.uint64).reshape(NSLOT, self.g.nout)
         for s, w in self.want_raw.items():
             assert np.array_equal(raw[s], w), ("raw slot", s, "\n".join(self.log[-60:]))
+        hgot = self.hout.view(np.uint32).reshape(NSLOT, self.g.nout)
+        for s, w in self.want_host.items():
+            assert np.array_equal(hgot[s], w), ("host slot", s, "\n".join(self.log[-60:]))
 
     @invariant()
     def pending_matches(self):
@@ -213,3 +280,4 @@ def test_api_model(gpu):
         suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large]))
     print("api model calls:", dict(sorted(CALLS.items())))
     assert CALLS.get("check", 0) >= 10 and CALLS.get("integrate_n", 0) >= 10
+    assert CALLS.get("finish_async_host", 0) >= 5 and CALLS.get("unregister", 0) >= 5
