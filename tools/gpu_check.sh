@@ -15,6 +15,12 @@ export DADA_HOLDER_IDLE_S=900
 OUT=gpurun_out
 mkdir -p "$OUT"
 STEPS=${*:-smoke tests bench prof}
+# the libraries must be built from the sources in the snapshot (they are
+# built here in the container, never on the box): refuse stale ones
+if ! make -q -C paf-baseband2power_amd all >/dev/null 2>&1 || ! make -q -C oracle >/dev/null 2>&1; then
+  echo "stale build: run make -C paf-baseband2power_amd all && make -C oracle before gpurun" | tee -a "$OUT/steps.log"
+  exit 2
+fi
 
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
