@@ -206,6 +206,46 @@ def test_dfdb_far_future_frames(gpu, tmp_path, case):
     assert placed == (nblk * block_ndf * nchunk - 1 if case == "corrupt_frame" else 2 * block_ndf * nchunk), log
 
 
+def test_dfdb_lagging_source_drops_late_frames_only(gpu, tmp_path):
+    """One source (chunk 0) arrives 4 blocks behind the others.  Its frames
+    are more than one block late when they arrive, so paf_dfdb drops them,
+    as the capture drops late frames (capture.c:464-531) -- and they must
+    not hold its read-ahead back: before round 5 every batch's lowest block
+    stayed 4 blocks back, the 6 batch slots overflowed and the oldest batch,
+    holding most of the current block, was evicted (advisor, round 4).  Every
+    block comes out with every on-time frame placed and chunk 0 empty."""
+    nchunk, block_ndf, nblk, lag = 48, 16, 10, 4
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=block_ndf * 128)
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, SEED, 7, 3)
+    ref_idf, ref_sec = 1000, 27 * 40
+    dfs, chunk = npo.df_stream(payload, nchunk, ref_idf, ref_sec)
+    t = np.arange(dfs.shape[0]) // nchunk
+    arrival = t + np.where(chunk == 0, lag * block_ndf, 0)
+    order = np.argsort(arrival, kind="stable")
+    df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
+    dfs[order].tofile(df)
+    chunk[order].tofile(ck)
+    kin, kout = fresh_key(), fresh_key()
+    sp, log = _run_chain(tmp_path, kin, kout,
+                         [os.path.join(BIN, "paf_dfdb"), "-a", f"{kin:x}", "-b", HDR, "-c", str(df),
+                          "-k", str(ck), "-n", str(nchunk), "-x", str(ref_idf), "-s", str(ref_sec)],
+                         "bmf", g.nout, 3, g.block_bytes)
+    assert sp.shape[0] == nblk, log[-800:]
+    placed = [int(x) for x in re.findall(r"block \d+: (\d+) of", log)]
+    on_time = (nchunk - 1) * block_ndf
+    assert len(placed) == nblk and all(p >= on_time for p in placed), (placed, log[-800:])
+    assert "dropped for want of slots" not in log, log[-800:]
+    on_time_only = chunk != 0
+    idf = ref_idf
+    for b in range(nblk - lag):  # the late source's frames of these blocks all came > 1 block late
+        assert placed[b] == on_time, (b, placed)
+        want = np.zeros(g.block_bytes, np.uint8)
+        co.assemble(dfs[on_time_only], chunk[on_time_only], idf, ref_sec, want, block_ndf, nchunk)
+        assert np.array_equal(sp[b].view(np.uint32), co.power(g, want, nthreads=8).view(np.uint32)), b
+        idf += block_ndf
+
+
 @pytest.mark.parametrize("device", [0, -1])  # GPU-resident ring, and a host ring for contrast
 def test_replay_reuses_blocks(gpu, tmp_path, device):
     g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=256, nsamp_int=1 << 14)

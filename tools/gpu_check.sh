@@ -195,6 +195,13 @@ for s in $STEPS; do
     debughunt) # the host-staging property under the debug library, 1500 examples, seed 777
                run debug_staging_hunt 900 python3 -u tests/debug_build_checks.py staging 1500 777 ;;
     devleak20) run devring_leak20 900 python3 tools/devring_probe.py 20 use ;;
+    hunt5) # round 5's host-memory rules at scale, fresh seeds: the ABI state machine (registration,
+           # host-output finishes, unregister drains) and the host-staging property (release library)
+           run hunt5_api 900 env B2P_HYPOTHESIS_SCALE=20 B2P_HYPOTHESIS_SEED=5151 python3 -u -m pytest \
+             tests/test_gpu_api_model.py -v -s --timeout 800 --timeout-method thread --hypothesis-show-statistics &&
+           run hunt5_staging 900 env B2P_HYPOTHESIS_SCALE=20 B2P_HYPOTHESIS_SEED=5152 python3 -u -m pytest \
+             tests/test_gpu_random_layouts.py -k staging -v --timeout 800 --timeout-method thread \
+             --hypothesis-show-statistics ;;
     cpuwait) # the CPU baseline's thread count and OpenMP wait policy: spread and throttling
              run cpu_wait_a 300 python3 tools/cpu_spread_probe.py 5 \
                spread2:15:passive,spread2:15:default,spread2:15:active,spread2:14:passive,spread2:12:passive &&
