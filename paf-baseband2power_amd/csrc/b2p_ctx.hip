@@ -507,12 +507,23 @@ int b2p_register_host(b2p_ctx_t *c, void *base, size_t bytes) {
   return B2P_OK;
 }
 
+static int flush_pending(b2p_ctx_t *c);
+
 // Release a registration once no copy of this context can still read or
-// write the range: the context's streams are drained first (a host finish
-// may still be landing in it; a failed push's copies were drained by
-// b2p_push).  Work the caller enqueued on other contexts or streams that
-// touches the range must be complete before this call.
+// write the range: a deferred finalize (b2p_finish_async into host memory
+// that no launch has carried yet) is enqueued first, then the context's
+// streams are drained (a host finish may still be landing in the range; a
+// failed push's copies were drained by b2p_push).  Found by the ABI state
+// machine (tests/test_gpu_api_model.py): without the flush, a spectrum
+// finished into the range was copied only at the next sync -- after the
+// caller had unregistered, and possibly freed, it.  Work the caller
+// enqueued on other contexts or streams that touches the range must be
+// complete before this call.
 static int unregister_locked(b2p_ctx_t *c, const char *base) {
+  if (!c->failed && c->pend.valid) {
+    const int rf = flush_pending(c);
+    if (rf != B2P_OK) return rf;
+  }
   if (c->stream) CK(c, hipStreamSynchronize(c->stream));
   if (c->copy_stream) CK(c, hipStreamSynchronize(c->copy_stream));
   CK(c, hipHostUnregister(const_cast<char *>(base)));
