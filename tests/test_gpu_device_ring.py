@@ -54,6 +54,13 @@ def _wait(procs, timeout=300):
             p.wait()
     errs = [p.stderr.read().decode(errors="replace") for p in procs]
     msgs = [f"{os.path.basename(p.args[0])} rc={p.returncode}: {e[-600:]}" for p, e in zip(procs, errs)]
+    if bad:  # the stage logs to <-c dir>/paf_baseband2power.log, not stderr
+        for p in procs:
+            a = list(p.args)
+            if os.path.basename(a[0]) == "paf_baseband2power" and "-c" in a:
+                log = os.path.join(a[a.index("-c") + 1], "paf_baseband2power.log")
+                if os.path.exists(log):
+                    msgs.append("stage log: " + open(log, errors="replace").read()[-2000:])
     assert not bad, "\n".join(msgs)
     return errs
 

@@ -7,7 +7,7 @@
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 #          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4 pmc1
-#          devleak devleak20 replay9090 debughunt hunt5 cpuwait
+#          devleak devleak20 replay9090 debughunt hunt5 cpuwait gatherhunt
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -202,6 +202,11 @@ for s in $STEPS; do
            run hunt5_staging 900 env B2P_HYPOTHESIS_SCALE=20 B2P_HYPOTHESIS_SEED=5152 python3 -u -m pytest \
              tests/test_gpu_random_layouts.py -k staging -v --timeout 800 --timeout-method thread \
              --hypothesis-show-statistics ;;
+    gatherhunt) # the gathered C stage on GPU-resident rings (paf_diskdb writers), fresh seed, scale 5;
+                # a failing stage's log is in the assertion (tests/test_gpu_device_ring.py _wait)
+                run gather_hunt 900 env B2P_HYPOTHESIS_SEED=6161 B2P_HYPOTHESIS_SCALE=5 python3 -u -m pytest \
+                  tests/test_gpu_stage_random.py -v -rf --timeout 800 --timeout-method thread \
+                  -k "gathered_subbands and not inproc" --hypothesis-show-statistics ;;
     cpuwait) # the CPU baseline's thread count and OpenMP wait policy: spread and throttling
              run cpu_wait_a 300 python3 tools/cpu_spread_probe.py 5 \
                spread2:15:passive,spread2:15:default,spread2:15:active,spread2:14:passive,spread2:12:passive &&
