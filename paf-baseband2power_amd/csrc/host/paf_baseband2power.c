@@ -30,6 +30,7 @@
  * (libpafdada extensions) are then off, and blocks are pinned when first
  * seen.
  */
+#include <errno.h>
 #include <getopt.h>
 #include <inttypes.h>
 #include <pthread.h>
@@ -342,9 +343,17 @@ typedef struct worker_t {
 static int write_output(shared_t *sh, const float *spec) {
   uint64_t bid;
   char *o = ipcio_open_block_write(sh->out->data_block, &bid);
-  if (!o) return -1;
+  if (!o) {
+    multilog(sh->log, LOG_ERR, "output block %" PRIu64 ": ipcio_open_block_write failed (%s)", sh->nblocks,
+             strerror(errno));
+    return -1;
+  }
   memcpy(o, spec, sh->obytes);
-  ipcio_close_block_write(sh->out->data_block, sh->obytes);
+  if (ipcio_close_block_write(sh->out->data_block, sh->obytes) < 0) {
+    multilog(sh->log, LOG_ERR, "output block %" PRIu64 ": ipcio_close_block_write failed (%s)", sh->nblocks,
+             strerror(errno));
+    return -1;
+  }
   sh->nblocks++;
   sh->t_last = now_s();
   if (sh->nblocks == kWarm) sh->t_warm = sh->t_last;
@@ -1096,7 +1105,10 @@ int main(int argc, char *argv[]) {
   {
     char *ohdr = ipcbuf_get_next_write(out->header_block);
     uint64_t ohsz = ipcbuf_get_bufsz(out->header_block);
-    if (!ohdr) goto done;
+    if (!ohdr) {
+      multilog(log, LOG_ERR, "output header block: ipcbuf_get_next_write failed (%s)", strerror(errno));
+      goto done;
+    }
     memset(ohdr, 0, ohsz);
     memcpy(ohdr, sub[0].hdr, sub[0].hdr_size < ohsz ? sub[0].hdr_size : ohsz);
     ohdr[ohsz - 1] = 0;
@@ -1122,7 +1134,10 @@ int main(int argc, char *argv[]) {
     ascii_header_del(ohdr, "NSAMP_DF");
     ascii_header_del(ohdr, "BYTE_ORDER");
 #endif
-    if (ipcbuf_mark_filled(out->header_block, ohsz) < 0) goto done;
+    if (ipcbuf_mark_filled(out->header_block, ohsz) < 0) {
+      multilog(log, LOG_ERR, "output header block: ipcbuf_mark_filled failed (%s)", strerror(errno));
+      goto done;
+    }
   }
 
   sh.bmax = 1;
@@ -1149,16 +1164,24 @@ int main(int argc, char *argv[]) {
     const size_t hb = ((sh.gather_dev ? 3 : 1) * sh.bmax * sh.obytes + 4095) / 4096 * 4096;
     sh.spec_host = aligned_alloc(4096, hb);
     sh.stage = malloc(sh.obytes);
-    if (!sh.spec_host || !sh.stage) goto done;
-    b2p_register_host(sub[0].ctx, sh.spec_host, hb);
+    if (!sh.spec_host || !sh.stage) {
+      multilog(log, LOG_ERR, "cannot allocate %zu B of output staging", hb);
+      goto done;
+    }
+    if (b2p_register_host(sub[0].ctx, sh.spec_host, hb) != B2P_OK) /* the copies still work, unpinned */
+      multilog(log, LOG_WARNING, "output staging not pinned: %s", b2p_last_error(sub[0].ctx));
   }
   if (split) {
     for (int r = 0; r < nmem; r++)
-      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].part_dev, info.nout * sizeof(uint64_t)) != B2P_OK)
+      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].part_dev, info.nout * sizeof(uint64_t)) != B2P_OK) {
+        multilog(log, LOG_ERR, "member %d: b2p_dev_alloc: %s", r, b2p_last_error(sub[r].ctx));
         goto done;
+      }
     if (b2p_dev_alloc(sub[0].ctx, (void **)&sub[0].spec_dev, info.nout * sizeof(float)) != B2P_OK ||
-        b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_sum, info.nout * sizeof(uint64_t)) != B2P_OK)
+        b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_sum, info.nout * sizeof(uint64_t)) != B2P_OK) {
+      multilog(log, LOG_ERR, "b2p_dev_alloc: %s", b2p_last_error(sub[0].ctx));
       goto done;
+    }
     b2p_ctx_t *ctxs[MAX_SUB];
     for (int r = 0; r < nmem; r++) ctxs[r] = sub[r].ctx;
     const int mode = group_mode(&conf, dup_dev, log);
@@ -1173,9 +1196,15 @@ int main(int argc, char *argv[]) {
              mode ? "peer copies (shared device)" : "RCCL ncclReduce");
   } else if (sh.grouped) {
     for (int r = 0; r < conf.nsub; r++)
-      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, 3 * sh.bmax * info.nout * sizeof(float)) != B2P_OK)
+      if (b2p_dev_alloc(sub[r].ctx, (void **)&sub[r].spec_dev, 3 * sh.bmax * info.nout * sizeof(float)) !=
+          B2P_OK) {
+        multilog(log, LOG_ERR, "sub-band %d: b2p_dev_alloc: %s", r, b2p_last_error(sub[r].ctx));
         goto done;
-    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, 3 * sh.bmax * sh.obytes) != B2P_OK) goto done;
+      }
+    if (b2p_dev_alloc(sub[0].ctx, (void **)&sh.root_dev, 3 * sh.bmax * sh.obytes) != B2P_OK) {
+      multilog(log, LOG_ERR, "b2p_dev_alloc: %s", b2p_last_error(sub[0].ctx));
+      goto done;
+    }
     b2p_ctx_t *ctxs[MAX_SUB];
     for (int r = 0; r < conf.nsub; r++) ctxs[r] = sub[r].ctx;
     const int mode = group_mode(&conf, dup_dev, log);
