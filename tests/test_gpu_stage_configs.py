@@ -1,4 +1,5 @@
-"""The drop-in C stage at the BASELINE multi-sub-band sizes.
+"""The drop-in C stage at the BASELINE multi-sub-band sizes (and configs[0]
+from a file, last test).
 
 configs[3] (4 sub-bands x 256 ch x 2 pol int8) and configs[4] (8 sub-bands x
 1024 ch x 2 pol int8) run through `paf_baseband2power -n N`, the process the
@@ -100,3 +101,50 @@ def test_c_stage_gathers_full_size_subbands(gpu, tmp_path, nsub, nchan):
         scratch.free()
     # distinct sub-bands really are distinct (a mixed-up gather would show)
     assert len({sp[0, r].tobytes() for r in range(nsub)}) == nsub
+
+
+def test_c_stage_configs0_file_through_host_ring(gpu, tmp_path):
+    """configs[0], the reference's own CPU-runnable case, through the GPU
+    drop-in: a DADA file of two full 1024x1024-sample integrations (256 ch x
+    2 pol int8, 1 GiB each) and half of a third -> `paf_diskdb` -> a HOST
+    ring of 1 GiB blocks (paf-baseband2power.py:114's shape) -> the stage
+    (push from the registered ring block through the staging chunks) ->
+    `paf_dbdisk`.  Both spectra equal the C oracle's of the file's bytes, bit
+    for bit; the half integration at the end of the file is skipped."""
+    g = npo.Geom(nbit=8, nchan_chunk=256, nsamp_int=1 << 20)   # 1 GiB
+    nblk = 2
+    payload = co.fill_synthetic(g, nblk * g.block_bytes + g.block_bytes // 2, SEED, 0, 0)
+    src = tmp_path / "c1.dada"
+    dada.write_dada_file(str(src), "FILE_HEADER_IS_SKIPPED 1\n", payload)
+    want = [co.power(g, payload[b * g.block_bytes:(b + 1) * g.block_bytes], nthreads=16) for b in range(nblk)]
+    del payload
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text("HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 256\nTSAMP 0.84375\n")
+    kin, kout = fresh_key(), fresh_key()
+    dada.create_ring(kin, 2, g.block_bytes)
+    dada.create_ring(kout, 4, g.nout * 4)
+    out = tmp_path / "power.dada"
+    procs = []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b", f"{kout:x}",
+                                   "-c", str(tmp_path), "-d", "0", "-f", "int8:256"], stderr=subprocess.PIPE),
+                 subprocess.Popen([os.path.join(BIN, "paf_diskdb"), "-a", f"{kin:x}", "-b", str(tmp_path), "-c",
+                                   "c1.dada", "-d", str(hdr), "-e", "1", "-T", "4"], stderr=subprocess.PIPE)]
+        _wait(procs, timeout=300)
+        ohdr, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+    log = open(str(tmp_path / "paf_baseband2power.log")).read()
+    sp = data.view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == nblk, log[-800:]
+    for b in range(nblk):
+        assert np.array_equal(sp[b], want[b].view(np.uint32)), b
+    assert "partial integration skipped" in log and f"FINISH PAF_PROCESS: {nblk} integrations" in log, log[-800:]
+    assert dada.header_get(ohdr, "NBIT", "%d") == 32 and dada.header_get(ohdr, "NCHAN", "%d") == 256
