@@ -281,6 +281,17 @@ static void pin_block(sub_t *s, char *blk, multilog_t *log) {
   s->pinned[s->npinned++] = blk;
 }
 
+/* A failed run also names its errors on stderr (the reference's errors go
+ * there, paf_baseband2power.cu:51-52): this run's ERR lines of the log. */
+static void echo_errors(FILE *fp, long from, const char *fname) {
+  char line[1200];
+  fflush(fp);
+  if (from < 0 || fseek(fp, from, SEEK_SET) != 0) return;
+  while (fgets(line, sizeof line, fp))
+    if (strstr(line, "] ERR: ")) fprintf(stderr, "paf_baseband2power: %s", line);
+  fprintf(stderr, "paf_baseband2power: FAILED, log %s\n", fname);
+}
+
 /* next input block, or NULL at the end of the transfer (checked with
  * ipcbuf_eod first, so a reader never waits on a ring whose transfer ended) */
 static char *next_block(dada_hdu_t *h, uint64_t *bytes) {
@@ -961,6 +972,8 @@ int main(int argc, char *argv[]) {
     fprintf(stderr, "Can not open log file %s\n", log_fname);
     return EXIT_FAILURE;
   }
+  fseek(fp_log, 0, SEEK_END);
+  const long log_start = ftell(fp_log); /* this run's lines start here */
   multilog_t *log = multilog_open("paf_baseband2power", 0);
   multilog_add(log, fp_log);
   multilog(log, LOG_INFO, "START PAF_PROCESS");
@@ -1295,6 +1308,7 @@ done:
            sh.nblocks > kWarm ? sh.t_last - sh.t_warm : 0.0,
            sh.nblocks > kWarm ? sh.nblocks - kWarm : (uint64_t)0);
   multilog_close(log);
+  if (status != EXIT_SUCCESS) echo_errors(fp_log, log_start, log_fname);
   fclose(fp_log);
   return status;
 }
