@@ -169,3 +169,18 @@ def test_stage_orchestration_random(stages, tmp_path_factory, case):
     assert f"FINISH PAF_PROCESS: {n} integrations" in log, (case, log[-600:])
     if len(set(nblks)) == 1:  # (the GPU-resident gather also logs the longer transfer's unmatched block)
         assert ("partial integration skipped" in log) == case["short"], (case, log[-600:])
+
+
+def test_failed_stage_names_its_errors_on_stderr(stages, tmp_path):
+    """a run that fails (here: no input ring at the key) exits 1 and repeats
+    this run's ERR log lines on stderr, as the reference reports errors
+    there (paf_baseband2power.cu:51-52); earlier runs' lines in the same
+    log file are not repeated"""
+    (tmp_path / "paf_baseband2power.log").write_text("[earlier] ERR: an earlier run's error\n")
+    k = _key()
+    dada.destroy_ring(k)
+    r = subprocess.run([stages["host"], "-a", f"{k:x}", "-b", f"{k + 2:x}", "-c", str(tmp_path), "-d", "0",
+                        "-f", "int8:256"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1
+    assert f"ERR: cannot attach/lock input ring {k:x}" in r.stderr, r.stderr
+    assert "FAILED, log" in r.stderr and "earlier run" not in r.stderr, r.stderr
