@@ -132,6 +132,10 @@ def parse(argv=None):
                     help="when the headline batches queued blocks, also time this long of regions "
                          "with ONE block per launch (the real-time stage's launch shape) and report "
                          "it beside the headline (0 disables)")
+    ap.add_argument("--bmf-seconds", type=float, default=2.0,
+                    help="with the default configs[1] workload at one rank, also time this long of the "
+                         "reference-native BMF layout (int16 BE TFTFP, 336 ch, 2.625 GiB) and report it as "
+                         "`secondary.bmf`, verified against the oracle (0 disables)")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="seconds one multi-rank phase (rendezvous, first collective, a timed "
                          "region, verification) may take; past it the rank exits 4 naming it")
@@ -342,6 +346,94 @@ def synthetic_reader(geom_dict: dict, subband: int, block: int, threads: int):
     def rd(off, n):
         return co.fill_synthetic(g, n, SEED, subband, block, elem0=off // esz)
     return rd
+
+
+def bmf_leg(dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
+    """The reference-native layout beside the headline (the
+    BMF-native parity/drop-in run): 336 channels int16 big-endian TFTFP
+    (capture.h:20,28; paf-baseband2power.conf:2-9), one 2.625 GiB
+    integration per block, NBLOCKS rotating HBM-resident blocks, one block
+    per integrate launch (floor(4 GiB / 2.625 GiB) = 1, the stage's rule).
+    A region is NBLOCKS integrations bracketed by device syncs; regions
+    repeat for `seconds`; the last region's spectra are checked against the
+    C oracle bit for bit.  Algorithmic bytes: 4 B per complex dual-pol
+    sample, the block per launch."""
+    import numpy as np
+
+    import paf_b2p
+    from paf_b2p.geometry import CONFIGS, samples_per_block
+    geom = CONFIGS["bmf"]["geom"]()
+    gd = {f: int(getattr(geom, f)) for f, _ in geom._fields_ if f != "reserved"}
+    it = paf_b2p.Integrator(geom, device=dev)
+    nout, bb, K = it.nout, it.block_bytes, NBLOCKS
+    blocks = []
+    try:
+        for b in range(K):
+            d = it.alloc(bb)
+            it.fill_synthetic(d, SEED, 0, b)
+            blocks.append(d)
+        out = it.alloc(K * nout * 4)
+        it.sync()
+
+        def region():
+            it.sync()
+            t0 = time.perf_counter()
+            it.set_timing(2)
+            for k in range(K):
+                it.integrate(blocks[k], out.ptr + k * nout * 4, True)
+            it.set_timing(0)
+            it.sync()
+            return time.perf_counter() - t0
+
+        region()  # warm-up region
+        it.reset_stats()
+        els = [region()]
+        while sum(els) < seconds and len(els) < 100000:
+            els.append(region())
+        st = it.stats()
+        ok = None
+        if verify:
+            spec = it.download(out, nbytes=K * nout * 4).view(np.float32).reshape(K, nout)
+            ok = True
+            for k in range(K):
+                def rd(off, n, blk=blocks[k]):
+                    return it.download(blk, nbytes=n, offset=off)
+                ref = oracle_spectrum(gd, rd, bb, vthreads)
+                ok &= bool(np.array_equal(spec[k].view(np.uint32), ref.view(np.uint32)))
+        el = statistics.median(els)
+        kern_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
+        per_launch = st["bytes"] / max(st["launches"], 1)
+        achieved = per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
+        traffic, src, prov = pmc_traffic("bmf", per_launch)
+        return {
+            "workload": (f"reference-native BMF: {paf_b2p.geometry.nchan(geom)} ch x 2 pol int16 BE TFTFP "
+                         f"(48 chunks x 7 ch, 128 samples per frame), {bb} B per integration, {K} rotating "
+                         "HBM-resident blocks, 1 block per integrate launch"),
+            "value": round(samples_per_block(geom) / (el / K) / 1e6, 1),
+            "unit": "Msamples/s",
+            "ms_per_step": round(el / K * 1e3, 4),
+            "timed_regions": len(els),
+            "timed_seconds": round(sum(els), 4),
+            "verified": ok,
+            "verification": f"every spectrum of the last region ({K}) against the C oracle of its block, bit for bit",
+            "roofline": {
+                "bound": "hbm", "kernel": "b2p_integrate_kernel<..., MULTI=false> (int16 BE)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac_of_value": round(bb / (el / K) / 1e9 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": int(per_launch),
+                "bytes_per_sample": 4,
+                "avg_launch_us": round(kern_s * 1e6, 2),
+                "launches_timed": int(st["launches"]),
+                "traffic": traffic, "traffic_source": src, "traffic_provenance": prov,
+                "timing": ("frac: HIP events bracketing each region's launches (finalizes included); "
+                           "frac_of_value: the host-timed median region"),
+            },
+        }
+    finally:
+        for d in blocks:
+            d.free()
+        it.close()
 
 
 # --------------------------------------------------------------------------
@@ -859,6 +951,11 @@ def main(argv=None) -> int:
                            "pinned-host staging copies overlapped with the integrate launches); peak: "
                            "peak_source, the bare H2D stream of the same bytes in the same run"),
             })
+        if world == 1 and not split and a.config == "c2" and a.bmf_seconds > 0:
+            # the layout the drop-in serves, in the driver's own record
+            res["secondary"] = {"bmf": bmf_leg(dev, a.bmf_seconds, max(1, cpu_threads()), not a.no_verify)}
+            if res["secondary"]["bmf"]["verified"] is False:
+                res["verified"] = verified = False
         if world == 1 and a.cpu_seconds > 0 and not host_mode:
             res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)
         print(json.dumps(res), flush=True)

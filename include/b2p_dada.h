@@ -257,6 +257,24 @@ int dada_db_create_work(key_t key, uint64_t nbufs, uint64_t bufsz, unsigned n_re
                         uint64_t hdr_nbufs, uint64_t hdr_bufsz, int device_id);
 int dada_db_destroy(key_t key);
 
+/* Extension: the holder of a GPU-resident ring, read from block 0's segment
+ * without opening any block (dada_db -g; SURVEY.md 8f rank 3 -- PSRDADA's
+ * ipc_alloc_cuda has no holder to ask).  export_retries counts ring blocks
+ * whose HIP IPC export was refused once and exported after a retry (0 on a
+ * healthy ring; the GPU tests assert it for every ring they make);
+ * primer_refused is 1 when the holder's first allocation -- a 2 MiB primer
+ * no block uses -- was refused export (counted, harmless).  0, or -1 with
+ * errno ENOENT (no ring / no holder record) or ENODEV (a host ring). */
+typedef struct {
+  int device;
+  int holder_pid;
+  int holder_state; /* 0 starting, 1 serving, 2 gone (blocks freed) */
+  int importers;    /* processes with the blocks open, as the holder last counted */
+  int export_retries;
+  int primer_refused;
+} dada_device_info_t;
+int dada_device_ring_info(key_t key, dada_device_info_t *info);
+
 /* ---- ASCII header (ascii_header_set at capture.c:758-778) ---- */
 /* returns the number of items scanned (>= 1), or -1 if the key is absent */
 int ascii_header_get(const char *header, const char *keyword, const char *format, ...)

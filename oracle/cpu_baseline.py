@@ -345,8 +345,14 @@ def run(geom: dict, seconds: float, seed: int, one_thread: bool = True, isa: str
     nodes = numa_nodes()
     used_nodes = sorted({n for n, c in nodes.items() for p in places if p in c})
     ln = leg(r_n, el_n, thr_n)
+    quota = host.get("cgroup_cpus")
     return {
         "value": ln["value"], "unit": "Msamples/s", "cores": threads,
+        # what `cores` is: the job's CPU share of a shared host, not the host
+        "cores_scope": (f"{threads} threads = this job's cgroup CPU quota ({quota:g} CPUs, cpu.max) less one, "
+                        f"on a {host.get('logical_cpus')}-logical-CPU host shared with other jobs: the "
+                        "baseline is bound by the quota, not by the host's cores" if quota else
+                        f"{threads} threads: every CPU this process may use, less one (no cgroup quota)"),
         "kind": "port",          # the contract's two kinds: "reference" | "port"
         "port": "tuned (oracle/b2p_cpu_port.c), not the scalar checker",
         "isa": used,

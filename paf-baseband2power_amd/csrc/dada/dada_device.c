@@ -112,12 +112,14 @@ static void report(int fd, const char *what, int code) {
 #define DEV_ALLOC_ALIGN (2ull << 20)
 #define DEV_EXPORT_TRIES 4
 
-/* processes attached to block 0's segment besides the holder and the
- * destroyers that only wait for it: the importers (dada_internal.h) */
-static long importers_attached(int seg0_id, const dev_seg_t *seg0) {
+/* processes attached to block 0's segment besides the holder: the importers
+ * (dada_internal.h).  A destroyer's momentary look (dev_stop_holder) can only
+ * add to the count, so a race makes the holder wait a tick longer, never
+ * free blocks an importer still has open. */
+static long importers_attached(int seg0_id) {
   struct shmid_ds ds;
   if (shmctl(seg0_id, IPC_STAT, &ds) < 0) return 0; /* gone: nobody can be attached */
-  const long n = (long)ds.shm_nattch - 1 - __atomic_load_n(&seg0->stop_waiters, __ATOMIC_ACQUIRE);
+  const long n = (long)ds.shm_nattch - 1;
   return n > 0 ? n : 0;
 }
 
@@ -237,6 +239,8 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
   for (int j = 0; j < nspare; j++) hip.free_(spare[j]);
   hip.sync();
   seg0->holder_pid = (int32_t)getpid();
+  seg0->export_retries = retries;
+  seg0->primer_refused = primer_refused;
   __atomic_store_n(&seg0->holder_state, 1, __ATOMIC_RELEASE);
   char ready[300];
   /* 'R' + export retries of ring blocks, 'P' + 1 if the primer's export was refused */
@@ -259,7 +263,7 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
     if (sigtimedwait(&set, NULL, &tick) > 0) stopping = 1;
     struct shmid_ds ds;
     if (shmctl(id->syncid, IPC_STAT, &ds) < 0 || (ds.shm_perm.mode & SHM_DEST)) stopping = 1; /* ring removed */
-    const long others = importers_attached(seg0_id, seg0);
+    const long others = importers_attached(seg0_id);
     __atomic_store_n(&seg0->importers, (int32_t)others, __ATOMIC_RELEASE);
     if (!stopping) {
       idle = others == 0 ? idle + 1 : 0;
@@ -333,33 +337,39 @@ int dev_create_blocks(ipcbuf_t *id, int device) {
   return -1;
 }
 
-int dev_stop_holder(dev_seg_t *seg0) {
-  if (seg0->holder_pid <= 0 || __atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) != 1) return 0;
-  /* this process stays attached to block 0's segment only to watch the
-   * holder's state: it says so, so the holder does not wait for it */
-  __atomic_add_fetch(&seg0->stop_waiters, 1, __ATOMIC_ACQ_REL);
-  int rc = 0;
-  if (kill(seg0->holder_pid, SIGTERM) < 0) {
-    rc = errno == ESRCH ? 0 : -1;
-  } else {
-    rc = -1;
-    for (int i = 0; i < 1000; i++) { /* <= 10 s for the holder to free the blocks */
-      if (__atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE) == 2) {
-        rc = 0;
-        break;
-      }
-      struct timespec t = {0, 10 * 1000 * 1000};
-      nanosleep(&t, NULL);
-    }
-    if (rc) {
-      snprintf(dev_err, sizeof dev_err,
-               "device ring holder %d: %d process(es) still have the blocks open; it frees them when they detach",
-               seg0->holder_pid, __atomic_load_n(&seg0->importers, __ATOMIC_ACQUIRE));
-      errno = EBUSY;
-    }
+/* one look at block 0's segment, attached only for the look (the holder
+ * counts attachments as importers): 0, or -1 once the segment is gone */
+int dev_look_seg0(int seg0_id, dev_seg_t *out) {
+  const dev_seg_t *seg0 = shmat(seg0_id, NULL, SHM_RDONLY);
+  if (seg0 == (void *)-1) return -1;
+  memcpy(out->handle, seg0->handle, sizeof out->handle);
+  out->holder_pid = seg0->holder_pid;
+  out->holder_state = __atomic_load_n(&seg0->holder_state, __ATOMIC_ACQUIRE);
+  out->importers = __atomic_load_n(&seg0->importers, __ATOMIC_ACQUIRE);
+  out->export_retries = seg0->export_retries;
+  out->primer_refused = seg0->primer_refused;
+  shmdt(seg0);
+  return 0;
+}
+
+int dev_stop_holder(int seg0_id) {
+  dev_seg_t v;
+  if (dev_look_seg0(seg0_id, &v) < 0 || v.holder_pid <= 0 || v.holder_state != 1) return 0;
+  if (kill(v.holder_pid, SIGTERM) < 0) return errno == ESRCH ? 0 : -1;
+  /* the holder frees the blocks once no importer is attached; this process
+   * looks every 10 ms and stays attached for no longer than each look, so
+   * dying while it waits (Ctrl-C on dada_db -d, a test timeout) leaves the
+   * holder's count as it was */
+  for (int i = 0; i < 1000; i++) { /* <= 10 s */
+    struct timespec t = {0, 10 * 1000 * 1000};
+    nanosleep(&t, NULL);
+    if (dev_look_seg0(seg0_id, &v) < 0 || v.holder_state == 2) return 0;
   }
-  __atomic_sub_fetch(&seg0->stop_waiters, 1, __ATOMIC_ACQ_REL);
-  return rc;
+  snprintf(dev_err, sizeof dev_err,
+           "device ring holder %d: %d process(es) still have the blocks open; it frees them when they detach",
+           v.holder_pid, v.importers);
+  errno = EBUSY;
+  return -1;
 }
 
 int dev_open_blocks(ipcbuf_t *id) {

@@ -91,16 +91,28 @@ static inline size_t sync_size(uint64_t nbufs) { return sizeof(ipcsync_t) + 5 * 
  * the blocks' IPC handles stays attached to block 0's segment until it has
  * closed them (free_local: dev_close_blocks, then shmdt), and the holder
  * frees the blocks only once no such process is attached -- counted by the
- * kernel as shm_nattch of block 0's segment, less the holder itself and the
- * destroyers waiting for it (stop_waiters).  A killed importer detaches
- * when it dies, so the count needs no cooperation to come down. */
+ * kernel as shm_nattch of block 0's segment, less the holder itself.  A
+ * killed importer detaches when it dies, so the count needs no cooperation
+ * to come down; and nothing else stays attached: a destroyer attaches only
+ * for a moment per look at the holder's state (dev_stop_holder), so a
+ * destroyer that dies mid-wait leaves nothing behind, and a look that
+ * meets the holder's count makes it wait one more tick, never free early.
+ *
+ * The holder also records how its IPC exports went (dada_device_ring_info):
+ * export_retries -- ring blocks whose first export was refused and that
+ * were exported after a retry (0 expected; a test asserts it); and
+ * primer_refused -- its first allocation, the 2 MiB primer no block uses,
+ * was refused (the refusal that probes saw on first allocations, counted,
+ * allowed). */
 #define DEV_HANDLE_BYTES 64
 typedef struct {
   unsigned char handle[DEV_HANDLE_BYTES];
   int32_t holder_pid;
-  int32_t holder_state; /* 0 starting, 1 serving, 2 gone */
-  int32_t stop_waiters; /* destroyers attached here only to wait for the holder */
-  int32_t importers;    /* last count the holder saw (diagnostics) */
+  int32_t holder_state;   /* 0 starting, 1 serving, 2 gone */
+  int32_t importers;      /* last count the holder saw (diagnostics) */
+  int32_t export_retries; /* ring blocks exported only after a retry */
+  int32_t primer_refused; /* 1: the primer allocation's export was refused */
+  int32_t reserved;
 } dev_seg_t;
 
 /* dada_device.c: HIP reached through dlopen, so libpafdada loads without ROCm */
@@ -108,10 +120,14 @@ typedef struct {
 uint64_t ipcbuf_view_position(const ipcbuf_t *id);
 
 int dev_create_blocks(ipcbuf_t *id, int device); /* fork the holder, fill the handles */
-/* stop the holder and wait (<= 10 s) until it has freed the blocks; -1 with
- * errno EBUSY (text in dada_device_error) while importers stay attached --
- * the holder then frees the blocks when the last one detaches */
-int dev_stop_holder(dev_seg_t *seg0);
+/* stop the holder of the ring whose block 0 is segment seg0_id and wait
+ * (<= 10 s) until it has freed the blocks; -1 with errno EBUSY (text in
+ * dada_device_error) while importers stay attached -- the holder then frees
+ * the blocks when the last one detaches */
+int dev_stop_holder(int seg0_id);
+/* copy block 0's segment, attached read-only for the copy only; -1 once the
+ * segment is gone */
+int dev_look_seg0(int seg0_id, dev_seg_t *out);
 int dev_open_blocks(ipcbuf_t *id);
 void dev_close_blocks(ipcbuf_t *id);
 int dev_copy(void *dst, const void *src, uint64_t n); /* hipMemcpyDefault */

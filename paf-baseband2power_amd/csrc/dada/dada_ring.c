@@ -257,9 +257,13 @@ static void free_local(ipcbuf_t *id) {
 static void remove_ipc(ipcbuf_t *id) {
   ipcsync_t *s = id->sync;
   if (s->on_device_id >= 0 && id->shm_addr && id->shm_addr[0]) {
-    /* this process's own handles first (the ordering rule, dada_internal.h) */
+    /* this process's own handles first, then its attachment to block 0's
+     * segment, which the holder would count as an importer (the ordering
+     * rule, dada_internal.h) */
     if (id->buffer) dev_close_blocks(id);
-    dev_stop_holder(id->shm_addr[0]);
+    shmdt(id->shm_addr[0]);
+    id->shm_addr[0] = NULL;
+    if (id->shmid) dev_stop_holder(id->shmid[0]);
   }
   for (uint64_t i = 0; id->shmid && i < s->nbufs; i++)
     if (id->shmid[i] >= 0) shmctl(id->shmid[i], IPC_RMID, NULL);
@@ -1340,14 +1344,13 @@ static int ring_remove(key_t key) {
     return -1;
   }
   ipcsync_t *s = id.sync;
-  int rc = 0;
+  int rc = 0, busy = 0;
   if (s->semkey_connect == 0) rc = -1; /* not a (complete) ring */
   if (s->on_device_id >= 0) {
     const int sid = shmget(shmkey_get(&id, 0), 0, 0);
-    void *seg0 = sid >= 0 && seg_size(sid) >= sizeof(dev_seg_t) ? shmat(sid, NULL, 0) : (void *)-1;
-    if (seg0 != (void *)-1) {
-      if (dev_stop_holder(seg0) < 0) rc = -1;
-      shmdt(seg0);
+    if (sid >= 0 && seg_size(sid) >= sizeof(dev_seg_t) && dev_stop_holder(sid) < 0) {
+      rc = -1;
+      busy = errno == EBUSY; /* kept through the removals below */
     }
   }
   for (uint64_t i = 0; i < s->nbufs; i++) {
@@ -1362,6 +1365,7 @@ static int ring_remove(key_t key) {
   if (sem >= 0) semctl(sem, 0, IPC_RMID);
   shmdt(s);
   shmctl(id.syncid, IPC_RMID, NULL);
+  if (busy) errno = EBUSY; /* the holder still serves importers: not "nothing to destroy" */
   return rc;
 }
 
@@ -1371,6 +1375,36 @@ int dada_db_destroy(key_t key) {
   const int b = ring_remove(key + 1);
   if (a != 0) errno = e;
   return a == 0 && b == 0 ? 0 : -1;
+}
+
+int dada_device_ring_info(key_t key, dada_device_info_t *info) {
+  if (!info) {
+    errno = EINVAL;
+    return -1;
+  }
+  memset(info, 0, sizeof *info);
+  ipcbuf_t id = IPCBUF_INIT;
+  if (sync_get(&id, key, 0, 0) < 0) return -1;
+  const int dev = id.sync->on_device_id;
+  const key_t k0 = shmkey_get(&id, 0);
+  shmdt(id.sync);
+  if (dev < 0) {
+    errno = ENODEV; /* a host ring */
+    return -1;
+  }
+  const int sid = shmget(k0, 0, 0);
+  dev_seg_t v;
+  if (sid < 0 || seg_size(sid) < sizeof(dev_seg_t) || dev_look_seg0(sid, &v) < 0) {
+    errno = ENOENT;
+    return -1;
+  }
+  info->device = dev;
+  info->holder_pid = v.holder_pid;
+  info->holder_state = v.holder_state;
+  info->importers = v.importers;
+  info->export_retries = v.export_retries;
+  info->primer_refused = v.primer_refused;
+  return 0;
 }
 
 long fileread(const char *filename, char *buffer, unsigned bufsz) {

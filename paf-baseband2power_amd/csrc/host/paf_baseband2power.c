@@ -252,17 +252,19 @@ static int read_header(dada_hdu_t *h, char **hdr, uint64_t *size) {
 }
 
 /* ring location of an input ring's blocks: -1 host, else the HIP device */
-static int ring_device(dada_hdu_t *h) {
+static int ring_device(dada_hdu_t *h, int member_device) {
 #if DEVICE_RINGS && defined(B2P_TEST_HOST_RING_AS_DEVICE)
   /* test build only (tests/test_sanitizers.py): host rings take the
    * GPU-resident paths, driven by the CPU test double tests/c/b2p_cpu_stub.c,
-   * so their threads run under ThreadSanitizer on a machine with no GPU */
+   * so their threads run under ThreadSanitizer on a machine with no GPU;
+   * each ring counts as living on its member's device */
   (void)h;
-  return 0;
+  return member_device;
 #elif DEVICE_RINGS
+  (void)member_device;
   return ipcbuf_get_device(data_buf(h));
 #else
-  (void)h;
+  (void)h, (void)member_device;
   return -1;
 #endif
 }
@@ -392,10 +394,15 @@ static void *worker(void *arg) {
     }
     if (stop || skip) {
       if (blk) ipcio_close_block_read(s->in->data_block, bytes);
+      int whole = 0; /* a member had a whole block for a round another member's end of data stops */
+      for (int r = 0; r < sh->nsub; r++) whole |= sh->have[r] == 1;
       if (w->r == 0 && skip && !stop) {
         sh->nskipped++;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band block held %" PRIu64
                  " of %" PRIu64 " B)", bytes, s->rbufsz);
+      } else if (w->r == 0 && stop && whole && !sh->failed && !g_stop) {
+        sh->nskipped++;
+        multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
       }
       pthread_barrier_wait(&sh->bar);
       if (stop) break;
@@ -601,13 +608,23 @@ static void *worker_gather_dev(void *arg) {
     int drain = mm && !stop; /* nobody has a block queued: finish batch k now */
     for (int q = 0; q < sh->nsub; q++) drain &= sh->idle[q];
     if (r == 0) {
+      /* an integration is lost when a member's transfer ended while another
+       * had a whole block for it: taken in this round's queued loop (got >
+       * mm), or as the round's first block (have 1 in a stop round) --
+       * counted the same however the writers' timing split the blocks */
       int lost = skip && !stop;
-      for (int q = 0; q < sh->nsub; q++) lost |= (uint32_t)sh->got[q] > mm || sh->partial[q];
+      for (int q = 0; q < sh->nsub; q++)
+        lost |= (uint32_t)sh->got[q] > mm || sh->partial[q] || (stop && sh->have[q] == 1);
       if (lost) {
         sh->nskipped++;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
       }
-      if (!sh->failed && m_prev && root_gather_batch(sh, k - 1, m_prev, nfl, sh->tick, &gq[ngq++]) < 0)
+      /* batch k-1's gather, behind every member's fence of this round.  In a
+       * drain round the members go on to flush and fence batch k at once, so
+       * the root issues it after B3b instead: a gather reads each member's
+       * fence ring (b2p_group_gather_async), which b2p_fence writes -- found
+       * by ThreadSanitizer on the asynchronous CPU double (b2p_cpu_stub.c) */
+      if (!drain && !sh->failed && m_prev && root_gather_batch(sh, k - 1, m_prev, nfl, sh->tick, &gq[ngq++]) < 0)
         sh->failed = 1;
       if (mm) {
         sh->nlaunches++;
@@ -631,8 +648,9 @@ static void *worker_gather_dev(void *arg) {
       sh->tick2[r] = t2;
       pthread_barrier_wait(&sh->bar); /* B3b: every member's batch k is finalized on its stream */
       if (r == 0 && !sh->failed) {
+        if (m_prev && root_gather_batch(sh, k - 1, m_prev, nfl, sh->tick, &gq[ngq++]) < 0) sh->failed = 1;
         const int i0 = ngq;
-        if (root_gather_batch(sh, k, mm, nfl, sh->tick2, &gq[ngq++]) < 0) sh->failed = 1;
+        if (!sh->failed && root_gather_batch(sh, k, mm, nfl, sh->tick2, &gq[ngq++]) < 0) sh->failed = 1;
         /* write everything once batch k's gather is done, unless every
          * member's next block arrives first (then the rounds go on in flight) */
         while (!sh->failed && !g_stop) {
@@ -1056,7 +1074,7 @@ int main(int argc, char *argv[]) {
       multilog(log, LOG_ERR, "b2p_open: %s (%s)", b2p_strerror(rc), b2p_last_error(NULL));
       goto done;
     }
-    const int ring_dev = ring_device(s->in);
+    const int ring_dev = ring_device(s->in, s->device);
     s->ondev = ring_dev >= 0;
     if (s->ondev && split) {
       multilog(log, LOG_ERR, "-t splits host rings (one PCIe link per GPU); ring %x is on a GPU",

@@ -25,7 +25,7 @@ def dlib():
     if _dl is None:
         if not os.path.exists(DADA_LIB):
             raise ImportError(f"{DADA_LIB} not built (make -C paf-baseband2power_amd)")
-        L = C.CDLL(DADA_LIB)
+        L = C.CDLL(DADA_LIB, use_errno=True)
         P = C.c_void_p
         L.ascii_header_get.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, P]
         L.ascii_header_set.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p]
@@ -80,8 +80,15 @@ def dlib():
         L.ipcio_write.argtypes = [P, P, C.c_size_t]
         L.dada_db_create_work.argtypes = [C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint64,
                                           C.c_uint64, C.c_int]
+        L.dada_device_ring_info.argtypes = [C.c_int, C.POINTER(DeviceInfo)]
         _dl = L
     return _dl
+
+
+class DeviceInfo(C.Structure):
+    """dada_device_info_t (include/b2p_dada.h)"""
+    _fields_ = [(n, C.c_int) for n in ("device", "holder_pid", "holder_state", "importers", "export_retries",
+                                        "primer_refused")]
 
 
 class HduStruct(C.Structure):
@@ -152,9 +159,29 @@ def create_ring(key: int, nbufs: int, bufsz: int, nreaders: int = 1, hdr_nbufs: 
                            capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             raise OSError(f"dada_db {'-g %d' % device if device >= 0 else '-p'} {key:x}: {r.stderr.strip()}")
+        if device >= 0:
+            DEVICE_RINGS.append(dict(key=key, nbufs=nbufs, bufsz=bufsz, **device_ring_info(key)))
         return
     if dlib().dada_db_create(key, nbufs, bufsz, nreaders, hdr_nbufs, hdr_bufsz) != 0:
         raise OSError(C.get_errno(), f"dada_db_create {key:x}")
+
+
+# every GPU-resident ring create_ring made in this process, with its holder's
+# export record (device_ring_info) as it stood once the ring was ready: the
+# GPU tests assert export_retries == 0 for each (tests/conftest.py)
+DEVICE_RINGS: list[dict] = []
+
+
+def device_ring_info(key: int) -> dict:
+    """the holder of GPU-resident ring `key` (dada_device_ring_info): pid,
+    state (1 serving, 2 blocks freed), importers it last counted, ring
+    blocks exported only after a retry, and whether its primer allocation's
+    export was refused"""
+    info = DeviceInfo()
+    if dlib().dada_device_ring_info(key, C.byref(info)) != 0:
+        e = C.get_errno()
+        raise OSError(e, f"dada_device_ring_info {key:x}: {os.strerror(e)}")
+    return {n: getattr(info, n) for n, _ in DeviceInfo._fields_}
 
 
 def device_error() -> str:

@@ -48,3 +48,27 @@ def gpu(have_gpu):
     if not have_gpu:
         pytest.fail("gpu test selected but no HIP device is visible")
     return 0
+
+
+@pytest.fixture(autouse=True)
+def device_ring_exports_clean():
+    """every GPU-resident ring a test makes (paf_b2p.dada.create_ring,
+    device >= 0) had each of its blocks exported by the holder at the first
+    try: a ring-block export retry fails the test that made the ring.  The
+    holder's primer refusal (its first, unused allocation) is
+    allowed and counted in the session summary."""
+    from paf_b2p import dada
+    n0 = len(dada.DEVICE_RINGS)
+    yield
+    bad = [r for r in dada.DEVICE_RINGS[n0:] if r["export_retries"]]
+    assert not bad, f"device-ring block exports retried by the holder: {bad}"
+
+
+def pytest_terminal_summary(terminalreporter):
+    from paf_b2p import dada
+    rings = dada.DEVICE_RINGS
+    if rings:
+        terminalreporter.write_line(
+            f"device rings made: {len(rings)}; ring-block export retries: "
+            f"{sum(r['export_retries'] for r in rings)}; holder primer refusals: "
+            f"{sum(r['primer_refused'] for r in rings)}")

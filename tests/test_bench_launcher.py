@@ -281,3 +281,63 @@ def test_trace_legs_cuts_a_kernel_trace_by_the_bench_phases(tmp_path):
     assert out["legs"]["calibration"]["launches"] == 16
     assert abs(out["legs"]["headline"]["frac_of_8TBps"] - (4 << 30) / 596e-6 / 1e9 / 8000) < 1e-4
     assert json.dumps(out)
+
+
+@pytest.mark.parametrize("n,config,baseline", [(2, "c2", "configs[1] per GPU x2"), (4, "c2", "configs[3]"),
+                                               (8, "c5", "configs[4]")])
+def test_bench_ranks_end_to_end_on_cpu(n, config, baseline):
+    """bench.py's whole multi-rank path on CPU for --gpus 2/4/8: its own
+    launcher spawns torch.distributed.run, the ranks meet over gloo, every
+    rank reports its device from the live group, each timed region gathers
+    the K spectra to rank 0, and the line rank 0 prints says so -- ranks ==
+    n_gpus == N, distinct GPUs read back from the identities (N), rank 0
+    holding every rank's spectra, each spectrum equal to the C oracle's.  The
+    GPU is a host-memory double (tests/bench_cpu_rehearsal.py); the driver's
+    8-GPU run takes the same code path with RCCL and the HIP library."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "bench_cpu_rehearsal.py"), "--gpus", str(n),
+                        "--steps", "4", "--warmup", "1", "--min-seconds", "0.3", "--bpl1-seconds", "0.2",
+                        "--dist-backend", "gloo", "--cpu-seconds", "0", "--config", config, "--dist-timeout", "120"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]          # rank 0 alone prints the line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == d["ranks"] == n
+    assert d["dist_backend"] == "gloo" and d["rccl_ranks"] == 0
+    assert d["distinct_gpus"] == n
+    assert [x["device"] for x in d["rank_devices"]] == list(range(n))
+    assert len({x["pci_bus_id"] for x in d["rank_devices"]}) == n
+    assert d["verified"] is True
+    assert d["verification"]["gather"] == "rank 0 holds every rank's K spectra"
+    assert d["config"]["launcher"] == "bench.py --gpus spawned torch.distributed.run"
+    assert d["config"]["baseline_config"].startswith(baseline)
+    assert f"over {n} MI355X" in d["config"]["workload"] and "spectra gathered to rank 0" in d["config"]["workload"]
+    assert "gloo gather to rank 0" in d["config"]["parallelism"]
+    assert d["one_per_launch"]["verified"] is True
+    assert d["value"] > 0 and d["cpu_baseline"] is None and "secondary" not in d
+
+
+def test_bench_line_carries_the_bmf_leg_on_cpu():
+    """the default one-rank line carries `secondary.bmf`: the reference-
+    native layout (int16 BE TFTFP, 48 x 7 channels) timed after the headline
+    and verified against the oracle, with a roofline of its own at 4 B per
+    sample and the PMC summary of that layout (profiles/pmc_bmf.json)"""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "bench_cpu_rehearsal.py"), "--steps", "4",
+                        "--warmup", "1", "--min-seconds", "0.2", "--bpl1-seconds", "0.1", "--bmf-seconds", "0.2",
+                        "--cpu-seconds", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    b = d["secondary"]["bmf"]
+    assert b["verified"] is True and d["verified"] is True
+    assert "int16 BE TFTFP" in b["workload"] and "336 ch" in b["workload"]
+    assert b["roofline"]["bound"] == "hbm" and b["roofline"]["bytes_per_sample"] == 4
+    assert b["roofline"]["algorithmic_bytes_per_launch"] == 336 * 2 * (4 * 128) * 4  # ch x pol x samples x 4 B
+    assert b["roofline"]["traffic_source"].startswith("profiles/pmc_bmf.json")
+    assert b["value"] > 0 and b["timed_regions"] >= 1
+    # the headline stays configs[1]
+    assert d["config"]["baseline_config"] == "configs[1]" and d["dtype"] == "int8"

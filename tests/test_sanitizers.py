@@ -115,6 +115,9 @@ def test_stage_threads_under_tsan(tmp_path, mode):
     write_conf(conf, 1 << 10, 1, 256, 64, kin, kin + 0x8000, str(hfile))
     env_keep = dict(os.environ)
     os.environ["TSAN_OPTIONS"] = "halt_on_error=1 second_deadlock_stack=1"
+    # the CPU double's asynchronous stream model: work completes up to 0.5 ms
+    # after it is enqueued, so fences, held blocks and gathers meet late work
+    os.environ["B2P_STUB_DELAY_US"] = "500"
     try:
         if nsub > 1:
             outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, files, nsub=nsub, gather=True,

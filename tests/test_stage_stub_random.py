@@ -1,7 +1,8 @@
 """CPU property test of the stage's orchestration (no GPU): the real
 `paf_baseband2power` host code, linked against the CPU test double of
-libpafb2p (tests/c/b2p_cpu_stub.c: exact sums, every call finished on
-return) and libpafdada's sources, between PSRDADA writers in this process
+libpafb2p (tests/c/b2p_cpu_stub.c: exact sums; every call finished on
+return, or a stream model whose work completes up to 2 ms late, drawn per
+example) and libpafdada's sources, between PSRDADA writers in this process
 and `paf_dbdisk`.  Random layouts (int8 / int16 LE, what the stub handles),
 ring depths, block counts, short last blocks, output pols, sum or mean, and
 every threading mode of the stage:
@@ -88,7 +89,10 @@ def cases(draw):
                 nblks=[max(1, nblk - d) for d in shorter],
                 short=mode in ("single", "single_dev", "split") and nframes > 1 and draw(st.booleans()),
                 sync=mode in ("single", "gathered") and draw(st.booleans()),
-                seed=draw(st.integers(0, 2 ** 32 - 1)))
+                seed=draw(st.integers(0, 2 ** 32 - 1)),
+                # the double's stream model: synchronous, or work completing
+                # up to this many us after it is enqueued (b2p_cpu_stub.c)
+                delay_us=draw(st.sampled_from([0, 300, 2000])))
 
 
 @(seed(int(_SEED)) if _SEED else (lambda f: f))
@@ -125,7 +129,8 @@ def test_stage_orchestration_random(stages, tmp_path_factory, case):
     out = tmp / "power.dada"
     procs, errs = [], []
     try:
-        env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1")
+        env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",
+                   B2P_STUB_DELAY_US=os.environ.get("B2P_STUB_DELAY_US", str(case["delay_us"])))
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([exe, "-a", f"{base:x}", "-b", f"{kout:x}", "-c", str(tmp), "-d", "0"] + args,
@@ -184,3 +189,125 @@ def test_failed_stage_names_its_errors_on_stderr(stages, tmp_path):
     assert r.returncode == 1
     assert f"ERR: cannot attach/lock input ring {k:x}" in r.stderr, r.stderr
     assert "FAILED, log" in r.stderr and "earlier run" not in r.stderr, r.stderr
+
+
+@pytest.mark.parametrize("mode", ["gathered", "gathered_dev"])
+@pytest.mark.parametrize("ndev,gather,want", [(8, None, "RCCL ncclGather"), (1, None, "peer copies"),
+                                              (4, "rccl", "refused")])
+def test_stage_n8_group_transport(stages, tmp_path, mode, ndev, gather, want):
+    """`paf_baseband2power -n 8 -d 0` (configs[4]'s eight
+    sub-bands) with B2P_STUB_NDEV devices visible: on 8 distinct GPUs every
+    member r drives GPU r and the stage picks RCCL (group_mode), not peer
+    copies; on one GPU it picks peer copies; `-G rccl` with members sharing
+    GPUs is refused at set-up as RCCL refuses it, and the stage exits 1
+    naming the call on stderr.  Spectra equal the oracle's where it runs."""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=64)
+    nmem, nblk = 8, 3
+    base, kout = _key(), _key()
+    base += 0x1000  # room for 8 rings at key + 0x10 r
+    keys = [base + 0x10 * r for r in range(nmem)]
+    blocks = [[co.fill_synthetic(g, g.block_bytes, 88, r, b) for b in range(nblk)] for r in range(nmem)]
+    hdr = (f"HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN {g.nchan_chunk}\nNCHUNK 1\nNCHAN_CHUNK {g.nchan_chunk}\n"
+           "NSAMP_DF 1\nBYTE_ORDER LE\nTSAMP 0.84375\n")
+    for k in keys + [kout]:
+        dada.destroy_ring(k)
+    for k in keys:
+        dada.create_ring(k, 4, g.block_bytes)
+    dada.create_ring(kout, 4, nmem * g.nout * 4)
+    out = tmp_path / "power.dada"
+    env = dict(os.environ, B2P_STUB_NDEV=str(ndev))
+    args = ["-n", str(nmem), "-f", "header"] + (["-G", gather] if gather else [])
+    procs = []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([stages["dev" if mode.endswith("_dev") else "host"], "-a", f"{base:x}", "-b",
+                                   f"{kout:x}", "-c", str(tmp_path), "-d", "0"] + args,
+                                  stderr=subprocess.PIPE, text=True, env=env)]
+        for k, bl in zip(keys, blocks):  # 3 blocks and the end of data fit the 4-block rings
+            with dada.Hdu(k, "W") as w:
+                w.write_header(hdr)
+                for b in bl:
+                    w.write_block(b.tobytes())
+        if want == "refused":  # the stage reads every ring's header, then sets the group up
+            _, err = procs[1].communicate(timeout=60)
+            assert procs[1].returncode == 1, err
+            assert "b2p_group_open" in err and "Duplicate GPU" in err, err
+            return
+        for p in procs[::-1]:
+            _, e = p.communicate(timeout=60)
+            assert p.returncode == 0, e[-800:] if isinstance(e, str) else e.decode(errors="replace")[-800:]
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for k in keys + [kout]:
+            dada.destroy_ring(k)
+    log = open(str(tmp_path / "paf_baseband2power.log")).read()
+    assert f"gather of {nmem} sub-bands to GPU 0 via {want}" in log, log[-1500:]
+    for r in range(nmem):
+        assert f"member {r}: GPU {r if ndev == 8 else 0} " in log, log[-1500:]
+    sp = data.view(np.uint32).reshape(-1, nmem, g.nout)
+    assert sp.shape[0] == nblk
+    for b in range(nblk):
+        for r in range(nmem):
+            assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=1).view(np.uint32)), (b, r)
+
+
+def test_stage_recorded_gather_case_async(stages, tmp_path):
+    """round 5's failing GPU example (profiles/r05_gpu_suite_gather_flake.txt),
+    through the stage's real host code on the asynchronous CPU double (work
+    completes 0-3 ms after it is enqueued): -n 2 on the GPU-resident path,
+    rings of 6 blocks written by paf_diskdb processes, transfers of 1 and 2
+    blocks, int8 11 x 53 ch, 67 frames of 8 samples, npol_out 2, mean.  Each
+    of 12 runs must exit 0 with the one common integration of both
+    sub-bands equal to the oracle's, the unmatched block of the longer
+    transfer logged as skipped."""
+    g = npo.Geom(nbit=8, big_endian=0, nchunk=11, nsamp_df=8, nchan_chunk=53, npol_out=2, nsamp_int=536, mean=1)
+    nblks = [1, 2]
+    blocks = [[co.fill_synthetic(g, g.block_bytes, 1440, r, b) for b in range(nblks[r])] for r in range(2)]
+    want = [co.power(g, blocks[r][0], nthreads=2).view(np.uint32) for r in range(2)]
+    hdr = (f"HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN {g.nchunk * g.nchan_chunk}\nNCHUNK {g.nchunk}\n"
+           f"NCHAN_CHUNK {g.nchan_chunk}\nNSAMP_DF {g.nsamp_df}\nBYTE_ORDER LE\nTSAMP 0.84375\n")
+    for r in range(2):
+        dada.write_dada_file(str(tmp_path / f"in{r}.dada"), "FILE_HEADER_IS_SKIPPED 1\n",
+                             np.concatenate([b.reshape(-1).view(np.uint8) for b in blocks[r]]))
+        (tmp_path / f"hdr{r}.txt").write_text(hdr)
+    env = dict(os.environ, B2P_STUB_DELAY_US="3000")
+    for run in range(12):
+        base, kout = _key(), _key()
+        keys = [base, base + 0x10]
+        for k in keys + [kout]:
+            dada.destroy_ring(k)
+        for k in keys:
+            dada.create_ring(k, 6, g.block_bytes)
+        dada.create_ring(kout, 4, 2 * g.nout * 4)
+        d = tmp_path / f"run{run}"
+        d.mkdir()
+        procs = []
+        try:
+            procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(d / "p.dada")],
+                                      stderr=subprocess.PIPE),
+                     subprocess.Popen([stages["dev"], "-a", f"{base:x}", "-b", f"{kout:x}", "-c", str(d), "-d", "0",
+                                       "-f", "header", "-n", "2", "-p", "2", "-m"], stderr=subprocess.PIPE, env=env)]
+            procs += [subprocess.Popen([os.path.join(BIN, "paf_diskdb"), "-a", f"{keys[r]:x}", "-b", str(tmp_path),
+                                        "-c", f"in{r}.dada", "-d", str(tmp_path / f"hdr{r}.txt"), "-e", "1"],
+                                       stderr=subprocess.PIPE) for r in (run % 2, 1 - run % 2)]
+            for p in procs[::-1]:
+                _, e = p.communicate(timeout=60)
+                assert p.returncode == 0, (run, p.args[0], e.decode(errors="replace")[-800:])
+            _, data = dada.read_dada_file(str(d / "p.dada"))
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+            for k in keys + [kout]:
+                dada.destroy_ring(k)
+        sp = data.view(np.uint32).reshape(-1, 2, g.nout)
+        assert sp.shape[0] == 1, run
+        assert np.array_equal(sp[0, 0], want[0]) and np.array_equal(sp[0, 1], want[1]), run
+        log = (d / "paf_baseband2power.log").read_text()
+        assert "FINISH PAF_PROCESS: 1 integrations, 1 skipped, ok" in log, log[-800:]
