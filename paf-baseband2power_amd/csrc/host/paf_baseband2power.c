@@ -335,6 +335,7 @@ typedef struct shared_t {
   atomic_int failed;
   int mfail[MAX_SUB]; /* worker / worker_split: this member failed this round */
   uint64_t nblocks, nskipped;
+  int end_lost; /* -n N: the integration lost when the first sub-band's transfer ended is counted (once) */
   uint64_t nlaunches; /* device ring: integrate launches, several queued blocks each at most */
   uint32_t max_batch;
   double t_first, t_last; /* first integration started, last output written */
@@ -398,10 +399,12 @@ static void *worker(void *arg) {
       for (int r = 0; r < sh->nsub; r++) whole |= sh->have[r] == 1;
       if (w->r == 0 && skip && !stop) {
         sh->nskipped++;
+        if (sh->nsub > 1) sh->end_lost = 1;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band block held %" PRIu64
                  " of %" PRIu64 " B)", bytes, s->rbufsz);
-      } else if (w->r == 0 && stop && whole && !sh->failed && !g_stop) {
+      } else if (w->r == 0 && stop && whole && !sh->end_lost && !sh->failed && !g_stop) {
         sh->nskipped++;
+        sh->end_lost = 1;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
       }
       pthread_barrier_wait(&sh->bar);
@@ -610,12 +613,14 @@ static void *worker_gather_dev(void *arg) {
     if (r == 0) {
       /* an integration is lost when a member's transfer ended while another
        * had a whole block for it: taken in this round's queued loop (got >
-       * mm), or as the round's first block (have 1 in a stop round) --
-       * counted the same however the writers' timing split the blocks */
+       * mm), or as the round's first block (have 1 in a stop round).  The
+       * first such round counts one skipped integration, however the
+       * writers' timing split the blocks between the two rounds */
       int lost = skip && !stop;
       for (int q = 0; q < sh->nsub; q++)
         lost |= (uint32_t)sh->got[q] > mm || sh->partial[q] || (stop && sh->have[q] == 1);
-      if (lost) {
+      if (lost && !sh->end_lost) {
+        sh->end_lost = 1;
         sh->nskipped++;
         multilog(sh->log, LOG_INFO, "partial integration skipped (a sub-band's transfer ended)");
       }
