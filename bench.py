@@ -50,6 +50,12 @@ differ by the region's host bracketing), `frac_kernel_only` from per-launch
 packet events.  `traffic` is the committed PMC summary's, marked STALE when
 the kernel's sources changed after it was measured (`provenance`).
 
+Secondary layouts.  At one rank with the default configs[1] workload the
+line also carries `secondary`: the reference-native BMF layout, configs[4]'s
+per-GPU share and configs[2] (pinned host, PCIe-bound), each timed for
+--secondary-seconds after the headline, verified against the oracle and
+given a roofline of its own; the headline `value` stays configs[1].
+
 Prints ONE JSON line on rank 0.  Options beyond the driver contract:
   --config c2|c5|bmf|c3   workload (c3 = pinned host buffer, H2D overlapped;
                           its value is PCIe-bound and is never the default)
@@ -132,14 +138,20 @@ def parse(argv=None):
                     help="when the headline batches queued blocks, also time this long of regions "
                          "with ONE block per launch (the real-time stage's launch shape) and report "
                          "it beside the headline (0 disables)")
-    ap.add_argument("--bmf-seconds", type=float, default=2.0,
-                    help="with the default configs[1] workload at one rank, also time this long of the "
-                         "reference-native BMF layout (int16 BE TFTFP, 336 ch, 2.625 GiB) and report it as "
-                         "`secondary.bmf`, verified against the oracle (0 disables)")
+    ap.add_argument("--secondary", default="bmf,c5,c3",
+                    help="with the default configs[1] workload at one rank, also time these layouts after the "
+                         "headline and report each under `secondary`, verified against the oracle: bmf "
+                         "(reference-native int16 BE TFTFP, 2.625 GiB), c5 (configs[4] per GPU, 1024 ch, 4 GiB), "
+                         "c3 (configs[2], 4 GiB from pinned host memory, PCIe-bound); '' for none")
+    ap.add_argument("--secondary-seconds", type=float, default=2.0,
+                    help="timed seconds per secondary layout")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="seconds one multi-rank phase (rendezvous, first collective, a timed "
                          "region, verification) may take; past it the rank exits 4 naming it")
     a = ap.parse_args(argv)
+    bad = [x for x in a.secondary.split(",") if x and x not in SECONDARY_WHAT]
+    if bad:
+        ap.error(f"--secondary: unknown layout(s) {bad}; choose from {sorted(SECONDARY_WHAT)}")
     if a.gpus < 1 or a.steps < 1 or a.warmup < 0 or a.blocks < 0:
         ap.error("--gpus and --steps must be >= 1, --warmup and --blocks >= 0")
     return a
@@ -348,30 +360,50 @@ def synthetic_reader(geom_dict: dict, subband: int, block: int, threads: int):
     return rd
 
 
-def bmf_leg(dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
-    """The reference-native layout beside the headline (the
-    BMF-native parity/drop-in run): 336 channels int16 big-endian TFTFP
-    (capture.h:20,28; paf-baseband2power.conf:2-9), one 2.625 GiB
-    integration per block, NBLOCKS rotating HBM-resident blocks, one block
-    per integrate launch (floor(4 GiB / 2.625 GiB) = 1, the stage's rule).
-    A region is NBLOCKS integrations bracketed by device syncs; regions
-    repeat for `seconds`; the last region's spectra are checked against the
-    C oracle bit for bit.  Algorithmic bytes: 4 B per complex dual-pol
-    sample, the block per launch."""
+SECONDARY_WHAT = {
+    "bmf": ("reference-native", "BMF: 336 ch x 2 pol int16 BE TFTFP (48 chunks x 7 ch, 128 samples per frame)"),
+    "c5": ("configs[4] per GPU", "1024 ch x 2 pol int8 (one of configs[4]'s eight sub-bands)"),
+    "c3": ("configs[2]", "1024 ch x 2 pol int8 from a pinned host buffer, H2D overlapped"),
+}
+
+
+def secondary_leg(name: str, dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
+    """One of the other BASELINE layouts beside the headline, in the same
+    run: "bmf" the reference-native layout the drop-in serves
+    (capture.h:20,28; paf-baseband2power.conf:2-9), "c5" one GPU's share of
+    configs[4], both HBM-resident over NBLOCKS rotating blocks, one block per
+    integrate launch (floor(4 GiB / block) = 1, the stage's rule); "c3"
+    configs[2], one block in a registered host buffer pushed through the
+    staging pair (PCIe-bound; its ceiling, a bare H2D of the same block, is
+    measured right after).  A region is the leg's integrations bracketed by
+    device syncs; regions repeat for `seconds`; the last region's spectra
+    are checked against the C oracle bit for bit.  Algorithmic bytes: 2 B
+    per complex sample (int8), 4 B (int16); the block per launch."""
     import numpy as np
 
     import paf_b2p
     from paf_b2p.geometry import CONFIGS, samples_per_block
-    geom = CONFIGS["bmf"]["geom"]()
+    geom = CONFIGS[name]["geom"]()
     gd = {f: int(getattr(geom, f)) for f, _ in geom._fields_ if f != "reserved"}
+    host = name == "c3"
     it = paf_b2p.Integrator(geom, device=dev)
-    nout, bb, K = it.nout, it.block_bytes, NBLOCKS
+    nout, bb = it.nout, it.block_bytes
+    K = 1 if host else NBLOCKS
     blocks = []
     try:
-        for b in range(K):
+        if host:  # the block in pinned host memory, generated on the GPU and copied home once
+            hb = np.empty(bb, dtype=np.uint8)
             d = it.alloc(bb)
-            it.fill_synthetic(d, SEED, 0, b)
-            blocks.append(d)
+            it.fill_synthetic(d, SEED, 0, 0)
+            hb[:] = it.download(d)
+            d.free()
+            it.register_host(hb)
+            blocks = [hb]
+        else:
+            for b in range(K):
+                d = it.alloc(bb)
+                it.fill_synthetic(d, SEED, 0, b)
+                blocks.append(d)
         out = it.alloc(K * nout * 4)
         it.sync()
 
@@ -380,7 +412,11 @@ def bmf_leg(dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
             t0 = time.perf_counter()
             it.set_timing(2)
             for k in range(K):
-                it.integrate(blocks[k], out.ptr + k * nout * 4, True)
+                if host:
+                    it.push(blocks[k])
+                    it.finish_async(out.ptr + k * nout * 4, True)
+                else:
+                    it.integrate(blocks[k], out.ptr + k * nout * 4, True)
             it.set_timing(0)
             it.sync()
             return time.perf_counter() - t0
@@ -391,24 +427,43 @@ def bmf_leg(dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
         while sum(els) < seconds and len(els) < 100000:
             els.append(region())
         st = it.stats()
+        h2d = None
+        if host:  # the leg's ceiling: a bare pinned H2D of the same block, same process
+            dst = it.alloc(bb)
+            it.upload_into(dst, blocks[0])
+            rates, t_all = [], time.perf_counter()
+            while len(rates) < 3 or (time.perf_counter() - t_all < 1.0 and len(rates) < 50):
+                t0 = time.perf_counter()
+                it.upload_into(dst, blocks[0])
+                rates.append(bb / (time.perf_counter() - t0) / 1e9)
+            dst.free()
+            h2d = {"gbs": round(statistics.median(rates), 2), "copies": len(rates),
+                   "range": [round(min(rates), 2), round(max(rates), 2)],
+                   "what": f"hipMemcpy of the same {bb >> 20} MiB registered host block into HBM, no kernel"}
         ok = None
         if verify:
             spec = it.download(out, nbytes=K * nout * 4).view(np.float32).reshape(K, nout)
             ok = True
             for k in range(K):
-                def rd(off, n, blk=blocks[k]):
-                    return it.download(blk, nbytes=n, offset=off)
+                if host:
+                    def rd(off, n, blk=blocks[k]):
+                        return blk[off:off + n]
+                else:
+                    def rd(off, n, blk=blocks[k]):
+                        return it.download(blk, nbytes=n, offset=off)
                 ref = oracle_spectrum(gd, rd, bb, vthreads)
                 ok &= bool(np.array_equal(spec[k].view(np.uint32), ref.view(np.uint32)))
         el = statistics.median(els)
         kern_s = st["kernel_ms"] / max(st["launches"], 1) / 1e3
         per_launch = st["bytes"] / max(st["launches"], 1)
         achieved = per_launch / kern_s / 1e9 if kern_s > 0 else 0.0
-        traffic, src, prov = pmc_traffic("bmf", per_launch)
-        return {
-            "workload": (f"reference-native BMF: {paf_b2p.geometry.nchan(geom)} ch x 2 pol int16 BE TFTFP "
-                         f"(48 chunks x 7 ch, 128 samples per frame), {bb} B per integration, {K} rotating "
-                         "HBM-resident blocks, 1 block per integrate launch"),
+        traffic, src, prov = pmc_traffic(name, per_launch)
+        baseline, what = SECONDARY_WHAT[name]
+        res = {
+            "baseline_config": baseline,
+            "workload": (f"{what}, {bb} B per integration, "
+                         + ("one block in a registered host buffer" if host else
+                            f"{K} rotating HBM-resident blocks, 1 block per integrate launch")),
             "value": round(samples_per_block(geom) / (el / K) / 1e6, 1),
             "unit": "Msamples/s",
             "ms_per_step": round(el / K * 1e3, 4),
@@ -417,12 +472,12 @@ def bmf_leg(dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
             "verified": ok,
             "verification": f"every spectrum of the last region ({K}) against the C oracle of its block, bit for bit",
             "roofline": {
-                "bound": "hbm", "kernel": "b2p_integrate_kernel<..., MULTI=false> (int16 BE)",
+                "bound": "hbm", "kernel": "b2p_integrate_kernel<..., MULTI=false>",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "frac_of_value": round(bb / (el / K) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(per_launch),
-                "bytes_per_sample": 4,
+                "bytes_per_sample": int(geom.nbit // 8 * 2),
                 "avg_launch_us": round(kern_s * 1e6, 2),
                 "launches_timed": int(st["launches"]),
                 "traffic": traffic, "traffic_source": src, "traffic_provenance": prov,
@@ -430,9 +485,24 @@ def bmf_leg(dev: int, seconds: float, vthreads: int, verify: bool) -> dict:
                            "frac_of_value: the host-timed median region"),
             },
         }
+        if host:
+            pcie = bb / (el / K) / 1e9
+            hbm = dict(res["roofline"])
+            res["roofline"] = {
+                "bound": "pcie", "achieved": round(pcie, 2), "peak": h2d["gbs"], "unit": "GB/s",
+                "frac": round(pcie / h2d["gbs"], 4), "peak_source": h2d,
+                "algorithmic_bytes_per_launch": hbm["algorithmic_bytes_per_launch"],
+                "hbm": {k: hbm[k] for k in ("achieved", "frac", "avg_launch_us", "launches_timed")},
+                "timing": ("achieved: the block's bytes per ms_per_step (staging copies overlapped with the "
+                           "integrate launches); peak: peak_source, the bare H2D stream of the same bytes"),
+            }
+        return res
     finally:
+        if host and blocks:
+            it.unregister_host(blocks[0])
         for d in blocks:
-            d.free()
+            if hasattr(d, "free"):
+                d.free()
         it.close()
 
 
@@ -951,10 +1021,12 @@ def main(argv=None) -> int:
                            "pinned-host staging copies overlapped with the integrate launches); peak: "
                            "peak_source, the bare H2D stream of the same bytes in the same run"),
             })
-        if world == 1 and not split and a.config == "c2" and a.bmf_seconds > 0:
-            # the layout the drop-in serves, in the driver's own record
-            res["secondary"] = {"bmf": bmf_leg(dev, a.bmf_seconds, max(1, cpu_threads()), not a.no_verify)}
-            if res["secondary"]["bmf"]["verified"] is False:
+        legs = [x for x in a.secondary.split(",") if x]
+        if world == 1 and not split and a.config == "c2" and legs and a.secondary_seconds > 0:
+            # the other BASELINE layouts and the one the drop-in serves, in the driver's own record
+            res["secondary"] = {x: secondary_leg(x, dev, a.secondary_seconds, max(1, cpu_threads()),
+                                                 not a.no_verify) for x in legs}
+            if any(v["verified"] is False for v in res["secondary"].values()):
                 res["verified"] = verified = False
         if world == 1 and a.cpu_seconds > 0 and not host_mode:
             res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)

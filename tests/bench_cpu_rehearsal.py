@@ -76,6 +76,25 @@ class FakeIntegrator:
         self._stats["bytes"] += nblk * self.block_bytes
         self._stats["kernel_ms"] += 1e-3 * nblk
 
+    # the host-span path (configs[2]): push a registered host block, finish into device memory
+    def register_host(self, arr):
+        self._pushed = None
+
+    def unregister_host(self, arr):
+        pass
+
+    def push(self, blk):
+        self._pushed = blk if isinstance(blk, np.ndarray) else blk.arr[:self.block_bytes]
+        self._launch(1)
+
+    def finish_async(self, dst, out_is_device):
+        sp = co.power(self.g, self._pushed, nthreads=1)
+        C.memmove(dst, sp.ctypes.data, self.nout * 4)
+        return 0
+
+    def upload_into(self, d, arr, offset=0):
+        d.arr[offset:offset + arr.nbytes] = arr.view(np.uint8).reshape(-1)
+
     def integrate(self, blk, dst, out_is_device):
         self._spectrum_into(blk, dst)
         self._launch(1)
@@ -111,6 +130,7 @@ def _small(nchan):
 
 geometry.CONFIGS["c2"]["geom"] = _small(256)
 geometry.CONFIGS["c5"]["geom"] = _small(1024)
+geometry.CONFIGS["c3"]["geom"] = _small(1024)
 geometry.CONFIGS["bmf"]["geom"] = lambda: geometry.bmf_geom(nsamp_int=4 * 128)
 paf_b2p.Integrator = FakeIntegrator
 paf_b2p.pci_bus_id = lambda d: f"0000:{0x10 + d:02x}:00.0"

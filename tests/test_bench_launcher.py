@@ -320,24 +320,38 @@ def test_bench_ranks_end_to_end_on_cpu(n, config, baseline):
     assert d["value"] > 0 and d["cpu_baseline"] is None and "secondary" not in d
 
 
-def test_bench_line_carries_the_bmf_leg_on_cpu():
-    """the default one-rank line carries `secondary.bmf`: the reference-
-    native layout (int16 BE TFTFP, 48 x 7 channels) timed after the headline
-    and verified against the oracle, with a roofline of its own at 4 B per
-    sample and the PMC summary of that layout (profiles/pmc_bmf.json)"""
+def test_bench_line_carries_the_secondary_layouts_on_cpu():
+    """the default one-rank line carries `secondary`: the reference-native
+    BMF layout (int16 BE TFTFP, 48 x 7 channels), configs[4]'s per-GPU share
+    (1024 ch int8) and configs[2] (pinned host, PCIe-bound against a bare
+    H2D of the same block), each timed after the headline and verified
+    against the oracle, each with a roofline of its own and the PMC summary
+    of its layout"""
     import json
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "bench_cpu_rehearsal.py"), "--steps", "4",
-                        "--warmup", "1", "--min-seconds", "0.2", "--bpl1-seconds", "0.1", "--bmf-seconds", "0.2",
-                        "--cpu-seconds", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+                        "--warmup", "1", "--min-seconds", "0.2", "--bpl1-seconds", "0.1", "--secondary-seconds",
+                        "0.2", "--cpu-seconds", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["verified"] is True and sorted(d["secondary"]) == ["bmf", "c3", "c5"]
     b = d["secondary"]["bmf"]
-    assert b["verified"] is True and d["verified"] is True
+    assert b["verified"] is True and b["baseline_config"] == "reference-native"
     assert "int16 BE TFTFP" in b["workload"] and "336 ch" in b["workload"]
     assert b["roofline"]["bound"] == "hbm" and b["roofline"]["bytes_per_sample"] == 4
     assert b["roofline"]["algorithmic_bytes_per_launch"] == 336 * 2 * (4 * 128) * 4  # ch x pol x samples x 4 B
     assert b["roofline"]["traffic_source"].startswith("profiles/pmc_bmf.json")
-    assert b["value"] > 0 and b["timed_regions"] >= 1
+    c5 = d["secondary"]["c5"]
+    assert c5["verified"] is True and c5["baseline_config"] == "configs[4] per GPU"
+    assert c5["roofline"]["bytes_per_sample"] == 2 and c5["roofline"]["traffic_source"].startswith("profiles/pmc_c5")
+    c3 = d["secondary"]["c3"]
+    assert c3["verified"] is True and c3["baseline_config"] == "configs[2]"
+    assert c3["roofline"]["bound"] == "pcie" and c3["roofline"]["peak_source"]["copies"] >= 3
+    assert "frac" in c3["roofline"]["hbm"]
+    assert all(v["value"] > 0 and v["timed_regions"] >= 1 for v in d["secondary"].values())
     # the headline stays configs[1]
     assert d["config"]["baseline_config"] == "configs[1]" and d["dtype"] == "int8"
+    # and the list is the caller's
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--secondary", "c9"], capture_output=True,
+                       text=True, timeout=120, env=env, cwd=REPO)
+    assert r.returncode == 2 and "unknown layout" in r.stderr
