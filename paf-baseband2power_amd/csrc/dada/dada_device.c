@@ -426,13 +426,16 @@ void dev_close_blocks(ipcbuf_t *id) {
     }
 }
 
-int dev_copy(void *dst, const void *src, uint64_t n) {
+int dev_copy(void *dst, const void *src, uint64_t n, int into_block) {
   if (!n) return 0;
   if (hip_load() < 0) {
     dev_fail("dlopen libamdhip64.so.7", -1);
     return -1;
   }
-  const int rc = hip.memcpy_(dst, src, n, 4 /* hipMemcpyDefault */);
+  int rc = hip.memcpy_(dst, src, n, 4 /* hipMemcpyDefault */);
+  /* into a block: the bytes are in HBM before the caller marks it filled
+   * (hipMemcpy does not promise completion for a pageable source) */
+  if (rc == 0 && into_block) rc = hip.sync();
   if (rc != 0) {
     char w[96];
     snprintf(w, sizeof w, "hipMemcpy of %llu B (%p <- %p)", (unsigned long long)n, dst, src);

@@ -130,7 +130,7 @@ int dev_stop_holder(int seg0_id);
 int dev_look_seg0(int seg0_id, dev_seg_t *out);
 int dev_open_blocks(ipcbuf_t *id);
 void dev_close_blocks(ipcbuf_t *id);
-int dev_copy(void *dst, const void *src, uint64_t n); /* hipMemcpyDefault */
+int dev_copy(void *dst, const void *src, uint64_t n, int into_block); /* hipMemcpyDefault; into_block: finished on return */
 int dev_zero(void *dst, uint64_t n);                  /* hipMemset, synchronised */
 
 #endif

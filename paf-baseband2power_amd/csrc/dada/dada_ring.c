@@ -767,14 +767,14 @@ int ipcbuf_get_device(ipcbuf_t *id) { return id && id->sync ? id->sync->on_devic
 
 int ipcbuf_copy_in(ipcbuf_t *id, char *block, const void *src, uint64_t n) {
   if (!id || !id->sync || (!block && n) || (!src && n)) return -1;
-  if (id->sync->on_device_id >= 0) return dev_copy(block, src, n);
+  if (id->sync->on_device_id >= 0) return dev_copy(block, src, n, 1);
   memcpy(block, src, n);
   return 0;
 }
 
 int ipcbuf_copy_out(ipcbuf_t *id, void *dst, const char *block, uint64_t n) {
   if (!id || !id->sync || (!block && n) || (!dst && n)) return -1;
-  if (id->sync->on_device_id >= 0) return dev_copy(dst, block, n);
+  if (id->sync->on_device_id >= 0) return dev_copy(dst, block, n, 0);
   memcpy(dst, block, n);
   return 0;
 }

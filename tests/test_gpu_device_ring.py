@@ -570,3 +570,30 @@ def test_holder_frees_blocks_only_after_importers_detach(gpu):
             child.kill()
             child.wait()
     assert not _holder_pids(key)
+
+
+def test_device_ring_info_reports_the_holder(gpu):
+    """dada_device_ring_info on a real HIP holder: serving, its pid live, no
+    ring block exported after a retry; a process that opens the blocks is
+    counted as an importer within a holder tick; after destroy the ring is
+    gone (ENOENT) and so is the holder"""
+    key = fresh_key()
+    dada.create_ring(key, 3, 1 << 20, device=0)
+    try:
+        info = dada.device_ring_info(key)
+        assert info["device"] == 0 and info["holder_state"] == 1 and info["export_retries"] == 0, info
+        assert os.path.exists(f"/proc/{info['holder_pid']}")
+        assert _holder_pids(key) == [info["holder_pid"]]
+        v = dada.Hdu(key, "r")
+        try:
+            t_end = time.time() + 5
+            while dada.device_ring_info(key)["importers"] < 1 and time.time() < t_end:
+                time.sleep(0.05)
+            assert dada.device_ring_info(key)["importers"] == 1
+        finally:
+            v.close()
+    finally:
+        assert dada.destroy_ring(key), dada.device_error()
+    with pytest.raises(OSError):
+        dada.device_ring_info(key)
+    assert not _holder_pids(key)
