@@ -39,6 +39,16 @@ for i in $(seq 1 "$N"); do
   if [ $rc -gt 1 ]; then echo "stopping: import exit $rc"; $BIN/dada_db -k $KEY -d; exit $rc; fi
   [ $((i % 50)) -eq 0 ] && echo "[$(date +%T)] import $i"
 done
+# the stage and its writers open the same ring's handles at the same moment
+# (the GPU tests start them together): three importers at once, N/2 times
+for i in $(seq 1 $((N / 2))); do
+  for j in 1 2 3; do
+    timeout -k 5 30 $BIN/ipc_probe import $KEY >> "$OUT.par$j" 2>> "$OUT.err" &
+  done
+  wait
+  [ $((i % 50)) -eq 0 ] && echo "[$(date +%T)] concurrent import $i"
+done
+cat "$OUT".par* >> "$OUT" && rm -f "$OUT".par*
 $BIN/dada_db -k $KEY -d
 python3 - "$OUT" <<'EOF'
 import json, sys
