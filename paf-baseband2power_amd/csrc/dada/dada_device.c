@@ -174,7 +174,12 @@ static void holder(ipcbuf_t *id, int device, int wfd) {
    * export was refused is reported with the retries (the "P" count). */
   void *primer = NULL;
   int primer_refused = 0;
-  if (hip.malloc_(&primer, DEV_ALLOC_ALIGN) == 0) {
+  /* DADA_HOLDER_NO_PRIMER=1: diagnostics only (tools/devring_probe.py
+   * noprimer): the first allocation is block 0 again, as before round 5 */
+  const char *no_primer = getenv("DADA_HOLDER_NO_PRIMER");
+  if (no_primer && no_primer[0] == '1') {
+    /* no primer */
+  } else if (hip.malloc_(&primer, DEV_ALLOC_ALIGN) == 0) {
     ipc_handle_t ph;
     primer_refused = hip.memset_(primer, 0, DEV_ALLOC_ALIGN) == 0 && hip.get_handle(&ph, primer) != 0;
   } else {

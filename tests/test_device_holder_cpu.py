@@ -173,3 +173,18 @@ def test_destroy_with_importer_reports_it(fake_env):
         time.sleep(0.05)
     st = open(f"/proc/{pid}/stat").read().split(") ")[1][0] if os.path.exists(f"/proc/{pid}") else "gone"
     assert st in ("Z", "gone"), st
+
+
+def test_holder_without_primer_diagnostic(fake_env):
+    """DADA_HOLDER_NO_PRIMER=1 (tools/devring_probe.py noprimer): block 0 is
+    the holder's first allocation again, so a refused first export lands on
+    a ring block and is counted as its retry"""
+    key = _key()
+    r = _create(dict(fake_env, DADA_HOLDER_NO_PRIMER="1"), key, "0")
+    try:
+        assert r.returncode == 0, r.stderr
+        info = dada.device_ring_info(key)
+        assert info["export_retries"] == 1 and info["primer_refused"] == 0, (info, r.stderr)
+        assert "on block 0" in r.stderr, r.stderr
+    finally:
+        assert _destroy(fake_env, key).returncode == 0

@@ -9,7 +9,12 @@ each used ring's line also carries this process's open file descriptors
 and mapped size after the ring was closed, so a per-import leak in the HIP
 runtime's IPC path shows as steady growth.
 
-  python3 tools/devring_probe.py [ROUNDS] [use]   (use: open and write every ring)
+  python3 tools/devring_probe.py [ROUNDS] [use] [noprimer] [pause=S]
+    use       open and write every ring
+    noprimer  the holders make no primer allocation (DADA_HOLDER_NO_PRIMER=1):
+              block 0 is their first allocation, as before round 5
+    pause=S   sleep S seconds between a ring's destroy and the next create
+              (the previous holder has then long exited)
 """
 import collections
 import json
@@ -17,6 +22,7 @@ import os
 import re
 import subprocess
 import sys
+import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "paf-baseband2power_amd"))
@@ -39,7 +45,12 @@ def main():
     print(json.dumps({"rlimit_nofile": resource.getrlimit(resource.RLIMIT_NOFILE),
                       "fds": len(os.listdir("/proc/self/fd"))}), flush=True)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    use = len(sys.argv) > 2 and sys.argv[2] == "use"
+    use = "use" in sys.argv[2:]
+    pause = next((float(a[6:]) for a in sys.argv[2:] if a.startswith("pause=")), 0.0)
+    env = dict(os.environ)
+    if "noprimer" in sys.argv[2:]:
+        env["DADA_HOLDER_NO_PRIMER"] = "1"
+    print(json.dumps({"use": use, "noprimer": "noprimer" in sys.argv[2:], "pause_s": pause}), flush=True)
     import tempfile
     tmp = tempfile.mkdtemp(prefix="devring_probe_")
     key = 0x7e40
@@ -50,9 +61,12 @@ def main():
             for nb in (2, 4, 6):
                 attempts += 1
                 dada.destroy_ring(key)
+                if pause:
+                    time.sleep(pause)
                 try:
                     p = subprocess.run([os.path.join(dada.BIN_DIR, "dada_db"), "-k", f"{key:x}", "-b", str(sz),
-                                        "-n", str(nb), "-g", "0"], capture_output=True, text=True, timeout=120)
+                                        "-n", str(nb), "-g", "0"], capture_output=True, text=True, timeout=120,
+                                       env=env)
                     if "primer allocation was not exportable" in p.stderr:
                         primer[f"{sz}x{nb}"] += 1
                     m = re.search(r"(\d+) IPC export retr", p.stderr)
