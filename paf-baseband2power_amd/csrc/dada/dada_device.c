@@ -357,6 +357,24 @@ int dev_look_seg0(int seg0_id, dev_seg_t *out) {
   return 0;
 }
 
+/* until process pid has exited (gone, or a zombie whose resources -- its GPU
+ * context among them -- are released), at most ms milliseconds */
+static void wait_exited(pid_t pid, int ms) {
+  char path[64], st[256];
+  snprintf(path, sizeof path, "/proc/%d/stat", (int)pid);
+  for (int t = 0; t < ms; t += 5) {
+    if (kill(pid, 0) < 0 && errno == ESRCH) return;
+    FILE *f = fopen(path, "r");
+    if (!f) return;
+    const size_t n = fread(st, 1, sizeof st - 1, f);
+    fclose(f);
+    st[n] = 0;
+    const char *q = strrchr(st, ')'); /* "pid (comm) S ..." */
+    if (q && q[1] == ' ' && (q[2] == 'Z' || q[2] == 'X')) return;
+    nanosleep(&(struct timespec){0, 5 * 1000 * 1000}, NULL);
+  }
+}
+
 int dev_stop_holder(int seg0_id) {
   dev_seg_t v;
   if (dev_look_seg0(seg0_id, &v) < 0 || v.holder_pid <= 0 || v.holder_state != 1) return 0;
@@ -365,10 +383,18 @@ int dev_stop_holder(int seg0_id) {
    * looks every 10 ms and stays attached for no longer than each look, so
    * dying while it waits (Ctrl-C on dada_db -d, a test timeout) leaves the
    * holder's count as it was */
+  const pid_t pid = v.holder_pid;
   for (int i = 0; i < 1000; i++) { /* <= 10 s */
     struct timespec t = {0, 10 * 1000 * 1000};
     nanosleep(&t, NULL);
-    if (dev_look_seg0(seg0_id, &v) < 0 || v.holder_state == 2) return 0;
+    if (dev_look_seg0(seg0_id, &v) < 0 || v.holder_state == 2) {
+      /* and until the holder's process has ended: a holder that starts
+       * while the previous one's GPU context is still being torn down can
+       * have its first allocation refused IPC export (DESIGN.md 7b,
+       * profiles/r06_devring_*.jsonl) */
+      wait_exited(pid, 3000);
+      return 0;
+    }
   }
   snprintf(dev_err, sizeof dev_err,
            "device ring holder %d: %d process(es) still have the blocks open; it frees them when they detach",
