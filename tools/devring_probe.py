@@ -9,12 +9,14 @@ each used ring's line also carries this process's open file descriptors
 and mapped size after the ring was closed, so a per-import leak in the HIP
 runtime's IPC path shows as steady growth.
 
-  python3 tools/devring_probe.py [ROUNDS] [use] [noprimer] [pause=S]
+  python3 tools/devring_probe.py [ROUNDS] [use] [noprimer] [pause=S] [handles]
     use       open and write every ring
     noprimer  the holders make no primer allocation (DADA_HOLDER_NO_PRIMER=1):
               block 0 is their first allocation, as before round 5
     pause=S   sleep S seconds between a ring's destroy and the next create
               (the previous holder has then long exited)
+    handles   read every block's 64-B IPC handle from its segment (no block is
+              opened) and report handles that recur across rings
 """
 import collections
 import json
@@ -40,6 +42,26 @@ def _vm() -> dict:
     return out
 
 
+def _handles(key: int, nbufs: int) -> list:
+    """the 64-B IPC handle in each block's segment (key + 0x10000 (10 + i)),
+    read through SysV calls without opening the block"""
+    import ctypes
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.shmat.restype = ctypes.c_void_p
+    libc.shmat.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    libc.shmdt.argtypes = [ctypes.c_void_p]
+    out = []
+    for i in range(nbufs):
+        sid = libc.shmget(key + 0x10000 * (10 + i), 0, 0)
+        if sid < 0:
+            out.append(None)
+            continue
+        a = libc.shmat(sid, None, 0o10000)  # SHM_RDONLY
+        out.append(ctypes.string_at(a, 64).hex())
+        libc.shmdt(ctypes.c_void_p(a))
+    return out
+
+
 def main():
     import resource
     print(json.dumps({"rlimit_nofile": resource.getrlimit(resource.RLIMIT_NOFILE),
@@ -50,6 +72,9 @@ def main():
     env = dict(os.environ)
     if "noprimer" in sys.argv[2:]:
         env["DADA_HOLDER_NO_PRIMER"] = "1"
+    want_handles = "handles" in sys.argv[2:]
+    seen = {}  # handle -> first (round, case, block)
+    recur = []
     print(json.dumps({"use": use, "noprimer": "noprimer" in sys.argv[2:], "pause_s": pause}), flush=True)
     import tempfile
     tmp = tempfile.mkdtemp(prefix="devring_probe_")
@@ -75,6 +100,14 @@ def main():
                         # the holder's first failed try: call, error, address range
                         print(json.dumps({"retry": f"{sz}x{nb}", "round": r,
                                           "holder": p.stderr.strip()[-300:]}), flush=True)
+                    if p.returncode == 0 and want_handles:
+                        for i, h in enumerate(_handles(key, nb)):
+                            if h in seen:
+                                recur.append({"handle": h, "first": seen[h], "again": [r, f"{sz}x{nb}", i]})
+                            else:
+                                seen.setdefault(h, [r, f"{sz}x{nb}", i])
+                        if r == 0 and sz == SIZES[0] and nb == 2:
+                            print(json.dumps({"sample_handles": _handles(key, nb)}), flush=True)
                     if p.returncode != 0:
                         fails[f"{sz}x{nb}"] += 1
                         e = p.stderr.strip()[-200:]
@@ -104,6 +137,9 @@ def main():
                     dada.destroy_ring(key)
         print(json.dumps({"round": r, "attempts": attempts, "failures": sum(fails.values()),
                           "retries": sum(retries.values()), "primer_refused": sum(primer.values())}), flush=True)
+    if want_handles:
+        print(json.dumps({"distinct_handles": len(seen), "recurring": len(recur), "recur_examples": recur[:10]}),
+              flush=True)
     print(json.dumps({"attempts": attempts, "failures": sum(fails.values()), "by_case": fails,
                       "retries": sum(retries.values()), "retries_by_case": retries,
                       "primer_refused": sum(primer.values()), "primer_refused_by_case": primer,
