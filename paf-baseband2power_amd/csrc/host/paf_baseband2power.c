@@ -736,6 +736,7 @@ static void run_device_pipelined(shared_t *sh) {
   const size_t sb = (sh->obytes * bmax + 4095) / 4096 * 4096;
   float *spec = aligned_alloc(4096, 3 * sb); /* spectra of batches k-2, k-1, k */
   if (!spec || ipcbuf_set_read_depth(&in->buf, depth < 2 ? 2 : depth) < 0) {
+    multilog(sh->log, LOG_ERR, "%s", !spec ? "cannot allocate the output spectra" : "read depth refused");
     free(spec);
     sh->failed = 1;
     return;
@@ -825,7 +826,10 @@ static void run_device_pipelined(shared_t *sh) {
       if (rc == B2P_OK && !blk && !g_stop) continue; /* the next block decides */
     }
     /* end of data, a partial block, a stop or a failure: drain the pipeline */
-    if (b2p_sync(s->ctx) != B2P_OK) sh->failed = 1;
+    if (b2p_sync(s->ctx) != B2P_OK) {
+      multilog(sh->log, LOG_ERR, "drain: %s", b2p_last_error(s->ctx));
+      sh->failed = 1;
+    }
     for (; held; held--) ipcio_close_block_read(in, 0);
     for (; !sh->failed && written < k; written++)
       for (uint32_t j = 0; !sh->failed && j < bat[written % 3].n; j++)

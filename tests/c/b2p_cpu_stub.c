@@ -33,6 +33,11 @@
  * RCCL mode (mode 0) with two members on one device is refused, as RCCL
  * refuses it ("Duplicate GPU detected"), naming the call.
  *
+ * B2P_STUB_FAIL=name:n[,name:n...] (environment): the n-th call (1-based,
+ * process-wide) of entry point `name` fails with B2P_EHIP as a HIP error
+ * would, so the stage's failure paths run: every member stops, the output
+ * transfer ends, the ERR line reaches stderr, nothing hangs.
+ *
  * B2P_STUB_DELAY_US=D (environment): each queue runs on a thread of its own
  * and sleeps 0..D us before every piece of work, so the stage's fences,
  * held blocks and gathers are exercised against work that completes late --
@@ -81,6 +86,45 @@ struct queue {
   int async, stop;
   unsigned delay_us, seed;
 };
+
+static pthread_mutex_t g_inj_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+  char name[48];
+  int n, calls;
+} g_inj[8];
+static int g_ninj = -1;
+
+/* 1 when this call of `name` is the one B2P_STUB_FAIL names */
+static int inject(const char *name) {
+  int hit = 0;
+  pthread_mutex_lock(&g_inj_mu);
+  if (g_ninj < 0) {
+    g_ninj = 0;
+    const char *e = getenv("B2P_STUB_FAIL");
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s", e ? e : "");
+    for (char *save = NULL, *t = strtok_r(buf, ",", &save); t && g_ninj < 8; t = strtok_r(NULL, ",", &save)) {
+      char *colon = strchr(t, ':');
+      if (!colon) continue;
+      *colon = 0;
+      snprintf(g_inj[g_ninj].name, sizeof g_inj[g_ninj].name, "%s", t);
+      g_inj[g_ninj].n = atoi(colon + 1);
+      g_ninj++;
+    }
+  }
+  for (int i = 0; i < g_ninj; i++)
+    if (!strcmp(g_inj[i].name, name) && ++g_inj[i].calls == g_inj[i].n) hit = 1;
+  pthread_mutex_unlock(&g_inj_mu);
+  return hit;
+}
+
+#define INJECT(name)                                                        \
+  do {                                                                      \
+    if (inject(name)) {                                                     \
+      fprintf(stderr, "b2p_cpu_stub: injected failure of %s\n", name);     \
+      return B2P_EHIP;                                                      \
+    }                                                                       \
+  } while (0)
 
 static unsigned stub_delay_us(void) {
   const char *e = getenv("B2P_STUB_DELAY_US");
@@ -390,6 +434,7 @@ int b2p_dev_free(b2p_ctx_t *c, void *dev) { /* after the stream, as hipStreamSyn
 }
 
 int b2p_memcpy(b2p_ctx_t *c, void *dst, const void *src, size_t bytes, int kind) {
+  INJECT("b2p_memcpy");
   if (!c || !dst || !src || kind < 1 || kind > 3) return B2P_EINVAL;
   queue_wait(&c->q, queue_pos(&c->q)); /* the library syncs the stream, then copies */
   memcpy(dst, src, bytes);
@@ -412,6 +457,7 @@ static void flush_pending(b2p_ctx_t *c) {
 
 int b2p_push(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device) {
   if (!c) return B2P_EINVAL;
+  INJECT("b2p_push");
   if (nbytes == 0) return B2P_OK;
   if (!buf) return B2P_EINVAL;
   if (nbytes % c->frame_bytes) return B2P_ERAGGED;
@@ -451,16 +497,19 @@ static int finish_common(b2p_ctx_t *c, void *out, int raw) {
 }
 
 int b2p_finish_async(b2p_ctx_t *c, float *out, int out_is_device) {
+  INJECT("b2p_finish_async");
   (void)out_is_device;
   return finish_common(c, out, 0);
 }
 
 int b2p_finish_partial_async(b2p_ctx_t *c, uint64_t *sums, int sums_is_device) {
+  INJECT("b2p_finish_partial_async");
   (void)sums_is_device;
   return finish_common(c, sums, 1);
 }
 
 int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64_t nsamp_total, float *out) {
+  INJECT("b2p_finalize_sums");
   if (!c || !sums || !out) return B2P_EINVAL;
   flush_pending(c);
   op_t *o = new_op(OP_CONV);
@@ -475,6 +524,7 @@ int b2p_finalize_sums(b2p_ctx_t *c, const uint64_t *sums, uint64_t nspec, uint64
 
 int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, float *out, int out_is_device) {
   if (!c || !out) return B2P_EINVAL;
+  INJECT("b2p_integrate");
   if (c->samples) return B2P_EINVAL; /* "b2p_integrate with a push pending" */
   if (nbytes != c->block_bytes) return nbytes % c->frame_bytes ? B2P_ERAGGED : B2P_EINVAL;
   int rc = b2p_push(c, buf, nbytes, is_device);
@@ -483,6 +533,7 @@ int b2p_integrate(b2p_ctx_t *c, const void *buf, size_t nbytes, int is_device, f
 
 int b2p_integrate_n(b2p_ctx_t *c, const void *const *bufs, uint32_t nblk, float *out, int out_is_device) {
   (void)out_is_device;
+  INJECT("b2p_integrate_n");
   if (!c || !bufs || !out || !nblk || nblk > B2P_MAX_BLOCKS) return B2P_EINVAL;
   if (c->samples) return B2P_EINVAL;
   for (uint32_t b = 0; b < nblk; b++)
@@ -506,6 +557,7 @@ int b2p_integrate_n(b2p_ctx_t *c, const void *const *bufs, uint32_t nblk, float 
 }
 
 int b2p_fence(b2p_ctx_t *c, uint64_t *ticket) {
+  INJECT("b2p_fence");
   if (!c || !ticket) return B2P_EINVAL;
   c->fence_seq[c->fence_next % 8] = queue_pos(&c->q);
   *ticket = c->fence_next++;
@@ -513,17 +565,20 @@ int b2p_fence(b2p_ctx_t *c, uint64_t *ticket) {
 }
 
 int b2p_fence_wait(b2p_ctx_t *c, uint64_t ticket) {
+  INJECT("b2p_fence_wait");
   if (!c || ticket >= c->fence_next) return B2P_EINVAL;
   queue_wait(&c->q, c->fence_next - ticket > 8 ? queue_pos(&c->q) : c->fence_seq[ticket % 8]);
   return B2P_OK;
 }
 
 int b2p_fence_done(b2p_ctx_t *c, uint64_t ticket) {
+  INJECT("b2p_fence_done");
   if (!c || ticket >= c->fence_next) return B2P_EINVAL;
   return queue_reached(&c->q, c->fence_next - ticket > 8 ? queue_pos(&c->q) : c->fence_seq[ticket % 8]);
 }
 
 int b2p_flush(b2p_ctx_t *c) {
+  INJECT("b2p_flush");
   if (!c) return B2P_EINVAL;
   flush_pending(c);
   return B2P_OK;
@@ -531,6 +586,7 @@ int b2p_flush(b2p_ctx_t *c) {
 
 int b2p_sync(b2p_ctx_t *c) {
   if (!c) return B2P_EINVAL;
+  INJECT("b2p_sync");
   flush_pending(c);
   queue_wait(&c->q, queue_pos(&c->q));
   return B2P_OK;
@@ -590,6 +646,7 @@ static void copy_on(b2p_group_t *g, void *dst, const void *src, uint64_t n) {
 
 /* behind everything each member has enqueued, its deferred finalize included */
 int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
+  INJECT("b2p_group_gather");
   if (!g || !spectra || !root_out) return B2P_EINVAL;
   const uint64_t nout = g->m[0]->nout;
   for (int r = 0; r < g->n; r++) {
@@ -602,6 +659,7 @@ int b2p_group_gather(b2p_group_t *g, float *const *spectra, float *root_out) {
 
 int b2p_group_gather_async(b2p_group_t *g, float *const *spectra, uint32_t nspec, float *root_out,
                            const uint64_t *tickets, float *host_out, uint64_t *gticket) {
+  INJECT("b2p_group_gather_async");
   if (!g || !spectra || !root_out || !tickets || !gticket || nspec < 1) return B2P_EINVAL;
   if (g->gnext >= 8) queue_wait(&g->q, g->gseq[(g->gnext - 8) % 8]); /* its event slot is reused */
   for (int r = 0; r < g->n; r++) { /* b2p_internal_fence_event: one of the member's last 8 tickets */
@@ -622,6 +680,7 @@ int b2p_group_gather_async(b2p_group_t *g, float *const *spectra, uint32_t nspec
 }
 
 int b2p_group_wait(b2p_group_t *g, uint64_t gticket) {
+  INJECT("b2p_group_wait");
   if (!g || gticket >= g->gnext) return B2P_EINVAL;
   if (g->gnext - gticket > 8) return B2P_OK;
   queue_wait(&g->q, g->gseq[gticket % 8]);
@@ -629,12 +688,14 @@ int b2p_group_wait(b2p_group_t *g, uint64_t gticket) {
 }
 
 int b2p_group_done(b2p_group_t *g, uint64_t gticket) {
+  INJECT("b2p_group_done");
   if (!g || gticket >= g->gnext) return B2P_EINVAL;
   if (g->gnext - gticket > 8) return 1;
   return queue_reached(&g->q, g->gseq[gticket % 8]);
 }
 
 int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint64_t *root_sum) {
+  INJECT("b2p_group_reduce");
   if (!g || !sums || !root_sum || !count) return B2P_EINVAL;
   for (int r = 0; r < g->n; r++) {
     flush_pending(g->m[r]);
@@ -660,6 +721,7 @@ int b2p_group_reduce(b2p_group_t *g, uint64_t *const *sums, uint64_t count, uint
 }
 
 int b2p_group_sync(b2p_group_t *g) {
+  INJECT("b2p_group_sync");
   if (!g) return B2P_EINVAL;
   queue_wait(&g->q, queue_pos(&g->q));
   for (int r = 0; r < g->n; r++) queue_wait(&g->m[r]->q, queue_pos(&g->m[r]->q));

@@ -313,3 +313,155 @@ def test_stage_recorded_gather_case_async(stages, tmp_path):
         assert np.array_equal(sp[0, 0], want[0]) and np.array_equal(sp[0, 1], want[1]), run
         log = (d / "paf_baseband2power.log").read_text()
         assert "FINISH PAF_PROCESS: 1 integrations, 1 skipped, ok" in log, log[-800:]
+
+
+@pytest.mark.parametrize("mode,fail", [
+    ("single", "b2p_push:3"),
+    ("single_dev", "b2p_integrate:1,b2p_integrate_n:1"),
+    ("single_dev", "b2p_sync:1"),
+    ("gathered", "b2p_push:4"),
+    ("gathered", "b2p_group_gather:2"),
+    ("gathered_dev", "b2p_integrate:2,b2p_integrate_n:2"),
+    ("gathered_dev", "b2p_group_gather_async:1"),
+    ("gathered_dev", "b2p_group_wait:1"),
+    ("split", "b2p_push:3"),
+    ("split", "b2p_group_reduce:2"),
+])
+def test_stage_failure_paths(stages, tmp_path, mode, fail):
+    """a HIP error in the middle of a run, injected into the CPU double
+    (B2P_STUB_FAIL) in each threading mode: the stage stops every member,
+    ends the output transfer (paf_dbdisk exits 0), exits 1 within seconds,
+    repeats its ERR line on stderr, and every spectrum it did write equals
+    the oracle's -- no hang, no garbage after a failure"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=32, npol_out=1, nsamp_int=256)
+    nmem = 1 if mode.startswith("single") else 2
+    nblk = 6
+    rings = 1 if mode in ("single", "single_dev", "split") else nmem
+    base, kout = _key(), _key()
+    keys = [base + 0x10 * r for r in range(rings)]
+    blocks = [[co.fill_synthetic(g, g.block_bytes, 31, r, b) for b in range(nblk)] for r in range(rings)]
+    hdr = (f"HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 32\nNCHUNK 1\nNCHAN_CHUNK 32\nNSAMP_DF 1\n"
+           "BYTE_ORDER LE\nTSAMP 0.84375\n")
+    for k in keys + [kout]:
+        dada.destroy_ring(k)
+    for k in keys:
+        dada.create_ring(k, nblk + 2, g.block_bytes)  # every block and the end of data fit: writers never wait
+    onsub = nmem if mode.startswith("gathered") else 1
+    dada.create_ring(kout, 8, onsub * g.nout * 4)
+    args = ["-f", "header"]
+    if mode.startswith("gathered"):
+        args += ["-n", str(nmem), "-G", "copy"]
+    if mode == "split":
+        args += ["-t", "2", "-G", "copy"]
+    out = tmp_path / "power.dada"
+    env = dict(os.environ, B2P_STUB_FAIL=fail, B2P_STUB_DELAY_US="300")
+    procs = []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([stages["dev" if mode.endswith("_dev") else "host"], "-a", f"{base:x}", "-b",
+                                   f"{kout:x}", "-c", str(tmp_path), "-d", "0"] + args,
+                                  stderr=subprocess.PIPE, text=True, env=env)]
+        for k, bl in zip(keys, blocks):
+            with dada.Hdu(k, "W") as w:
+                w.write_header(hdr)
+                for b in bl:
+                    w.write_block(b.tobytes())
+        _, err = procs[1].communicate(timeout=60)
+        assert procs[1].returncode == 1, err
+        _, derr = procs[0].communicate(timeout=60)
+        assert procs[0].returncode == 0, derr
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for k in keys + [kout]:
+            dada.destroy_ring(k)
+    assert "b2p_cpu_stub: injected failure of" in err, err
+    assert "] ERR: " in err and "FAILED, log" in err, err
+    log = open(str(tmp_path / "paf_baseband2power.log")).read()
+    assert "FAILED" in log.splitlines()[-1], log[-800:]
+    sp = data.view(np.uint32).reshape(-1, onsub, g.nout)
+    assert sp.shape[0] < nblk
+    for b in range(sp.shape[0]):
+        for r in range(onsub):
+            assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=1).view(np.uint32)), (b, r)
+
+
+_CALLS = ["b2p_push", "b2p_integrate", "b2p_integrate_n", "b2p_finish_async", "b2p_finish_partial_async",
+          "b2p_finalize_sums", "b2p_fence", "b2p_fence_wait", "b2p_fence_done", "b2p_flush", "b2p_sync",
+          "b2p_memcpy", "b2p_group_gather", "b2p_group_gather_async", "b2p_group_wait", "b2p_group_done",
+          "b2p_group_reduce", "b2p_group_sync"]
+
+
+@pytest.mark.parametrize("mode", ["single", "single_dev", "gathered", "gathered_dev", "split"])
+def test_stage_never_fails_silently(stages, tmp_path, mode):
+    """every entry point the stage calls, failed at its 1st and its 2nd call
+    (B2P_STUB_FAIL), in every threading mode: the stage either never made
+    that call (exit 0, every spectrum) or exits 1 within seconds with an ERR
+    line on stderr naming what failed, the output transfer ended, and only
+    correct spectra written -- no silent exit, no hang"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=128)
+    nmem = 1 if mode.startswith("single") else 2
+    nblk = 4
+    rings = 1 if mode in ("single", "single_dev", "split") else nmem
+    onsub = nmem if mode.startswith("gathered") else 1
+    blocks = [[co.fill_synthetic(g, g.block_bytes, 47, r, b) for b in range(nblk)] for r in range(rings)]
+    want = [[co.power(g, blocks[r][b], nthreads=1).view(np.uint32) for b in range(nblk)] for r in range(rings)]
+    hdr = (f"HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 16\nNCHUNK 1\nNCHAN_CHUNK 16\nNSAMP_DF 1\n"
+           "BYTE_ORDER LE\nTSAMP 0.84375\n")
+    args = ["-f", "header"] + (["-n", str(nmem), "-G", "copy"] if mode.startswith("gathered") else []) \
+        + (["-t", "2", "-G", "copy"] if mode == "split" else [])
+    failed_runs = 0
+    for call in _CALLS:
+        for nth in (1, 2):
+            base, kout = _key(), _key()
+            keys = [base + 0x10 * r for r in range(rings)]
+            for k in keys + [kout]:
+                dada.destroy_ring(k)
+            for k in keys:
+                dada.create_ring(k, nblk + 2, g.block_bytes)
+            dada.create_ring(kout, nblk + 2, onsub * g.nout * 4)
+            d = tmp_path / f"{call}_{nth}"
+            d.mkdir()
+            env = dict(os.environ, B2P_STUB_FAIL=f"{call}:{nth}", B2P_STUB_DELAY_US="200")
+            procs = []
+            try:
+                procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o",
+                                           str(d / "p.dada")], stderr=subprocess.PIPE),
+                         subprocess.Popen([stages["dev" if mode.endswith("_dev") else "host"], "-a", f"{base:x}",
+                                           "-b", f"{kout:x}", "-c", str(d), "-d", "0"] + args,
+                                          stderr=subprocess.PIPE, text=True, env=env)]
+                for k, bl in zip(keys, blocks):
+                    with dada.Hdu(k, "W") as w:
+                        w.write_header(hdr)
+                        for b in bl:
+                            w.write_block(b.tobytes())
+                _, err = procs[1].communicate(timeout=60)
+                _, derr = procs[0].communicate(timeout=60)
+                rc = procs[1].returncode
+                assert procs[0].returncode == 0, (call, nth, derr)
+                _, data = dada.read_dada_file(str(d / "p.dada"))
+            finally:
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+                        p.wait()
+                for k in keys + [kout]:
+                    dada.destroy_ring(k)
+            injected = "injected failure of" in err
+            sp = data.view(np.uint32).reshape(-1, onsub, g.nout)
+            if rc == 0:
+                assert not injected, (call, nth, err)  # a failure the stage swallowed
+                assert sp.shape[0] == nblk, (call, nth)
+            else:
+                failed_runs += 1
+                assert rc == 1 and injected, (call, nth, rc, err)
+                assert "] ERR: " in err and "FAILED, log" in err, (call, nth, err)
+                assert sp.shape[0] <= nblk, (call, nth)  # (a failure after the last output still fails the run)
+            for b in range(sp.shape[0]):
+                for r in range(onsub):
+                    assert np.array_equal(sp[b, r], want[r][b]), (call, nth, b, r)
+    assert failed_runs >= 4, failed_runs  # the mode's own calls were reached
