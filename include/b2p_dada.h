@@ -167,7 +167,9 @@ const char *dada_device_error(void);
  * ipcio_open_block_read returns NULL -- instead of resuming, once a signal
  * has interrupted it.  Async-signal-safe: meant for a SIGINT/SIGTERM
  * handler, so a stage stops between blocks and ends its output transfer
- * (unlock_write) cleanly instead of dying mid-ring. */
+ * (unlock_write) cleanly instead of dying mid-ring; also callable from any
+ * thread (the flag is a lock-free atomic), e.g. when one input ring failed
+ * and the threads waiting on the others must be woken. */
 void dada_interrupt_waits(void);
 
 /* ---- ipcio: block-level streaming over an ipcbuf ---- */

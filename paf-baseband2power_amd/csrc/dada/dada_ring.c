@@ -31,6 +31,7 @@
 #include <inttypes.h>
 #include <signal.h>
 #include <stdarg.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -43,8 +44,8 @@
 #include "b2p_dada.h"
 #include "dada_internal.h"
 
-/* set by dada_interrupt_waits (a signal handler): interrupted waits fail */
-static volatile sig_atomic_t g_interrupt;
+/* set by dada_interrupt_waits (a signal handler, or any thread): interrupted waits fail */
+static atomic_int g_interrupt; /* lock-free: set from a signal handler or another thread */
 
 void dada_interrupt_waits(void) { g_interrupt = 1; }
 

@@ -135,6 +135,10 @@ static void usage(void) {
  * Ring waits in progress give up (dada_interrupt_waits); worker threads
  * blocked in one are woken with SIGUSR2 by the main thread. */
 static volatile sig_atomic_t g_stop;
+/* a member's input ring failed under it (next_block): every other member
+ * waiting on its own ring is woken the same way, so the run ends instead of
+ * waiting for blocks that are not coming */
+static atomic_int g_abort; /* written by a worker, read by every thread */
 
 static void on_stop(int sig) {
   (void)sig;
@@ -295,12 +299,29 @@ static void echo_errors(FILE *fp, long from, const char *fname) {
 }
 
 /* next input block, or NULL at the end of the transfer (checked with
- * ipcbuf_eod first, so a reader never waits on a ring whose transfer ended) */
-static char *next_block(dada_hdu_t *h, uint64_t *bytes) {
+ * ipcbuf_eod first, so a reader never waits on a ring whose transfer
+ * ended).  A read that fails instead -- the ring's semaphores removed under
+ * the stage (EIDRM), not an end of data nor a stop signal -- sets *failed
+ * (the caller reports it and fails the run: it is not an end of data). */
+static char *next_block(dada_hdu_t *h, uint64_t *bytes, int *failed) {
   uint64_t bid = 0;
+  *failed = 0;
   if (ipcbuf_eod(data_buf(h))) return NULL;
-  return ipcio_open_block_read(h->data_block, bytes, &bid);
+  errno = 0;
+  char *p = ipcio_open_block_read(h->data_block, bytes, &bid);
+  *failed = !p && errno && !g_stop && !g_abort ? errno : 0;
+  if (*failed) {
+    g_abort = 1;
+#if DEVICE_RINGS
+    dada_interrupt_waits(); /* the main thread then signals the members still waiting */
+#endif
+  }
+  return p;
 }
+
+/* have[] of a member whose read failed (next_block): the round stops, and
+ * the run fails */
+#define HAVE_READ_FAILED (-2)
 
 /* ---- the integration loop, one thread per sub-band ---------------------- */
 
@@ -382,11 +403,15 @@ static void *worker(void *arg) {
   for (;;) {
     uint64_t bytes = 0;
     const double t_ask = now_s();
-    char *blk = g_stop ? NULL : next_block(s->in, &bytes);
+    int rfail = 0;
+    char *blk = g_stop || g_abort ? NULL : next_block(s->in, &bytes, &rfail);
     const double t_got = now_s();
+    if (rfail)
+      multilog(sh->log, LOG_ERR, "sub-band %d: reading input ring %x failed (%s)", w->r, (unsigned)s->key,
+               strerror(rfail));
     /* a 0-byte block only carries the end of data (PSRDADA's ipcio_close
      * after a full block): it ends the loop like a NULL one */
-    sh->have[w->r] = !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
+    sh->have[w->r] = rfail ? HAVE_READ_FAILED : !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
     pthread_barrier_wait(&sh->bar); /* all sub-bands agree on this round */
     int stop = sh->failed, skip = 0;
     for (int r = 0; r < sh->nsub; r++) {
@@ -396,7 +421,10 @@ static void *worker(void *arg) {
     if (stop || skip) {
       if (blk) ipcio_close_block_read(s->in->data_block, bytes);
       int whole = 0; /* a member had a whole block for a round another member's end of data stops */
-      for (int r = 0; r < sh->nsub; r++) whole |= sh->have[r] == 1;
+      for (int r = 0; r < sh->nsub; r++) {
+        whole |= sh->have[r] == 1;
+        if (w->r == 0 && sh->have[r] == HAVE_READ_FAILED) sh->failed = 1; /* stop is decided already */
+      }
       if (w->r == 0 && skip && !stop) {
         sh->nskipped++;
         if (sh->nsub > 1) sh->end_lost = 1;
@@ -548,9 +576,13 @@ static void *worker_gather_dev(void *arg) {
   for (uint64_t k = 0;; k++) {
     const void *blks[B2P_MAX_BLOCKS];
     uint64_t bytes = 0, bid = 0;
-    char *blk = g_stop || sh->failed ? NULL : next_block(s->in, &bytes);
+    int rfail = 0;
+    char *blk = g_stop || g_abort || sh->failed ? NULL : next_block(s->in, &bytes, &rfail);
     int taken = blk ? 1 : 0, avail = 0;
-    sh->have[r] = !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
+    if (rfail)
+      multilog(sh->log, LOG_ERR, "sub-band %d: reading input ring %x failed (%s)", r, (unsigned)s->key,
+               strerror(rfail));
+    sh->have[r] = rfail ? HAVE_READ_FAILED : !blk || !bytes ? -1 : (bytes == s->rbufsz ? 1 : 0);
     if (sh->have[r] == 1) {
       blks[0] = blk;
       const uint64_t q = ipcbuf_get_nfull_iread(&in->buf, in->buf.iread);
@@ -617,8 +649,10 @@ static void *worker_gather_dev(void *arg) {
        * first such round counts one skipped integration, however the
        * writers' timing split the blocks between the two rounds */
       int lost = skip && !stop;
-      for (int q = 0; q < sh->nsub; q++)
+      for (int q = 0; q < sh->nsub; q++) {
         lost |= (uint32_t)sh->got[q] > mm || sh->partial[q] || (stop && sh->have[q] == 1);
+        if (stop && sh->have[q] == HAVE_READ_FAILED) sh->failed = 1; /* the members break below */
+      }
       if (lost && !sh->end_lost) {
         sh->end_lost = 1;
         sh->nskipped++;
@@ -750,7 +784,15 @@ static void run_device_pipelined(shared_t *sh) {
   for (;;) {
     const void *blks[B2P_MAX_BLOCKS];
     uint64_t bytes = 0, bid = 0;
-    char *blk = g_stop ? NULL : ipcio_open_block_read(in, &bytes, &bid);
+    char *blk = NULL;
+    if (!g_stop && !ipcbuf_eod(&in->buf)) {
+      errno = 0;
+      blk = ipcio_open_block_read(in, &bytes, &bid);
+      if (!blk && errno && !g_stop) { /* not an end of data: the ring failed under the stage */
+        multilog(sh->log, LOG_ERR, "reading input ring %x failed (%s)", (unsigned)s->key, strerror(errno));
+        sh->failed = 1;
+      }
+    }
     uint32_t n = 0;
     while (blk && bytes == s->rbufsz) { /* gather this batch */
       blks[n++] = blk;
@@ -861,12 +903,17 @@ static void *worker_split(void *arg) {
   for (;;) {
     if (w->r == 0) {
       sh->blk_bytes = 0;
-      sh->blk = g_stop ? NULL : next_block(s0->in, &sh->blk_bytes);
+      int rfail = 0;
+      sh->blk = g_stop || g_abort ? NULL : next_block(s0->in, &sh->blk_bytes, &rfail);
       pin_block(s0, sh->blk, sh->log);
-      sh->have[0] = !sh->blk || !sh->blk_bytes ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
+      if (rfail)
+        multilog(sh->log, LOG_ERR, "reading input ring %x failed (%s)", (unsigned)s0->key, strerror(rfail));
+      sh->have[0] = rfail ? HAVE_READ_FAILED
+                          : !sh->blk || !sh->blk_bytes ? -1 : (sh->blk_bytes == s0->rbufsz ? 1 : 0);
     }
     pthread_barrier_wait(&sh->bar);
     if (sh->have[0] <= 0 || sh->failed) {
+      if (w->r == 0 && sh->have[0] == HAVE_READ_FAILED) sh->failed = 1; /* the round stops either way */
       if (w->r == 0 && sh->blk) {
         ipcio_close_block_read(s0->in->data_block, sh->blk_bytes);
         if (sh->have[0] == 0 && !sh->failed) {
@@ -1290,7 +1337,7 @@ int main(int argc, char *argv[]) {
           joined[r] = 1;
           left--;
         }
-      if (g_stop)
+      if (g_stop || g_abort)
         for (int r = 0; r < nmem; r++)
           if (!joined[r]) pthread_kill(th[r], SIGUSR2);
       if (left) usleep(20000);

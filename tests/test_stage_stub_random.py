@@ -22,6 +22,7 @@ kinds of cases through the HIP library on a GPU."""
 import os
 import subprocess
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -465,3 +466,75 @@ def test_stage_never_fails_silently(stages, tmp_path, mode):
                 for r in range(onsub):
                     assert np.array_equal(sp[b, r], want[r][b]), (call, nth, b, r)
     assert failed_runs >= 4, failed_runs  # the mode's own calls were reached
+
+
+@pytest.mark.parametrize("mode", ["single", "single_dev", "gathered", "gathered_dev", "split"])
+def test_stage_input_ring_removed_under_it(stages, tmp_path, mode):
+    """an input ring destroyed while the stage waits on it for its next block
+    (its semaphores removed: the wait fails with EIDRM) is not an end of
+    data: the stage names the ring and the error in an ERR line on stderr,
+    wakes every other member waiting on its own ring, ends the output
+    transfer and exits 1 -- within seconds, after writing the spectra of the
+    blocks it had, each equal to the oracle's"""
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=128)
+    nmem = 1 if mode.startswith("single") else 2
+    rings = 1 if mode in ("single", "single_dev", "split") else nmem
+    onsub = nmem if mode.startswith("gathered") else 1
+    nblk = 2
+    blocks = [[co.fill_synthetic(g, g.block_bytes, 53, r, b) for b in range(nblk)] for r in range(rings)]
+    hdr = (f"HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 16\nNCHUNK 1\nNCHAN_CHUNK 16\nNSAMP_DF 1\n"
+           "BYTE_ORDER LE\nTSAMP 0.84375\n")
+    base, kout = _key(), _key()
+    keys = [base + 0x10 * r for r in range(rings)]
+    for k in keys + [kout]:
+        dada.destroy_ring(k)
+    for k in keys:
+        dada.create_ring(k, 4, g.block_bytes)
+    dada.create_ring(kout, 8, onsub * g.nout * 4)
+    args = ["-f", "header"] + (["-n", str(nmem), "-G", "copy"] if mode.startswith("gathered") else []) \
+        + (["-t", "2", "-G", "copy"] if mode == "split" else [])
+    out = tmp_path / "power.dada"
+    procs, writers = [], []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE),
+                 subprocess.Popen([stages["dev" if mode.endswith("_dev") else "host"], "-a", f"{base:x}", "-b",
+                                   f"{kout:x}", "-c", str(tmp_path), "-d", "0"] + args,
+                                  stderr=subprocess.PIPE, text=True)]
+        for k, bl in zip(keys, blocks):  # the transfers stay open: the stage waits for a third block
+            w = dada.Hdu(k, "W")
+            writers.append(w)
+            w.write_header(hdr)
+            for b in bl:
+                w.write_block(b.tobytes())
+        log = tmp_path / "paf_baseband2power.log"
+        t_end = time.time() + 20
+        while time.time() < t_end and (not log.exists() or "integration" not in log.read_text()
+                                       and "round" not in log.read_text() and "launch" not in log.read_text()):
+            time.sleep(0.05)
+        time.sleep(0.5)
+        assert procs[1].poll() is None  # waiting for the next block
+        dada.destroy_ring(keys[0])
+        _, err = procs[1].communicate(timeout=30)
+        _, derr = procs[0].communicate(timeout=30)
+        assert procs[1].returncode == 1, err
+        assert procs[0].returncode == 0, derr
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for w in writers:
+            try:
+                w.close()
+            except OSError:
+                pass
+        for k in keys + [kout]:
+            dada.destroy_ring(k)
+    assert f"reading input ring {keys[0]:x} failed" in err and "] ERR: " in err, err
+    sp = data.view(np.uint32).reshape(-1, onsub, g.nout)
+    assert sp.shape[0] == nblk, sp.shape
+    for b in range(nblk):
+        for r in range(onsub):
+            assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=1).view(np.uint32)), (b, r)
