@@ -7,7 +7,7 @@
 #          prof pmc pmc5 profbmf pmcbmf asm profasm pmcasm asmsweep ring capture matrix knobs
 #          probe skew overlap spikes patterns asmprobe h2d diskdb idlerep keeprep tune tunebmf capturemt multi
 #          benchbpl profbpl benchcmp ringq ringn drvx3 tunelay tunefs cpuspread cpuspread2 cputhreads sustained matrix4 pmc1
-#          devleak devleak20 replay9090 debughunt hunt5 cpuwait gatherhunt
+#          devleak devleak20 replay9090 debughunt hunt5 cpuwait gatherhunt churnrep
 cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 # device-ring holders (dada_db -g) left by a killed step exit after 15 idle minutes
@@ -212,6 +212,9 @@ for s in $STEPS; do
                spread2:15:passive,spread2:15:default,spread2:15:active,spread2:14:passive,spread2:12:passive &&
              run cpu_wait_b 300 python3 tools/cpu_spread_probe.py 5 \
                spread2:12:passive,spread2:14:passive,spread2:15:active,spread2:15:default,spread2:15:passive ;;
+    churnrep) # DESIGN.md item 1's candidate cause, tested: the recorded gathered case, each run right
+              # after 6 device rings made, written from this process and destroyed back to back
+              run case_churn 900 python3 -u tools/stage_case_repeat.py 30 churn=6 ;;
     devleak) # a few hundred device-ring create / write / destroy cycles in one process:
              # open fds and mapped size per ring
              run devring_leak 600 python3 tools/devring_probe.py 10 use ;;

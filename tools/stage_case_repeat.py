@@ -10,7 +10,14 @@ The case (profiles/r05_gpu_suite_gather_flake.txt): `paf_baseband2power -n 2
 processes; sub-band 0's transfer is one block, sub-band 1's two.  Every
 output is checked against the C oracle.
 
-  python3 tools/stage_case_repeat.py N    (one JSON line per run, then a summary)
+  python3 tools/stage_case_repeat.py N [churn=K]   (one JSON line per run, then a summary)
+
+churn=K tests the candidate cause named in DESIGN.md item 1: before each
+run, THIS process makes K other device rings one after another, each
+written here (its blocks imported into this long-lived process, as the GPU
+suite's in-process writers do) and read by a paf_dbdisk, and destroyed just
+before the next is made -- the churn the recorded failure ran after.  The
+case's own rings are then made at once, without a pause.
 """
 import json
 import os
@@ -32,8 +39,40 @@ from paf_b2p import dada  # noqa: E402
 BIN = dada.BIN_DIR
 
 
+def churn(k: int, tmp: str, size: int) -> dict:
+    """k device rings made, written here, read by paf_dbdisk and destroyed,
+    back to back; the holders' export records"""
+    key, rec = 0x7e80, {"rings": 0, "export_retries": 0, "primer_refused": 0}
+    sink = os.path.join(tmp, "churn.dada")
+    for i in range(k):
+        nb = (2, 4, 6)[i % 3]
+        dada.destroy_ring(key)
+        dada.create_ring(key, nb, size, device=0)
+        info = dada.device_ring_info(key)
+        rec["rings"] += 1
+        rec["export_retries"] += info["export_retries"]
+        rec["primer_refused"] += info["primer_refused"]
+        if os.path.exists(sink):
+            os.remove(sink)
+        rd = subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{key:x}", "-o", sink],
+                              stderr=subprocess.DEVNULL)
+        try:
+            with dada.Hdu(key, "W") as w:
+                w.write_header("HDR_SIZE 4096\n")
+                for _ in range(nb + 1):
+                    w.write_block(b"\1" * size)
+            rd.wait(60)
+        finally:
+            if rd.poll() is None:
+                rd.kill()
+                rd.wait()
+            dada.destroy_ring(key)
+    return rec
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    k_churn = next((int(a[6:]) for a in sys.argv[2:] if a.startswith("churn=")), 0)
     g = npo.Geom(nbit=8, big_endian=0, nchunk=11, nsamp_df=8, nchan_chunk=53, npol_out=2, nsamp_int=536, mean=1)
     nblks = [1, 2]
     blocks = [[co.fill_synthetic(g, g.block_bytes, 1440, r, b) for b in range(nblks[r])] for r in range(2)]
@@ -48,9 +87,11 @@ def main():
     base = 0x7c00
     keys, kout = [base, base + 0x10], base + 2
     fails = 0
+    print(json.dumps({"runs": n, "churn": k_churn}), flush=True)
     for run in range(n):
         d = os.path.join(tmp, f"run{run}")
         os.makedirs(d)
+        ch = churn(k_churn, tmp, g.block_bytes) if k_churn else None
         for k in keys + [kout]:
             dada.destroy_ring(k)
         for k in keys:
@@ -88,6 +129,8 @@ def main():
             os.path.join(d, "paf_baseband2power.log")) else ""
         rec = {"run": run, "ok": ok, "rcs": dict(zip(["dbdisk", "stage", "diskdb0", "diskdb1"], rcs)),
                "s": round(time.time() - t0, 2)}
+        if ch:
+            rec["churn"] = ch
         if not ok:
             fails += 1
             rec.update(stderr=errs, stage_log=log[-3000:])
