@@ -24,6 +24,19 @@
 
 #include "b2p_dada.h"
 
+/* every byte of buf to fd (a block reaches the file when it leaves the ring,
+ * as in dada_dbdisk: no stdio buffer holding small spectra back) */
+static int write_all(int fd, const char *buf, uint64_t n) {
+  while (n) {
+    const ssize_t w = write(fd, buf, n > (1u << 30) ? (1u << 30) : (size_t)n);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return -1;
+    buf += w;
+    n -= (uint64_t)w;
+  }
+  return 0;
+}
+
 static void usage(void) {
   fprintf(stdout,
           "paf_dbdisk - write a DADA ring buffer to a file\n"
@@ -86,14 +99,13 @@ int main(int argc, char **argv) {
     snprintf(ofile, sizeof ofile, "%s/%s_%016" PRIu64 ".000000.dada", dir, utc, off);
   }
   const int fd = open(ofile, O_WRONLY | O_CREAT | (overwrite ? O_TRUNC : O_EXCL), 0644);
-  FILE *fp = fd >= 0 ? fdopen(fd, "wb") : NULL;
-  if (!fp) {
+  if (fd < 0) {
     fprintf(stderr, "paf_dbdisk: cannot open %s (%s)%s\n", ofile, strerror(errno),
             errno == EEXIST ? "; -W overwrites" : "");
     return EXIT_FAILURE;
   }
   int rc = EXIT_SUCCESS;
-  if (fwrite(hdu->header, 1, hdu->header_size, fp) != hdu->header_size) rc = EXIT_FAILURE;
+  if (write_all(fd, hdu->header, hdu->header_size) < 0) rc = EXIT_FAILURE;
   uint64_t total = 0, nblk = 0;
   ipcbuf_t *db = &hdu->data_block->buf;
   char *stage = NULL; /* a GPU-resident ring's blocks come back through host */
@@ -102,14 +114,19 @@ int main(int argc, char **argv) {
     uint64_t bytes = 0, bid = 0;
     char *b = ipcio_open_block_read(hdu->data_block, &bytes, &bid);
     if (!b) break;
-    if (stage && ipcbuf_copy_out(db, stage, b, bytes) < 0) rc = EXIT_FAILURE;
-    if (bytes && fwrite(stage ? stage : b, 1, bytes, fp) != bytes) rc = EXIT_FAILURE;
+    if (stage && ipcbuf_copy_out(db, stage, b, bytes) < 0) {
+      multilog(log, LOG_ERR, "dbdisk: block %" PRIu64 " from the GPU: %s", nblk, dada_device_error());
+      rc = EXIT_FAILURE;
+    } else if (bytes && write_all(fd, stage ? stage : b, bytes) < 0) {
+      multilog(log, LOG_ERR, "dbdisk: writing %s failed (%s)", ofile, strerror(errno));
+      rc = EXIT_FAILURE;
+    }
     ipcio_close_block_read(hdu->data_block, bytes);
     total += bytes;
     if (bytes) nblk++; /* a 0-byte block only carries the end of data */
   }
   free(stage);
-  fclose(fp);
+  if (close(fd) < 0) rc = EXIT_FAILURE;
   multilog(log, LOG_INFO, "dbdisk: %s: %" PRIu64 " B in %" PRIu64 " blocks", ofile, total, nblk);
   dada_hdu_unlock_read(hdu);
   dada_hdu_destroy(hdu);

@@ -405,6 +405,31 @@ def test_dbdisk_default_file_name(tmp_path, ring):
     assert os.listdir(tmp_path) == ["2018-11-05-00:00:00_0000000000000000.000000.dada"]
 
 
+def test_dbdisk_writes_each_block_as_it_leaves_the_ring(tmp_path, ring):
+    """a spectrum is in the file once paf_dbdisk has taken it from the ring,
+    while the transfer is still open (as dada_dbdisk writes: no stdio buffer
+    holding small blocks back until it fills or the transfer ends)"""
+    k = ring(4, 1344)  # one 336-channel fp32 spectrum per block (header_baseband2power.txt:42)
+    out = tmp_path / "power.dada"
+    sink = subprocess.Popen([f"{BIN}/paf_dbdisk", "-k", f"{k:x}", "-o", str(out)], stderr=subprocess.PIPE)
+    try:
+        with dada.Hdu(k, "W") as w:
+            w.write_header(TEMPLATE)
+            for n in (1, 2):
+                w.write_block(bytes([n]) * 1344)
+                t_end = time.time() + 10
+                while (not out.exists() or out.stat().st_size < 4096 + n * 1344) and time.time() < t_end:
+                    time.sleep(0.01)
+                assert out.stat().st_size == 4096 + n * 1344
+        assert sink.wait(30) == 0, sink.stderr.read()
+    finally:
+        if sink.poll() is None:
+            sink.kill()
+            sink.wait()
+    _, data = dada.read_dada_file(str(out))
+    assert data.tobytes() == b"\1" * 1344 + b"\2" * 1344
+
+
 # ---- configs[0]: 256 ch x 2 pol, 1024x1024 integrate from a diskdb file, CPU path ---
 
 def test_config1_diskdb_plumbing_cpu(tmp_path, ring):
