@@ -11,6 +11,8 @@ parses (the reference's launcher is a SyntaxError at :90 and reads undefined
 args.psrname / args.dfname at :37-38), stops the other stages if one fails,
 and with -s N runs N independent sub-band chains, chain r on GPU r with ring
 keys KEY + 0x10*r (one GPU, one stream, one ring per sub-band).
+With --pin it binds the stages to CPUs as the reference does (`taskset -c`,
+`dada_dbdisk -b`: paf-baseband2power.py:68,80,83,86-95).
 """
 from __future__ import annotations
 
@@ -53,6 +55,38 @@ def _bin(name: str, bin_dir: str | None = None) -> str:
     return os.path.join(bin_dir or dada.BIN_DIR, name)
 
 
+def pin_cpus(pin: int | None, r: int, gather: bool = False) -> tuple:
+    """(paf_diskdb, paf_baseband2power, paf_dbdisk) CPUs of chain r, or Nones
+    without pinning.  The reference's launcher binds its one chain to CPUs 0,
+    1, 2 (diskdb_cpu, baseband2power_cpu, dbdisk_cpu, paf-baseband2power.py
+    :68,80,83); here chain r takes pin + 3r .. pin + 3r + 2.  One gathered
+    process (-n N) has one stage and one sink: pin + 1 and pin + 2, the
+    diskdb of sub-band 0 on pin and of sub-band r > 0 on pin + 2 + r."""
+    if pin is None:
+        return None, None, None
+    if gather:
+        return (pin if r == 0 else pin + 2 + r), pin + 1, pin + 2
+    return pin + 3 * r, pin + 3 * r + 1, pin + 3 * r + 2
+
+
+def _check_pin(pin: int | None, nsub: int, gather: bool) -> None:
+    if pin is None:
+        return
+    want = {c for r in range(nsub) for c in pin_cpus(pin, r, gather)}
+    bad = sorted(want - os.sched_getaffinity(0))
+    if pin < 0 or bad:
+        raise ValueError(f"--pin {pin}: CPU(s) {bad or [pin]} not available to this process "
+                         f"(allowed: {sorted(os.sched_getaffinity(0))})")
+
+
+def _taskset(cpu: int | None, cmd: list) -> list:
+    return cmd if cpu is None else ["taskset", "-c", str(cpu)] + cmd
+
+
+def _dbdisk(kout: int, out: str, cpu: int | None) -> list:
+    return [_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"] + ([] if cpu is None else ["-b", str(cpu)])
+
+
 def _ring_device(gpu: int, r: int) -> int:
     """GPU of sub-band r's input ring: the same (d + r) mod visible-devices
     rule paf_baseband2power applies to its contexts (paf_baseband2power.cu:
@@ -66,7 +100,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
         device_ring: bool = False, split: int = 1, bin_dir: str | None = None,
-        stage_args: list | None = None, stage_exe: str | None = None) -> list:
+        stage_args: list | None = None, stage_exe: str | None = None, pin: int | None = None) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
     sub-bands and gathers their spectra to its first GPU).
@@ -76,10 +110,12 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
     integration of a (single) chain by time over N GPUs (paf_baseband2power
     -t N, SURVEY.md 8e second mode).  stage_args: extra paf_baseband2power
     options (e.g. ["-G", "rccl", "-T", "30"]).  stage_exe: another build of
-    paf_baseband2power (e.g. a sanitizer build in tests/test_sanitizers.py)."""
+    paf_baseband2power (e.g. a sanitizer build in tests/test_sanitizers.py).
+    pin: first CPU of the stages' bindings (pin_cpus), None: unbound."""
+    _check_pin(pin, nsub, gather)
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
-                             timeout, hfname, device_ring, stage_args, stage_exe)
+                             timeout, hfname, device_ring, stage_args, stage_exe, pin)
     c = read_conf(conf_path)
     hdr = hfname or c["diskdb_hfname"]
     if not os.path.isabs(hdr):
@@ -119,12 +155,12 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
             if split > 1:
                 b2p_cmd += ["-t", str(split)]
             b2p_cmd += list(stage_args or [])
-            procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
-                                          stderr=subprocess.PIPE))
-            procs.append(subprocess.Popen(b2p_cmd, stderr=subprocess.PIPE))
-            procs.append(subprocess.Popen(
-                [_bin("paf_diskdb", bin_dir), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
-                 "-c", os.path.basename(dfile), "-d", hdr, "-e", str(c["diskdb_sod"])],
+            cpu_db, cpu_stage, cpu_sink = pin_cpus(pin, r)
+            procs.append(subprocess.Popen(_dbdisk(kout, out, cpu_sink), stderr=subprocess.PIPE))
+            procs.append(subprocess.Popen(_taskset(cpu_stage, b2p_cmd), stderr=subprocess.PIPE))
+            procs.append(subprocess.Popen(_taskset(cpu_db, [
+                _bin("paf_diskdb", bin_dir), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
+                "-c", os.path.basename(dfile), "-d", hdr, "-e", str(c["diskdb_sod"])]),
                 stderr=subprocess.PIPE))
         t_end = time.time() + timeout
         failed = None
@@ -180,7 +216,7 @@ def _wait_all(procs, timeout):
 
 
 def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, mean, timeout,
-                  hfname, device_ring=False, stage_args=None, stage_exe=None):
+                  hfname, device_ring=False, stage_args=None, stage_exe=None, pin=None):
     c = read_conf(conf_path)
     hdr = _resolve_header(c, conf_path, hfname)
     os.makedirs(directory, exist_ok=True)
@@ -199,8 +235,7 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
                              device=_ring_device(gpu, r) if device_ring else -1, page=not device_ring)
             keys.append(kin)
         out = os.path.join(directory, "power.dada")
-        procs.append(subprocess.Popen([_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"],
-                                      stderr=subprocess.PIPE))
+        procs.append(subprocess.Popen(_dbdisk(kout, out, pin_cpus(pin, 0, True)[2]), stderr=subprocess.PIPE))
         cmd = [stage_exe or _bin("paf_baseband2power"), "-a", f"{c['diskdb_key']:x}", "-b", f"{kout:x}",
                "-c", directory, "-d", str(gpu), "-p", str(npol_out), "-n", str(nsub)]
         if layout:
@@ -208,13 +243,13 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
         if mean:
             cmd.append("-m")
         cmd += list(stage_args or [])
-        procs.append(subprocess.Popen(cmd, stderr=subprocess.PIPE))
+        procs.append(subprocess.Popen(_taskset(pin_cpus(pin, 0, True)[1], cmd), stderr=subprocess.PIPE))
         for r in range(nsub):
             dfile = datafiles[r]
-            procs.append(subprocess.Popen(
-                [_bin("paf_diskdb"), "-a", f"{c['diskdb_key'] + 0x10 * r:x}",
-                 "-b", os.path.dirname(os.path.abspath(dfile)), "-c", os.path.basename(dfile),
-                 "-d", hdr, "-e", str(c["diskdb_sod"])], stderr=subprocess.PIPE))
+            procs.append(subprocess.Popen(_taskset(pin_cpus(pin, r, True)[0], [
+                _bin("paf_diskdb"), "-a", f"{c['diskdb_key'] + 0x10 * r:x}",
+                "-b", os.path.dirname(os.path.abspath(dfile)), "-c", os.path.basename(dfile),
+                "-d", hdr, "-e", str(c["diskdb_sod"])]), stderr=subprocess.PIPE))
         _wait_all(procs, timeout)
         return [out]
     finally:
@@ -243,12 +278,16 @@ def main(argv=None) -> int:
     ap.add_argument("--bin-dir", default=None,
                     help="where paf_diskdb / paf_baseband2power live (e.g. bin/psrdada: the "
                          "PSRDADA builds, INTEGRATION.md); paf_dbdisk stays the default one")
+    ap.add_argument("--pin", type=int, nargs="?", const=0, default=None, metavar="CPU",
+                    help="bind the stages to CPUs as the reference's launcher does: paf_diskdb on CPU "
+                         "(default 0), paf_baseband2power on CPU+1, paf_dbdisk on CPU+2; sub-band chain r "
+                         "shifted by 3r")
     a = ap.parse_args(argv)
     if a.bin_dir and a.device_ring:
         ap.error("--device-ring needs libpafdada's hosts (GPU-resident rings are an extension)")
     files = a.dfname if a.subbands > 1 or a.gather else a.dfname[0]
     outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean,
-               gather=a.gather, device_ring=a.device_ring, split=a.split, bin_dir=a.bin_dir)
+               gather=a.gather, device_ring=a.device_ring, split=a.split, bin_dir=a.bin_dir, pin=a.pin)
     print("\n".join(outs))
     return 0
 

@@ -538,3 +538,61 @@ def test_stage_input_ring_removed_under_it(stages, tmp_path, mode):
     for b in range(nblk):
         for r in range(onsub):
             assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=1).view(np.uint32)), (b, r)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_pipeline_pins_the_stages_like_the_reference(stages, tmp_path, gather):
+    """python -m paf_b2p.pipeline --pin: the stages bound to CPUs as the
+    reference's launcher binds them (taskset -c 0 paf_diskdb, taskset -c 1
+    paf_baseband2power, dada_dbdisk -b 2; paf-baseband2power.py:68,80,83,
+    86-95), chain r shifted by 3r; the stage (here the CPU double's build,
+    behind a wrapper that records its CPU list) runs on its CPU and every
+    spectrum equals the oracle's"""
+    from paf_b2p import pipeline
+    from test_gpu_pipeline import write_conf
+    nsub = 2
+    assert pipeline.pin_cpus(None, 0) == (None, None, None)
+    assert [pipeline.pin_cpus(0, r) for r in range(2)] == [(0, 1, 2), (3, 4, 5)]
+    assert [pipeline.pin_cpus(1, r, True) for r in range(3)] == [(1, 2, 3), (4, 2, 3), (5, 2, 3)]
+    with pytest.raises(ValueError, match="not available"):
+        pipeline.run("unused.conf", str(tmp_path), 0, "x.dada", pin=max(os.sched_getaffinity(0)) + 1)
+    if not set(range(3 * nsub)) <= os.sched_getaffinity(0):
+        pytest.skip("CPUs 0-5 are not all available to this process")
+    g = npo.Geom(nbit=8, nchan_chunk=64, nsamp_int=1 << 10)
+    nblk = 2
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 64\nTSAMP 0.84375\n")
+    files, payloads = [], []
+    for r in range(nsub):
+        p = co.fill_synthetic(g, g.block_bytes * nblk, 20181105, r, 0)
+        f = tmp_path / f"sb{r}.dada"
+        dada.write_dada_file(str(f), "x 1\n", p)
+        files.append(str(f))
+        payloads.append(p)
+    kin = _key()
+    _key()  # kin + 0x10: the second sub-band's ring
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 10, 1, 256, 64, kin, _key(), str(hfile))
+    wrap = tmp_path / "stage.sh"
+    wrap.write_text("#!/bin/bash\ngrep Cpus_allowed_list /proc/self/status > \"$B2P_AFF_DIR/$$\"\n"
+                    f"exec {stages['host']} \"$@\"\n")
+    wrap.chmod(0o755)
+    aff = tmp_path / "aff"
+    aff.mkdir()
+    env_keep = dict(os.environ)
+    os.environ["B2P_AFF_DIR"] = str(aff)
+    try:
+        outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, files, nsub=nsub,
+                            gather=gather, timeout=120, stage_exe=str(wrap), pin=0)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_keep)
+    seen = sorted(p.read_text().split()[-1] for p in aff.iterdir())
+    assert seen == (["1"] if gather else ["1", "4"]), seen
+    for r in range(nsub):
+        data = dada.read_dada_file(outs[0 if gather else r])[1]
+        sp = data.view(np.uint32).reshape(-1, nsub if gather else 1, g.nout)
+        assert sp.shape[0] == nblk
+        for i in range(nblk):
+            blk = payloads[r][i * g.block_bytes:(i + 1) * g.block_bytes]
+            assert np.array_equal(sp[i, r if gather else 0], co.power(g, blk).view(np.uint32)), (r, i)
