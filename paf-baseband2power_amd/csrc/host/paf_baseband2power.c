@@ -30,6 +30,7 @@
  * (libpafdada extensions) are then off, and blocks are pinned when first
  * seen.
  */
+#include <dlfcn.h>
 #include <errno.h>
 #include <getopt.h>
 #include <inttypes.h>
@@ -1158,6 +1159,14 @@ int main(int argc, char *argv[]) {
   b2p_info_t info;
   b2p_get_info(sub[0].ctx, &info);
   sh.nout = info.nout;
+  { /* the bounds-checked debug build of libpafb2p (LD_LIBRARY_PATH=lib/debug:
+     * the launcher's -e, in the role cuda-memcheck has in the reference,
+     * paf-baseband2power.py:89-90) exports b2p_debug_build */
+    int (*dbg)(void) = NULL;
+    *(void **)&dbg = dlsym(RTLD_DEFAULT, "b2p_debug_build");
+    if (dbg && dbg())
+      multilog(log, LOG_INFO, "libpafb2p: debug build, every span load and output slot bounds-checked");
+  }
   for (int r = 0; r < nmem && nmem > 1; r++) { /* which physical GPU each member drives */
     b2p_info_t mi;
     char bus[32] = "?";

@@ -11,7 +11,8 @@ parses (the reference's launcher is a SyntaxError at :90 and reads undefined
 args.psrname / args.dfname at :37-38), stops the other stages if one fails,
 and with -s N runs N independent sub-band chains, chain r on GPU r with ring
 keys KEY + 0x10*r (one GPU, one stream, one ring per sub-band).
-With --pin it binds the stages to CPUs as the reference does (`taskset -c`,
+-e 1 (the reference's cuda-memcheck run) puts the stage on the bounds-checked
+debug build of libpafb2p.  With --pin it binds the stages to CPUs as the reference does (`taskset -c`,
 `dada_dbdisk -b`: paf-baseband2power.py:68,80,83,86-95).
 """
 from __future__ import annotations
@@ -87,6 +88,23 @@ def _dbdisk(kout: int, out: str, cpu: int | None) -> list:
     return [_bin("paf_dbdisk"), "-k", f"{kout:x}", "-o", out, "-W"] + ([] if cpu is None else ["-b", str(cpu)])
 
 
+def stage_env(memcheck: int) -> dict | None:
+    """the stage's environment: with memcheck (the reference's -e, which runs
+    the stage under cuda-memcheck, paf-baseband2power.py:89-90) the stage
+    loads the bounds-checked debug build of libpafb2p (lib/debug: every span
+    load of the integrate kernel and every output slot checked, an
+    out-of-bounds access fails the run with its index) ahead of the release
+    one its RUNPATH names"""
+    if not memcheck:
+        return None
+    dbg = os.path.join(os.path.dirname(dada.BIN_DIR), "lib", "debug")
+    if not os.path.exists(os.path.join(dbg, "libpafb2p.so")):
+        raise FileNotFoundError(f"{dbg}/libpafb2p.so not built (make -C paf-baseband2power_amd)")
+    env = dict(os.environ)
+    env["LD_LIBRARY_PATH"] = dbg + (":" + env["LD_LIBRARY_PATH"] if env.get("LD_LIBRARY_PATH") else "")
+    return env
+
+
 def _ring_device(gpu: int, r: int) -> int:
     """GPU of sub-band r's input ring: the same (d + r) mod visible-devices
     rule paf_baseband2power applies to its contexts (paf_baseband2power.cu:
@@ -100,7 +118,8 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
         layout: str = "", npol_out: int = 1, mean: bool = False, timeout: float = 3600,
         hfname: str | None = None, outfiles: list | None = None, gather: bool = False,
         device_ring: bool = False, split: int = 1, bin_dir: str | None = None,
-        stage_args: list | None = None, stage_exe: str | None = None, pin: int | None = None) -> list:
+        stage_args: list | None = None, stage_exe: str | None = None, pin: int | None = None,
+        memcheck: int = 0) -> list:
     """Run the chains; returns the output file path of every sub-band (one
     combined file with gather=True: one paf_baseband2power process serves all
     sub-bands and gathers their spectra to its first GPU).
@@ -111,11 +130,13 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
     -t N, SURVEY.md 8e second mode).  stage_args: extra paf_baseband2power
     options (e.g. ["-G", "rccl", "-T", "30"]).  stage_exe: another build of
     paf_baseband2power (e.g. a sanitizer build in tests/test_sanitizers.py).
-    pin: first CPU of the stages' bindings (pin_cpus), None: unbound."""
+    pin: first CPU of the stages' bindings (pin_cpus), None: unbound.
+    memcheck: the stage on the bounds-checked debug library (stage_env)."""
     _check_pin(pin, nsub, gather)
+    senv = stage_env(memcheck)
     if gather:
         return _run_gathered(conf_path, directory, gpu, datafile, nsub, layout, npol_out, mean,
-                             timeout, hfname, device_ring, stage_args, stage_exe, pin)
+                             timeout, hfname, device_ring, stage_args, stage_exe, pin, senv)
     c = read_conf(conf_path)
     hdr = hfname or c["diskdb_hfname"]
     if not os.path.isabs(hdr):
@@ -157,7 +178,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
             b2p_cmd += list(stage_args or [])
             cpu_db, cpu_stage, cpu_sink = pin_cpus(pin, r)
             procs.append(subprocess.Popen(_dbdisk(kout, out, cpu_sink), stderr=subprocess.PIPE))
-            procs.append(subprocess.Popen(_taskset(cpu_stage, b2p_cmd), stderr=subprocess.PIPE))
+            procs.append(subprocess.Popen(_taskset(cpu_stage, b2p_cmd), stderr=subprocess.PIPE, env=senv))
             procs.append(subprocess.Popen(_taskset(cpu_db, [
                 _bin("paf_diskdb", bin_dir), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
                 "-c", os.path.basename(dfile), "-d", hdr, "-e", str(c["diskdb_sod"])]),
@@ -216,7 +237,7 @@ def _wait_all(procs, timeout):
 
 
 def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, mean, timeout,
-                  hfname, device_ring=False, stage_args=None, stage_exe=None, pin=None):
+                  hfname, device_ring=False, stage_args=None, stage_exe=None, pin=None, senv=None):
     c = read_conf(conf_path)
     hdr = _resolve_header(c, conf_path, hfname)
     os.makedirs(directory, exist_ok=True)
@@ -243,7 +264,7 @@ def _run_gathered(conf_path, directory, gpu, datafiles, nsub, layout, npol_out, 
         if mean:
             cmd.append("-m")
         cmd += list(stage_args or [])
-        procs.append(subprocess.Popen(_taskset(pin_cpus(pin, 0, True)[1], cmd), stderr=subprocess.PIPE))
+        procs.append(subprocess.Popen(_taskset(pin_cpus(pin, 0, True)[1], cmd), stderr=subprocess.PIPE, env=senv))
         for r in range(nsub):
             dfile = datafiles[r]
             procs.append(subprocess.Popen(_taskset(pin_cpus(pin, r, True)[0], [
@@ -263,7 +284,9 @@ def main(argv=None) -> int:
     ap.add_argument("-b", "--directory", required=True, help="output / log directory")
     ap.add_argument("-c", "--gpu", type=int, default=0, help="index of the first GPU")
     ap.add_argument("-d", "--visiblegpu", default="", help="accepted for compatibility")
-    ap.add_argument("-e", "--memcheck", type=int, default=0, help="accepted (no cuda-memcheck)")
+    ap.add_argument("-e", "--memcheck", type=int, default=0,
+                    help="1: the stage on the bounds-checked debug build of libpafb2p (lib/debug), "
+                         "where the reference runs it under cuda-memcheck")
     ap.add_argument("-f", "--dfname", required=True, nargs="+", help="DADA data file(s)")
     ap.add_argument("-s", "--subbands", type=int, default=1)
     ap.add_argument("-g", "--layout", default="")
@@ -287,7 +310,8 @@ def main(argv=None) -> int:
         ap.error("--device-ring needs libpafdada's hosts (GPU-resident rings are an extension)")
     files = a.dfname if a.subbands > 1 or a.gather else a.dfname[0]
     outs = run(a.cfname, a.directory, a.gpu, files, a.subbands, a.layout, a.npol_out, a.mean,
-               gather=a.gather, device_ring=a.device_ring, split=a.split, bin_dir=a.bin_dir, pin=a.pin)
+               gather=a.gather, device_ring=a.device_ring, split=a.split, bin_dir=a.bin_dir, pin=a.pin,
+               memcheck=a.memcheck)
     print("\n".join(outs))
     return 0
 

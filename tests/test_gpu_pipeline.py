@@ -48,8 +48,11 @@ def spectra(path, nout):
     return hdr.decode(), data.view(np.float32).reshape(-1, nout)
 
 
-@pytest.mark.parametrize("npol_out,mean", [(1, 0), (2, 1)])
-def test_bmf_pipeline(gpu, tmp_path, npol_out, mean):
+@pytest.mark.parametrize("npol_out,mean,memcheck", [(1, 0, 0), (2, 1, 0), (1, 0, 1)])
+def test_bmf_pipeline(gpu, tmp_path, npol_out, mean, memcheck):
+    """memcheck 1: the launcher's -e (the reference's cuda-memcheck run,
+    paf-baseband2power.py:89-90) -- the same spectra from the stage on the
+    bounds-checked debug build of libpafb2p, which its log names"""
     # BMF-native TFTFP int16 BE, 64 DFs per block (8192 samples per integration),
     # 3 whole integrations + a partial one that must be skipped
     g = npo.Geom(nbit=16, big_endian=1, nchunk=48, nsamp_df=128, nchan_chunk=7,
@@ -61,7 +64,7 @@ def test_bmf_pipeline(gpu, tmp_path, npol_out, mean):
     conf = tmp_path / "p.conf"
     write_conf(conf, 64, 48, 7168, 336, 0x6a10, 0x6b10, "header_baseband2power.txt")
     outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, str(src), npol_out=npol_out,
-                        mean=bool(mean), layout="bmf", timeout=600)
+                        mean=bool(mean), layout="bmf", timeout=600, memcheck=memcheck)
     hdr, sp = spectra(outs[0], g.nout)
     assert sp.shape == (nblk, g.nout)
     for i in range(nblk):
@@ -73,6 +76,7 @@ def test_bmf_pipeline(gpu, tmp_path, npol_out, mean):
     assert abs(dada.header_get(hdr, "TSAMP", "%lf") - 8192 * 27 / 32) < 1e-6
     log = open(os.path.join(str(tmp_path / "out"), "paf_baseband2power.log")).read()
     assert "partial integration skipped" in log and "FINISH PAF_PROCESS: 3 integrations" in log
+    assert ("libpafb2p: debug build" in log) == bool(memcheck)
 
 
 def test_int8_header_layout_two_subbands(gpu, tmp_path):

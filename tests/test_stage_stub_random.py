@@ -596,3 +596,30 @@ def test_pipeline_pins_the_stages_like_the_reference(stages, tmp_path, gather):
         for i in range(nblk):
             blk = payloads[r][i * g.block_bytes:(i + 1) * g.block_bytes]
             assert np.array_equal(sp[i, r if gather else 0], co.power(g, blk).view(np.uint32)), (r, i)
+
+
+def test_pipeline_memcheck_runs_the_stage_on_the_debug_library(stages, tmp_path):
+    """-e 1 (the reference runs the stage under cuda-memcheck,
+    paf-baseband2power.py:89-90): the stage's loader finds the bounds-checked
+    debug build of libpafb2p (lib/debug) ahead of the release one; the other
+    stages keep the default environment"""
+    from paf_b2p import pipeline
+    from test_gpu_pipeline import write_conf
+    assert pipeline.stage_env(0) is None
+    dbg = os.path.join(PKG, "lib", "debug")
+    assert pipeline.stage_env(1)["LD_LIBRARY_PATH"].split(":")[0] == dbg
+    g = npo.Geom(nbit=8, nchan_chunk=64, nsamp_int=1 << 10)
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 64\nTSAMP 0.84375\n")
+    p = co.fill_synthetic(g, g.block_bytes, 20181105, 0, 0)
+    f = tmp_path / "sb0.dada"
+    dada.write_dada_file(str(f), "x 1\n", p)
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 10, 1, 256, 64, _key(), _key(), str(hfile))
+    wrap = tmp_path / "stage.sh"
+    wrap.write_text(f"#!/bin/bash\necho \"$LD_LIBRARY_PATH\" > {tmp_path}/ldpath\nexec {stages['host']} \"$@\"\n")
+    wrap.chmod(0o755)
+    outs = pipeline.run(str(conf), str(tmp_path / "out"), 0, str(f), timeout=120, stage_exe=str(wrap), memcheck=1)
+    assert (tmp_path / "ldpath").read_text().split(":")[0].strip() == dbg
+    sp = dada.read_dada_file(outs[0])[1].view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == 1 and np.array_equal(sp[0], co.power(g, p).view(np.uint32))
