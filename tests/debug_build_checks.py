@@ -15,7 +15,6 @@ library.
 Prints "debug build checks: ok" / "staging under debug build: N examples ok";
 any failed check raises (exit 1).
 """
-import ctypes as C
 import os
 import sys
 

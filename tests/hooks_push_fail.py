@@ -6,7 +6,6 @@ staging chunk 2 of a 4-chunk host span through b2p_test_inject_push_fail.
 Kept out of the pytest process so that process only ever maps the release
 library.  Prints "push-fail hook: ok" on success; any failed check raises.
 """
-import ctypes as C
 import os
 import sys
 
