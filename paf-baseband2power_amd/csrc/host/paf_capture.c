@@ -59,6 +59,19 @@
 #include "b2p_dada.h"
 #include "b2p_df.h"
 
+/* the GPU holding ring db's blocks, -1 for a host ring */
+static int ring_device_of(ipcbuf_t *db) {
+#if defined(B2P_TEST_HOST_RING_AS_DEVICE)
+  /* test build only (tests/test_frames_stub.py): a host ring takes the
+   * GPU-resident path, driven by the CPU test double tests/c/b2p_cpu_stub.c,
+   * so this host runs under ThreadSanitizer on a machine with no GPU */
+  (void)db;
+  return 0;
+#else
+  return ipcbuf_get_device(db);
+#endif
+}
+
 #define MAXPORT 16
 #define RECV_BATCH 64
 #define TBUF_NDF 256 /* capture.h:35 */
@@ -143,7 +156,10 @@ static int write_header(cap_t *c, const b2p_df_hdr_t *start) {
     multilog(c->log, LOG_ERR, "cannot set UTC_START / PICOSECONDS / FREQ in the header");
     return -1;
   }
-  if (ipcbuf_mark_filled(c->hdu->header_block, DADA_DEFAULT_HEADER_SIZE) < 0) return -1;
+  if (ipcbuf_mark_filled(c->hdu->header_block, DADA_DEFAULT_HEADER_SIZE) < 0) {
+    multilog(c->log, LOG_ERR, "cannot mark the header block filled");
+    return -1;
+  }
   c->hdr_done = 1;
   return 0;
 }
@@ -236,11 +252,16 @@ static void stop_rx(rxq_t *q, int n) {
 static int flush_batch(cap_t *c) {
   if (!c->hn) return 0;
   if (b2p_memcpy(c->ctx, c->d_frames, c->hf, c->hn * B2P_DF_BYTES, 1) != B2P_OK ||
-      b2p_memcpy(c->ctx, c->d_chunks, c->hc, c->hn, 1) != B2P_OK)
+      b2p_memcpy(c->ctx, c->d_chunks, c->hc, c->hn, 1) != B2P_OK) {
+    multilog(c->log, LOG_ERR, "block %" PRIu64 ": uploading %" PRIu64 " frames: %s", c->nblk_done, c->hn,
+             b2p_last_error(c->ctx));
     return -1;
+  }
   const int rc = b2p_assemble(c->ctx, c->d_frames, c->hn, B2P_DF_BYTES, c->d_chunks, c->ref.idf,
                               c->ref.sec, c->blk, c->block_ndf, (uint32_t)c->nchunk, c->d_cnt);
   c->hn = 0;
+  if (rc != B2P_OK)
+    multilog(c->log, LOG_ERR, "block %" PRIu64 ": assemble: %s", c->nblk_done, b2p_last_error(c->ctx));
   return rc == B2P_OK ? 0 : -1;
 }
 
@@ -264,9 +285,18 @@ static int file_frame(cap_t *c, const unsigned char *df, unsigned char chunk, in
 static int open_block(cap_t *c) {
   uint64_t bid;
   c->blk = ipcio_open_block_write(c->hdu->data_block, &bid);
-  if (!c->blk) return -1;
-  if (!c->nozero && b2p_memset(c->ctx, c->blk, 0, c->bufsz) != B2P_OK) return -1;
-  if (b2p_memset(c->ctx, c->d_cnt, 0, (c->nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) return -1;
+  if (!c->blk) {
+    multilog(c->log, LOG_ERR, "block %" PRIu64 ": no block to write in the ring", c->nblk_done);
+    return -1;
+  }
+  /* a failure from here on leaves the open block unfilled: the end of the
+   * transfer (dada_hdu_unlock_write) marks it as the 0-byte end-of-data
+   * block, so no reader integrates a half-assembled block */
+  if ((!c->nozero && b2p_memset(c->ctx, c->blk, 0, c->bufsz) != B2P_OK) ||
+      b2p_memset(c->ctx, c->d_cnt, 0, (c->nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) {
+    multilog(c->log, LOG_ERR, "block %" PRIu64 ": clearing: %s", c->nblk_done, b2p_last_error(c->ctx));
+    return -1;
+  }
   /* the spill, sorted again against this block's reference */
   const uint64_t n = c->sn;
   c->sn = 0;
@@ -291,8 +321,10 @@ static int close_block(cap_t *c) {
   if (flush_batch(c) < 0) return -1;
   unsigned long long cnt[256 + 3];
   if (b2p_sync(c->ctx) != B2P_OK ||
-      b2p_memcpy(c->ctx, cnt, c->d_cnt, (c->nchunk + 3) * sizeof(unsigned long long), 2) != B2P_OK)
+      b2p_memcpy(c->ctx, cnt, c->d_cnt, (c->nchunk + 3) * sizeof(unsigned long long), 2) != B2P_OK) {
+    multilog(c->log, LOG_ERR, "block %" PRIu64 ": assembly: %s", c->nblk_done, b2p_last_error(c->ctx));
     return -1;
+  }
   uint64_t placed = 0;
   for (int i = 0; i < c->nchunk; i++) placed += cnt[i];
   const uint64_t expect = c->block_ndf * (uint64_t)c->nchunk;
@@ -446,7 +478,10 @@ int main(int argc, char **argv) {
   if (record) {
     fo = fopen(ofile, "wb");
     fco = fopen(ocfile, "wb");
-    if (!fo || !fco) goto done;
+    if (!fo || !fco) {
+      multilog(c.log, LOG_ERR, "cannot open %s / %s (%s)", ofile, ocfile, strerror(errno));
+      goto done;
+    }
   } else {
     c.hdu = dada_hdu_create(c.log);
     dada_hdu_set_key(c.hdu, key);
@@ -466,7 +501,7 @@ int main(int argc, char **argv) {
       multilog(c.log, LOG_ERR, "Can not write data before start (capture.c:626)");
       goto done;
     }
-    if (ipcbuf_get_device(db) < 0) {
+    if (ring_device_of(db) < 0) {
       multilog(c.log, LOG_ERR, "ring %x is not GPU-resident (dada_db -g)", (unsigned)key);
       goto done;
     }
@@ -486,15 +521,17 @@ int main(int argc, char **argv) {
     b2p_geom_bmf(&g);
     g.nchunk = (uint32_t)c.nchunk;
     g.nsamp_int = rbuf_ndf * g.nsamp_df;
-    if (b2p_open(&c.ctx, &g, ipcbuf_get_device(db)) != B2P_OK) {
+    if (b2p_open(&c.ctx, &g, ring_device_of(db)) != B2P_OK) {
       multilog(c.log, LOG_ERR, "b2p_open: %s", b2p_last_error(NULL));
       goto done;
     }
     if (b2p_dev_alloc(c.ctx, &c.d_frames, rbuf_ndf * c.nchunk * B2P_DF_BYTES) != B2P_OK ||
-        b2p_dev_alloc(c.ctx, &c.d_chunks, rbuf_ndf * c.nchunk) != B2P_OK)
+        b2p_dev_alloc(c.ctx, &c.d_chunks, rbuf_ndf * c.nchunk) != B2P_OK ||
+        b2p_dev_alloc(c.ctx, (void **)&c.d_cnt, (c.nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) {
+      multilog(c.log, LOG_ERR, "device batch of %" PRIu64 " frames: %s", rbuf_ndf * c.nchunk,
+               b2p_last_error(c.ctx));
       goto done;
-    if (b2p_dev_alloc(c.ctx, (void **)&c.d_cnt, (c.nchunk + 3) * sizeof(unsigned long long)) != B2P_OK)
-      goto done;
+    }
   }
   /* host batch: one block's worth of frames at most (GPU mode), pinned */
   c.cap_frames = record ? 4096 : rbuf_ndf * (uint64_t)c.nchunk;
@@ -504,7 +541,10 @@ int main(int argc, char **argv) {
   c.spill_cap = record ? 0 : (uint64_t)(2 * TBUF_NDF) * (uint64_t)c.nchunk;
   c.sf = c.spill_cap ? malloc(c.spill_cap * B2P_DF_BYTES) : NULL;
   c.sc = c.spill_cap ? malloc(c.spill_cap) : NULL;
-  if (!c.hf || !c.hc || (c.spill_cap && (!c.sf || !c.sc))) goto done;
+  if (!c.hf || !c.hc || (c.spill_cap && (!c.sf || !c.sc))) {
+    multilog(c.log, LOG_ERR, "cannot allocate the host batch (%" PRIu64 " frames) and spill", c.cap_frames);
+    goto done;
+  }
   if (c.ctx) b2p_register_host(c.ctx, c.hf, c.cap_frames * B2P_DF_BYTES);
   if (have_ref) { /* the first block opens with the first frame, after the header */
     c.ref.idf = ref_idf;
@@ -519,7 +559,10 @@ int main(int argc, char **argv) {
     int nrx = nrx_req > 0 ? nrx_req : nport, rx_failed = 0, rx_ok = 0;
     if (nrx > nport) nrx = nport;
     rxq_t *rxq = calloc((size_t)nrx, sizeof *rxq);
-    if (!rxq) goto done;
+    if (!rxq) {
+      multilog(c.log, LOG_ERR, "cannot allocate %d receive queues", nrx);
+      goto done;
+    }
     int rx_started = 0;
     for (int t = 0; t < nrx; t++) {
       rxq[t].stop = &rx_stop;
@@ -528,8 +571,14 @@ int main(int argc, char **argv) {
         rxq[t].sock[rxq[t].nport++] = socks[p];
       }
       for (int k = 0; k < RX_SLOTS && rxq[t].nport; k++)
-        if (!(rxq[t].slot[k].buf = malloc((size_t)RECV_BATCH * B2P_DF_BYTES))) goto rx_end;
-      if (pthread_create(&rxq[t].th, NULL, rx_main, &rxq[t]) != 0) goto rx_end;
+        if (!(rxq[t].slot[k].buf = malloc((size_t)RECV_BATCH * B2P_DF_BYTES))) {
+          multilog(c.log, LOG_ERR, "receive thread %d: cannot allocate its batch slots", t);
+          goto rx_end;
+        }
+      if (pthread_create(&rxq[t].th, NULL, rx_main, &rxq[t]) != 0) {
+        multilog(c.log, LOG_ERR, "cannot start receive thread %d", t);
+        goto rx_end;
+      }
       rxq[t].started = 1;
       rx_started++;
     }
@@ -570,7 +619,10 @@ int main(int argc, char **argv) {
             ps->frames++;
             ps->chunks[ck >> 6] |= 1ull << (ck & 63);
             if (record) {
-              if (fwrite(df, B2P_DF_BYTES, 1, fo) != 1 || fwrite(&ck, 1, 1, fco) != 1) goto rx_fail;
+              if (fwrite(df, B2P_DF_BYTES, 1, fo) != 1 || fwrite(&ck, 1, 1, fco) != 1) {
+                multilog(c.log, LOG_ERR, "writing %s / %s failed (%s)", ofile, ocfile, strerror(errno));
+                goto rx_fail;
+              }
               continue;
             }
             if (t_first == 0) t_first = now_s();
@@ -697,8 +749,9 @@ done:
     c.efile = NULL;
     write_header(&c, &c.ref);
   }
-  if (locked) dada_hdu_unlock_write(c.hdu);
-  if (c.hdu) dada_hdu_destroy(c.hdu);
+  /* the context first: closing it drains its stream, so no clear or
+   * assembly a failure left in flight still writes into a ring block once
+   * the ring is detached (its IPC mapping closed) */
   if (c.ctx) {
     if (c.d_frames) b2p_dev_free(c.ctx, c.d_frames);
     if (c.d_chunks) b2p_dev_free(c.ctx, c.d_chunks);
@@ -706,6 +759,8 @@ done:
     if (c.hf) b2p_unregister_host(c.ctx, c.hf);
     b2p_close(c.ctx);
   }
+  if (locked) dada_hdu_unlock_write(c.hdu);
+  if (c.hdu) dada_hdu_destroy(c.hdu);
   for (int p = 0; p < nport; p++)
     if (socks[p] >= 0) close(socks[p]);
   if (fo) fclose(fo);

@@ -50,6 +50,19 @@
 #include "b2p_dada.h"
 #include "b2p_df.h"
 
+/* the GPU holding ring db's blocks, -1 for a host ring */
+static int ring_device_of(ipcbuf_t *db) {
+#if defined(B2P_TEST_HOST_RING_AS_DEVICE)
+  /* test build only (tests/test_frames_stub.py): a host ring takes the
+   * GPU-resident path, driven by the CPU test double tests/c/b2p_cpu_stub.c,
+   * so this host runs under ThreadSanitizer on a machine with no GPU */
+  (void)db;
+  return 0;
+#else
+  return ipcbuf_get_device(db);
+#endif
+}
+
 #define HDR_SIZE DADA_DEFAULT_HEADER_SIZE
 
 static double now_s(void) {
@@ -110,8 +123,10 @@ static int load_batch(b2p_ctx_t *ctx, FILE *fd, FILE *fc, batch_t *b, uint64_t c
     if (k > b->hi) b->hi = k;
   }
   if (b2p_memcpy(ctx, b->frames, hf, got * B2P_DF_BYTES, 1) != B2P_OK ||
-      b2p_memcpy(ctx, b->chunks, hc, got, 1) != B2P_OK)
+      b2p_memcpy(ctx, b->chunks, hc, got, 1) != B2P_OK) {
+    fprintf(stderr, "paf_dfdb: uploading %zu frames: %s\n", got, b2p_last_error(ctx));
     return -1;
+  }
   return 0;
 }
 
@@ -175,12 +190,12 @@ int main(int argc, char **argv) {
   locked = 1;
   ipcbuf_t *db = &hdu->data_block->buf;
   const uint64_t bufsz = ipcbuf_get_bufsz(db), nbufs = ipcbuf_get_nbufs(db);
-  const int ondev = ipcbuf_get_device(db) >= 0;
+  const int ondev = ring_device_of(db) >= 0;
   if (!ondev && !replay) {
     multilog(log, LOG_ERR, "ring %x is not GPU-resident (create it with dada_db -g)", (unsigned)key);
     goto done;
   }
-  if (ondev) device = ipcbuf_get_device(db);
+  if (ondev) device = ring_device_of(db);
 
   b2p_geom_t g;
   if (replay) {
@@ -214,11 +229,17 @@ int main(int argc, char **argv) {
   const double t0 = now_s();
   uint64_t nblk = 0;
   if (replay) {
-    if (!ondev && b2p_dev_alloc(ctx, &stage, bufsz) != B2P_OK) goto done;
+    if (!ondev && b2p_dev_alloc(ctx, &stage, bufsz) != B2P_OK) {
+      multilog(log, LOG_ERR, "staging block of %" PRIu64 " B: %s", bufsz, b2p_last_error(ctx));
+      goto done;
+    }
     for (uint64_t i = 0; i < replay; i++) {
       uint64_t bid;
       char *blk = ipcio_open_block_write(hdu->data_block, &bid);
-      if (!blk) goto done;
+      if (!blk) {
+        multilog(log, LOG_ERR, "no block to write in ring %x", (unsigned)key);
+        goto done;
+      }
       if (i < nbufs) { /* first pass: synthetic block i, then re-used as is */
         if (b2p_fill_synthetic(ctx, ondev ? (void *)blk : stage, bufsz, seed, subband, i, 0) != B2P_OK ||
             b2p_sync(ctx) != B2P_OK || (!ondev && b2p_memcpy(ctx, blk, stage, bufsz, 2) != B2P_OK)) {
@@ -238,14 +259,21 @@ int main(int argc, char **argv) {
     }
     hf = malloc(cap * B2P_DF_BYTES);
     hc = malloc(cap);
-    if (!hf || !hc) goto done;
+    if (!hf || !hc) {
+      multilog(log, LOG_ERR, "cannot allocate %" PRIu64 " frames of host staging", cap);
+      goto done;
+    }
     b2p_register_host(ctx, hf, cap * B2P_DF_BYTES); /* pinned: full PCIe rate */
     for (int k = 0; k < NSLOT; k++)
       if (b2p_dev_alloc(ctx, &bt[k].frames, cap * B2P_DF_BYTES) != B2P_OK ||
-          b2p_dev_alloc(ctx, &bt[k].chunks, cap) != B2P_OK)
+          b2p_dev_alloc(ctx, &bt[k].chunks, cap) != B2P_OK) {
+        multilog(log, LOG_ERR, "device batch %d: %s", k, b2p_last_error(ctx));
         goto done;
-    if (b2p_dev_alloc(ctx, (void **)&d_cnt, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK)
+      }
+    if (b2p_dev_alloc(ctx, (void **)&d_cnt, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) {
+      multilog(log, LOG_ERR, "device counters: %s", b2p_last_error(ctx));
       goto done;
+    }
     const b2p_df_hdr_t ref0 = {1, ref_idf, ref_sec, 0, 0, 0.0};
     b2p_df_hdr_t ref = ref0;
     /* live batches: slots head, head+1, ... (mod NSLOT), oldest first */
@@ -267,8 +295,10 @@ int main(int argc, char **argv) {
         }
         batch_t *x = &bt[(head + live) % NSLOT];
         if (load_batch(ctx, fd, fc, x, cap, hf, hc, &ref0, block_ndf, b > seen_hi - 1 ? b : seen_hi - 1,
-                       seen_hi + 2) < 0)
+                       seen_hi + 2) < 0) {
+          multilog(log, LOG_ERR, "reading the frame stream failed before block %" PRId64, b);
           goto done;
+        }
         if (!x->n) {
           eof = 1;
           break;
@@ -282,9 +312,18 @@ int main(int argc, char **argv) {
       if (!any) break; /* no frame of block b or later is left */
       uint64_t bid;
       char *blk = ipcio_open_block_write(hdu->data_block, &bid);
-      if (!blk) goto done;
-      if (!nozero && b2p_memset(ctx, blk, 0, bufsz) != B2P_OK) goto done;
-      if (b2p_memset(ctx, d_cnt, 0, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) goto done;
+      if (!blk) {
+        multilog(log, LOG_ERR, "no block to write in ring %x", (unsigned)key);
+        goto done;
+      }
+      /* a failure from here on leaves the open block unfilled: the end of
+       * the transfer (dada_hdu_unlock_write) marks it as the 0-byte
+       * end-of-data block, so no reader integrates a half-assembled block */
+      if ((!nozero && b2p_memset(ctx, blk, 0, bufsz) != B2P_OK) ||
+          b2p_memset(ctx, d_cnt, 0, (nchunk + 3) * sizeof(unsigned long long)) != B2P_OK) {
+        multilog(log, LOG_ERR, "block %" PRId64 ": clearing: %s", b, b2p_last_error(ctx));
+        goto done;
+      }
       for (int j = 0; j < live; j++) {
         batch_t *x = &bt[(head + j) % NSLOT];
         if (x->hi < b || x->lo > b) continue;
@@ -296,8 +335,10 @@ int main(int argc, char **argv) {
       }
       unsigned long long cnt[256 + 3];
       if (b2p_sync(ctx) != B2P_OK ||
-          b2p_memcpy(ctx, cnt, d_cnt, (nchunk + 3) * sizeof(unsigned long long), 2) != B2P_OK)
+          b2p_memcpy(ctx, cnt, d_cnt, (nchunk + 3) * sizeof(unsigned long long), 2) != B2P_OK) {
+        multilog(log, LOG_ERR, "block %" PRId64 ": assembly: %s", b, b2p_last_error(ctx));
         goto done;
+      }
       uint64_t placed = 0;
       for (int c = 0; c < nchunk; c++) placed += cnt[c];
       placed_all += placed;
@@ -324,8 +365,9 @@ int main(int argc, char **argv) {
   status = EXIT_SUCCESS;
 
 done:
-  if (locked) dada_hdu_unlock_write(hdu); /* ends the transfer (EOD) */
-  dada_hdu_destroy(hdu);
+  /* the context first: closing it drains its stream, so no clear or
+   * assembly a failure left in flight still writes into a ring block once
+   * the ring is detached (its IPC mapping closed) */
   if (ctx) {
     for (int k = 0; k < NSLOT; k++) {
       if (bt[k].frames) b2p_dev_free(ctx, bt[k].frames);
@@ -336,6 +378,8 @@ done:
     if (hf) b2p_unregister_host(ctx, hf);
     b2p_close(ctx);
   }
+  if (locked) dada_hdu_unlock_write(hdu); /* ends the transfer (EOD) */
+  dada_hdu_destroy(hdu);
   free(hf);
   free(hc);
   if (fd) fclose(fd);

@@ -12,7 +12,12 @@
  * Semantics kept: exact uint64 sums per output, one RNE rounding to fp32
  * (mean: (double)sum / nsamp_int), npol_out 1 or 2, partial-integration and
  * ragged-push codes, member-major gathers, summed time-split partials.
- * Layouts: int8 and little-endian int16 only (B2P_EINVAL otherwise).
+ * Layouts: int8, little-endian int16 and BMF's big-endian int16 (each 8-B
+ * word BSWAP_64-decoded, cudautil.cuh:118-125: X in bytes 4-7, Y in 0-3).
+ * For paf_dfdb and paf_capture (tests/test_frames_stub.py) also
+ * b2p_memset and b2p_assemble, on the context's queue like the rest: a frame
+ * is placed where capture.c:540 puts it, its index from libpafdada's
+ * b2p_df_index (capture.c:562-568), with the library's counts. 
  *
  * The stream model.  Every context owns a queue standing for its HIP stream
  * and every group one for its own gather streams (b2p_group_gather_async).
@@ -51,8 +56,9 @@
 #include <time.h>
 
 #include "b2p.h"
+#include "b2p_df.h"
 
-enum { OP_SUM, OP_SUMN, OP_FIN, OP_CONV, OP_COPY, OP_WAIT, OP_REDUCE, OP_FREE };
+enum { OP_SUM, OP_SUMN, OP_FIN, OP_CONV, OP_COPY, OP_WAIT, OP_REDUCE, OP_FREE, OP_SET, OP_ASM };
 
 typedef struct queue queue_t;
 
@@ -75,6 +81,11 @@ typedef struct op {
   uint64_t wait_seq;
   uint64_t *const *parts;          /* REDUCE inputs (count each) */
   int nparts;
+  int value;                       /* SET: the byte */
+  const uint8_t *chunks;           /* ASM: chunk of each frame (src[0]: the frames, nbytes: their count) */
+  uint64_t ref_idf, ref_sec, block_ndf;
+  uint32_t nchunk;
+  unsigned long long *counts;      /* ASM: nchunk + 3, accumulated */
 } op_t;
 
 struct queue {
@@ -141,18 +152,27 @@ uint64_t b2p_frame_bytes(const b2p_geom_t *g) {
   return (uint64_t)g->nchunk * g->nsamp_df * g->nchan_chunk * word_bytes(g);
 }
 
+/* component k of pol p's (re, im) pair at element i (one component per int) */
+static int64_t comp(const b2p_geom_t *g, const void *buf, uint64_t i) {
+  if (g->nbit == 8) return ((const int8_t *)buf)[i];
+  if (!g->big_endian) return ((const int16_t *)buf)[i];
+  /* BSWAP_64 of the word holding element i: lane k of the swapped word is
+   * the big-endian int16 at bytes 6-2k, 7-2k of the raw word */
+  const uint8_t *w = (const uint8_t *)buf + (i / 4) * 8;
+  const unsigned k = (unsigned)(i % 4);
+  return (int16_t)(uint16_t)((w[6 - 2 * k] << 8) | w[7 - 2 * k]);
+}
+
 /* [frame][chunk][samp][chan][pol][re,im] -> acc[chan*npol_out + pol?] */
 static void sum_span(const b2p_geom_t *g, const void *buf, uint64_t nbytes, uint64_t *acc) {
   const uint64_t frames = nbytes / b2p_frame_bytes(g);
-  const int8_t *b8 = buf;
-  const int16_t *b16 = buf;
   uint64_t i = 0;
   for (uint64_t f = 0; f < frames; f++)
     for (uint32_t c = 0; c < g->nchunk; c++)
       for (uint32_t s = 0; s < g->nsamp_df; s++)
         for (uint32_t ch = 0; ch < g->nchan_chunk; ch++)
           for (uint32_t p = 0; p < 2; p++, i += 2) {
-            const int64_t re = g->nbit == 8 ? b8[i] : b16[i], im = g->nbit == 8 ? b8[i + 1] : b16[i + 1];
+            const int64_t re = comp(g, buf, i), im = comp(g, buf, i + 1);
             const uint64_t o = ((uint64_t)c * g->nchan_chunk + ch) * g->npol_out + (g->npol_out == 2 ? p : 0);
             acc[o] += (uint64_t)(re * re + im * im);
           }
@@ -190,6 +210,31 @@ static void run_op(op_t *o) {
       }
       break;
     case OP_FREE: break;
+    case OP_SET: memset(o->dst, o->value, o->nbytes); break;
+    case OP_ASM: {
+      b2p_df_hdr_t ref = {0};
+      ref.idf = o->ref_idf;
+      ref.sec = o->ref_sec;
+      for (uint64_t d = 0; d < o->nbytes; d++) {
+        const uint8_t *df = (const uint8_t *)o->src[0] + d * B2P_DF_BYTES;
+        b2p_df_hdr_t h;
+        b2p_df_decode(df, &h);
+        const int64_t idf = b2p_df_index(&h, &ref);
+        const uint32_t ch = o->chunks[d];
+        if (ch >= o->nchunk) {
+          o->counts[o->nchunk + 2]++;
+        } else if (idf < 0) {
+          o->counts[o->nchunk]++;
+        } else if ((uint64_t)idf >= o->block_ndf) {
+          o->counts[o->nchunk + 1]++;
+        } else {
+          memcpy((uint8_t *)o->dst + ((uint64_t)idf * o->nchunk + ch) * B2P_DF_PAYLOAD_BYTES,
+                 df + B2P_DF_HDR_BYTES, B2P_DF_PAYLOAD_BYTES);
+          o->counts[ch]++;
+        }
+      }
+      break;
+    }
   }
   free(o->owned);
 }
@@ -334,7 +379,8 @@ int b2p_geom_bmf(b2p_geom_t *g) {
 }
 
 int b2p_geom_check(const b2p_geom_t *g) {
-  if (!g || (g->nbit != 8 && g->nbit != 16) || g->big_endian || g->npol != 2 || g->ndim != 2 ||
+  if (!g || (g->nbit != 8 && g->nbit != 16) || g->big_endian > 1 || (g->big_endian && g->nbit != 16) ||
+      g->npol != 2 || g->ndim != 2 ||
       (g->npol_out != 1 && g->npol_out != 2) || !g->nchunk || !g->nsamp_df || !g->nchan_chunk ||
       !g->nsamp_int || g->nsamp_int % g->nsamp_df || g->reserved)
     return B2P_EINVAL;
@@ -438,6 +484,46 @@ int b2p_memcpy(b2p_ctx_t *c, void *dst, const void *src, size_t bytes, int kind)
   if (!c || !dst || !src || kind < 1 || kind > 3) return B2P_EINVAL;
   queue_wait(&c->q, queue_pos(&c->q)); /* the library syncs the stream, then copies */
   memcpy(dst, src, bytes);
+  return B2P_OK;
+}
+
+int b2p_memset(b2p_ctx_t *c, void *dev, int value, size_t bytes) {
+  INJECT("b2p_memset");
+  if (!c || (!dev && bytes)) return B2P_EINVAL;
+  op_t *o = new_op(OP_SET);
+  o->dst = dev;
+  o->value = value;
+  o->nbytes = bytes;
+  enqueue(&c->q, o);
+  return B2P_OK;
+}
+
+/* not modelled: the synthetic generator (paf_dfdb -R, bench.py) runs on the
+ * GPU only (tests/test_gpu_device_ring.py) */
+int b2p_fill_synthetic(b2p_ctx_t *c, void *dev, size_t nbytes, uint64_t seed, uint32_t subband, uint64_t block,
+                       uint64_t elem0) {
+  (void)c, (void)dev, (void)nbytes, (void)seed, (void)subband, (void)block, (void)elem0;
+  return B2P_EINVAL;
+}
+
+int b2p_assemble(b2p_ctx_t *c, const void *dfs, uint64_t ndf, uint32_t df_bytes, const uint8_t *chunk_of_df,
+                 uint64_t ref_idf, uint64_t ref_sec, void *block, uint64_t block_ndf, uint32_t nchunk,
+                 unsigned long long *counts) {
+  INJECT("b2p_assemble");
+  if (!c || (ndf && (!dfs || !chunk_of_df)) || !block || !counts || df_bytes != B2P_DF_BYTES || !nchunk ||
+      nchunk > 255)
+    return B2P_EINVAL;
+  op_t *o = new_op(OP_ASM);
+  o->src[0] = dfs; /* read when the assembly runs, as the kernel reads device memory */
+  o->nbytes = ndf;
+  o->chunks = chunk_of_df;
+  o->ref_idf = ref_idf;
+  o->ref_sec = ref_sec;
+  o->dst = block;
+  o->block_ndf = block_ndf;
+  o->nchunk = nchunk;
+  o->counts = counts;
+  enqueue(&c->q, o);
   return B2P_OK;
 }
 

@@ -1,0 +1,223 @@
+"""CPU tests of the frame-assembly hosts on their GPU path (no GPU):
+`paf_dfdb` (a recorded frame stream into a ring) and `paf_capture` (UDP
+frames into a ring: receive threads, the sorting thread, block switching),
+built with ThreadSanitizer against the CPU test double of libpafb2p
+(tests/c/b2p_cpu_stub.c: b2p_memset and b2p_assemble on the context's queue,
+work completing up to B2P_STUB_DELAY_US late) and libpafdada's sources, with
+-DB2P_TEST_HOST_RING_AS_DEVICE so a host ring takes the GPU-resident path.
+Downstream, the stage built the same way integrates the ring's blocks (the
+double sums BMF's big-endian words as the library does) and `paf_dbdisk`
+writes the spectra; every spectrum must equal the C oracle's of the block
+the oracle assembles from the same frames (capture.c:540, 562-568).
+
+The failure sweep fails each b2p_* call these hosts make, at its first and
+second call (B2P_STUB_FAIL): the host exits 1 with an ERR line on stderr,
+the ring's transfer ends (the block being assembled becomes the 0-byte
+end-of-data block, never a half-assembled block), and the stage downstream
+exits 0 with correct spectra of the blocks delivered before -- or the call
+was never reached and every spectrum comes out.  tests/test_gpu_device_ring.py
+and tests/test_gpu_capture.py run the same hosts on the HIP library."""
+import os
+import re
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+import b2p_oracle as npo
+import oracle_c as co
+from conftest import REPO
+from paf_b2p import dada
+
+BIN = dada.BIN_DIR
+PKG = os.path.join(REPO, "paf-baseband2power_amd")
+HOST = os.path.join(PKG, "csrc", "host")
+STUB = os.path.join(REPO, "tests", "c", "b2p_cpu_stub.c")
+DADA_SRC = [os.path.join(PKG, "csrc", "dada", f)
+            for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c", "df_header.c")]
+_KEY = [0x4c00 + (os.getpid() % 64) * 0x40]
+NCHUNK, BLOCK_NDF, NBLK = 4, 32, 3
+REF_IDF, REF_SEC = 249990, 54  # the stream crosses a 27-s period
+TSAN_ENV = {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"}
+
+
+def _key():
+    _KEY[0] += 4
+    return _KEY[0]
+
+
+@pytest.fixture(scope="module")
+def exes(tmp_path_factory):
+    d = tmp_path_factory.mktemp("frames_stub")
+    out = {}
+    for name in ("paf_dfdb", "paf_capture", "paf_baseband2power"):
+        exe = d / name
+        subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
+                        "-fsanitize=thread", "-fno-omit-frame-pointer", "-I", os.path.join(REPO, "include"),
+                        "-DB2P_TEST_HOST_RING_AS_DEVICE", os.path.join(HOST, name + ".c"), STUB, *DADA_SRC,
+                        "-o", str(exe), "-pthread", "-ldl", "-lm"], check=True)
+        out[name] = str(exe)
+    return out
+
+
+def _stream(tmp_path, lost=0, seed=3):
+    """a BMF frame stream of NBLK blocks (paf_dfgen: frames shuffled within a
+    window, `lost` frames left out), its frames and chunk indices, and the
+    blocks the oracle assembles from it"""
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=NCHUNK, nsamp_df=128, nchan_chunk=7,
+                 nsamp_int=BLOCK_NDF * 128)
+    payload = co.fill_synthetic(g, g.block_bytes * NBLK, 20181105, 4, seed)
+    src = tmp_path / "in.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
+    subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(NCHUNK),
+                    "-c", str(ck), "-x", str(REF_IDF), "-s", str(REF_SEC), "-f", "1300", "-r", str(seed),
+                    "-w", str(BLOCK_NDF * NCHUNK * 3 // 2), "-l", str(lost)], check=True, capture_output=True)
+    dfs = np.fromfile(df, np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, np.uint8)
+    blocks, idf, sec = [], REF_IDF, REF_SEC
+    for b in range(NBLK):
+        want = np.zeros(g.block_bytes, np.uint8)  # lost frames read as zeros
+        co.assemble(dfs, chunk, idf, sec, want, BLOCK_NDF, NCHUNK)
+        if not lost:
+            assert np.array_equal(want, payload[b * g.block_bytes:(b + 1) * g.block_bytes])
+        blocks.append(want)
+        gi = idf + BLOCK_NDF
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27
+    return g, df, ck, blocks
+
+
+def _header(tmp_path, g):
+    h = tmp_path / "hdr.txt"
+    h.write_text(f"HDR_SIZE 4096\nNBIT 16\nNDIM 2\nNPOL 2\nNCHAN {NCHUNK * 7}\nNCHUNK {NCHUNK}\n"
+                 "NCHAN_CHUNK 7\nNSAMP_DF 128\nBYTE_ORDER BE\nTSAMP 0.84375\n")
+    return str(h)
+
+
+def _chain(tmp_path, exes, g, producer, env, start_producer=None, stage_env=None, timeout=120):
+    """producer -> host ring (as a device ring) -> the stage -> paf_dbdisk;
+    returns (spectra, exit codes and stderr of [dbdisk, stage, producer]).
+    stage_env: the stage's own environment (default: the producer's)"""
+    kin, kout = _key(), _key()
+    for k in (kin, kout):
+        dada.destroy_ring(k)
+    dada.create_ring(kin, 3, g.block_bytes)
+    dada.create_ring(kout, 8, g.nout * 4)
+    out = tmp_path / "power.dada"
+    procs = []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out), "-W"],
+                                  stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([exes["paf_baseband2power"], "-a", f"{kin:x}", "-b", f"{kout:x}", "-c",
+                                   str(tmp_path), "-d", "0", "-f", "header"],
+                                  stderr=subprocess.PIPE, text=True, env=stage_env or env),
+                 subprocess.Popen([a.replace("KEY", f"{kin:x}") for a in producer],
+                                  stderr=subprocess.PIPE, text=True, env=env)]
+        if start_producer:
+            start_producer()
+        errs = [None] * 3
+        for i in (2, 1, 0):
+            errs[i] = procs[i].communicate(timeout=timeout)[1]
+        rcs = [p.returncode for p in procs]
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for k in (kin, kout):
+            dada.destroy_ring(k)
+    for e in errs[1:]:
+        assert "WARNING: ThreadSanitizer" not in e, e[-3000:]
+    return data.view(np.uint32).reshape(-1, g.nout), rcs, errs
+
+
+def _check(g, sp, blocks):
+    for b in range(sp.shape[0]):
+        assert np.array_equal(sp[b], co.power(g, blocks[b]).view(np.uint32)), b
+
+
+@pytest.mark.parametrize("lost,delay", [(0, 0), (40, 500)])
+def test_dfdb_gpu_path_on_the_cpu_double(exes, tmp_path, lost, delay):
+    g, df, ck, blocks = _stream(tmp_path, lost)
+    env = dict(os.environ, B2P_STUB_DELAY_US=str(delay), **TSAN_ENV)
+    sp, rcs, errs = _chain(tmp_path, exes, g,
+                           [exes["paf_dfdb"], "-a", "KEY", "-b", _header(tmp_path, g), "-c", str(df), "-k", str(ck),
+                            "-n", str(NCHUNK), "-x", str(REF_IDF), "-s", str(REF_SEC)], env)
+    assert rcs == [0, 0, 0], errs
+    assert sp.shape[0] == NBLK, errs[2]
+    _check(g, sp, blocks)
+    placed = [int(x) for x in re.findall(r"block \d+: (\d+) of", errs[2])]
+    nframes = os.path.getsize(df) // npo.DF_BYTES  # the frames paf_dfgen kept (-l drops some)
+    assert sum(placed) == nframes and (nframes < NBLK * BLOCK_NDF * NCHUNK) == bool(lost), errs[2]
+
+
+def _capture_cmd(exes, hdr, port):
+    return [exes["paf_capture"], "-a", "KEY", "-f", hdr, "-c", str(BLOCK_NDF), "-n", str(NBLK), "-P", str(port),
+            "-N", "3", "-m", "freq:1300", "-x", str(REF_IDF), "-s", str(REF_SEC), "-t", "1", "-b", "1", "-d", "0"]
+
+
+def _sender(df, ck, port, delay_s=1.5):
+    def go():
+        time.sleep(delay_s)  # the capture binds its ports and opens its context first
+        snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-P", str(port),
+                              "-N", "3", "-r", "50"], capture_output=True, text=True)
+        assert snd.returncode == 0, snd.stderr
+    return go
+
+
+@pytest.mark.parametrize("delay", [0, 500])
+def test_capture_gpu_path_on_the_cpu_double(exes, tmp_path, delay):
+    """three receive threads, the sorting thread and the assembly on the
+    double's queue, under ThreadSanitizer; frames over loopback UDP"""
+    g, df, ck, blocks = _stream(tmp_path, seed=11)
+    env = dict(os.environ, B2P_STUB_DELAY_US=str(delay), **TSAN_ENV)
+    port = 26000 + (os.getpid() % 400) * 16 + delay // 100
+    sp, rcs, errs = _chain(tmp_path, exes, g, _capture_cmd(exes, _header(tmp_path, g), port), env,
+                           start_producer=_sender(df, ck, port))
+    assert rcs == [0, 0, 0], errs
+    assert sp.shape[0] == NBLK, errs[2]
+    _check(g, sp, blocks)
+    assert "0.000% lost" in errs[2] and "3 receive thread(s) over 3 port(s)" in errs[2], errs[2]
+
+
+# the b2p_* calls each host makes on its GPU path (b2p_open is refused before
+# any ring block: covered by its ERR line too)
+CALLS = {"paf_dfdb": ["b2p_open", "b2p_memcpy", "b2p_memset", "b2p_assemble", "b2p_sync"],
+         "paf_capture": ["b2p_open", "b2p_memcpy", "b2p_memset", "b2p_assemble", "b2p_sync"]}
+
+
+@pytest.mark.parametrize("host", ["paf_dfdb", "paf_capture"])
+def test_frame_hosts_never_fail_silently(exes, tmp_path, host):
+    g, df, ck, blocks = _stream(tmp_path, seed=5)
+    hdr = _header(tmp_path, g)
+    failed_runs = 0
+    for i, call in enumerate(CALLS[host]):
+        for nth in (1, 2):
+            run_dir = tmp_path / f"{call}_{nth}"
+            run_dir.mkdir()
+            env = dict(os.environ, B2P_STUB_FAIL=f"{call}:{nth}", B2P_STUB_DELAY_US="200", **TSAN_ENV)
+            if host == "paf_dfdb":
+                cmd = [exes["paf_dfdb"], "-a", "KEY", "-b", hdr, "-c", str(df), "-k", str(ck), "-n", str(NCHUNK),
+                       "-x", str(REF_IDF), "-s", str(REF_SEC)]
+                start = None
+            else:
+                port = 27000 + (os.getpid() % 400) * 16 + i * 2 + nth
+                cmd, start = _capture_cmd(exes, hdr, port), _sender(df, ck, port)
+            # the stage downstream runs without injected failures
+            stage_env = dict(env)
+            stage_env.pop("B2P_STUB_FAIL")
+            sp, rcs, errs = _chain(run_dir, exes, g, cmd, env, start, stage_env)
+            injected = "injected failure of" in errs[2]
+            if rcs[2] == 0:
+                assert not injected, (call, nth, errs[2])
+                assert sp.shape[0] == NBLK, (call, nth)
+            else:
+                failed_runs += 1
+                assert rcs[2] == 1 and injected, (call, nth, rcs, errs[2])
+                assert "] ERR: " in errs[2], (call, nth, errs[2])
+            assert rcs[:2] == [0, 0], (call, nth, rcs, errs[1][-800:])  # the stage and sink end cleanly
+            _check(g, sp, blocks)  # every block delivered is whole and correct
+    assert failed_runs >= len(CALLS[host]), failed_runs
+

@@ -59,7 +59,7 @@ def test_ring_surface_under_sanitizer(tmp_path, san, key):
 STAGE = os.path.join(REPO, "paf-baseband2power_amd", "csrc", "host", "paf_baseband2power.c")
 STUB = os.path.join(REPO, "tests", "c", "b2p_cpu_stub.c")
 DADA_SRC = [os.path.join(REPO, "paf-baseband2power_amd", "csrc", "dada", f)
-            for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c")]
+            for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c", "df_header.c")]
 
 
 def _stage_tsan(tmp_path, as_device: bool) -> str:

@@ -39,7 +39,7 @@ PKG = os.path.join(REPO, "paf-baseband2power_amd")
 STAGE = os.path.join(PKG, "csrc", "host", "paf_baseband2power.c")
 STUB = os.path.join(REPO, "tests", "c", "b2p_cpu_stub.c")
 DADA_SRC = [os.path.join(PKG, "csrc", "dada", f) for f in ("dada_ring.c", "dada_query.c", "dada_device.c",
-                                                            "ascii_header.c")]
+                                                            "ascii_header.c", "df_header.c")]
 _SCALE = int(os.environ.get("B2P_HYPOTHESIS_SCALE", "1"))
 _SEED = os.environ.get("B2P_HYPOTHESIS_SEED")
 _KEY = [0x5a00 + (os.getpid() % 64) * 0x80]
