@@ -46,16 +46,22 @@ _KEY = [0x5a00 + (os.getpid() % 64) * 0x80]
 # B2P_STAGE_TSAN=1: the stage built with ThreadSanitizer (halt on the first
 # report), so the random cases also hunt data races in its threads
 _TSAN = ["-fsanitize=thread", "-fno-omit-frame-pointer"] if os.environ.get("B2P_STAGE_TSAN") else []
+_ASAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"]
+ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=0:exitcode=86", "UBSAN_OPTIONS": "print_stacktrace=1:exitcode=87"}
 
 
 @pytest.fixture(scope="module")
 def stages(tmp_path_factory):
     d = tmp_path_factory.mktemp("stub_stage")
     out = {}
-    for name, defs in (("host", []), ("dev", ["-DB2P_TEST_HOST_RING_AS_DEVICE"])):
+    # "_asan": AddressSanitizer + UBSan builds, for the failure sweep: a
+    # failure path that frees or detaches memory the double's queue (standing
+    # for a HIP stream) still writes into is a heap-use-after-free there
+    for name, defs, san in (("host", [], _TSAN), ("dev", ["-DB2P_TEST_HOST_RING_AS_DEVICE"], _TSAN),
+                            ("host_asan", [], _ASAN), ("dev_asan", ["-DB2P_TEST_HOST_RING_AS_DEVICE"], _ASAN)):
         exe = d / f"stage_{name}"
         subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
-                        *_TSAN, "-I", os.path.join(REPO, "include"), *defs, STAGE, STUB, *DADA_SRC, "-o",
+                        *san, "-I", os.path.join(REPO, "include"), *defs, STAGE, STUB, *DADA_SRC, "-o",
                         str(exe), "-pthread", "-ldl", "-lm"], check=True)
         out[name] = str(exe)
     return out
@@ -397,13 +403,17 @@ _CALLS = ["b2p_push", "b2p_integrate", "b2p_integrate_n", "b2p_finish_async", "b
           "b2p_group_reduce", "b2p_group_sync"]
 
 
+@pytest.mark.parametrize("san", ["", "_asan"])
 @pytest.mark.parametrize("mode", ["single", "single_dev", "gathered", "gathered_dev", "split"])
-def test_stage_never_fails_silently(stages, tmp_path, mode):
+def test_stage_never_fails_silently(stages, tmp_path, mode, san):
     """every entry point the stage calls, failed at its 1st and its 2nd call
     (B2P_STUB_FAIL), in every threading mode: the stage either never made
     that call (exit 0, every spectrum) or exits 1 within seconds with an ERR
     line on stderr naming what failed, the output transfer ended, and only
-    correct spectra written -- no silent exit, no hang"""
+    correct spectra written -- no silent exit, no hang.  _asan: the stage
+    built with AddressSanitizer and UBSan, so memory a failure path releases
+    while queued work still uses it is reported (exit 1 without the ERR
+    line the assertion wants, and the report in the message)"""
     g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=128)
     nmem = 1 if mode.startswith("single") else 2
     nblk = 4
@@ -427,12 +437,13 @@ def test_stage_never_fails_silently(stages, tmp_path, mode):
             dada.create_ring(kout, nblk + 2, onsub * g.nout * 4)
             d = tmp_path / f"{call}_{nth}"
             d.mkdir()
-            env = dict(os.environ, B2P_STUB_FAIL=f"{call}:{nth}", B2P_STUB_DELAY_US="200")
+            env = dict(os.environ, B2P_STUB_FAIL=f"{call}:{nth}", B2P_STUB_DELAY_US="200", **ASAN_ENV)
             procs = []
             try:
                 procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o",
                                            str(d / "p.dada")], stderr=subprocess.PIPE),
-                         subprocess.Popen([stages["dev" if mode.endswith("_dev") else "host"], "-a", f"{base:x}",
+                         subprocess.Popen([stages[("dev" if mode.endswith("_dev") else "host") + san], "-a",
+                                           f"{base:x}",
                                            "-b", f"{kout:x}", "-c", str(d), "-d", "0"] + args,
                                           stderr=subprocess.PIPE, text=True, env=env)]
                 for k, bl in zip(keys, blocks):
@@ -452,6 +463,7 @@ def test_stage_never_fails_silently(stages, tmp_path, mode):
                         p.wait()
                 for k in keys + [kout]:
                     dada.destroy_ring(k)
+            assert "Sanitizer" not in err and "runtime error" not in err, (call, nth, err[-4000:])
             injected = "injected failure of" in err
             sp = data.view(np.uint32).reshape(-1, onsub, g.nout)
             if rc == 0:
