@@ -298,6 +298,7 @@ static int do_diskdb(conf_t *conf) {
     clock_gettime(CLOCK_MONOTONIC, &a);
     char *curbuf = ipcio_open_block_write(conf->hdu->data_block, &block_id);
     if (!curbuf) {
+      multilog(conf->log, LOG_ERR, "no block to write in ring %x (block %" PRIu64 ")", (unsigned)conf->key, nblk);
       free(stage);
       return EXIT_FAILURE;
     }
@@ -318,6 +319,7 @@ static int do_diskdb(conf_t *conf) {
 #ifndef B2P_PSRDADA
     if (stage && ipcbuf_copy_in(db, curbuf, stage, n) < 0) {
       multilog(conf->log, LOG_ERR, "copy into device block failed: %s", dada_device_error());
+      ipcio_close_block_write(conf->hdu->data_block, 0); /* the 0-byte end of data, not a half-copied block */
       free(stage);
       return EXIT_FAILURE;
     }

@@ -13,7 +13,9 @@
  *                          as the runtime refused first allocations (DESIGN.md
  *                          7b).  The holder's call 0 is its primer's.
  * FAKE_HIP_LOG=path        append "free <ptr>" per hipFree, "export <n>" per
- *                          export try, so a test sees when the holder frees. */
+ *                          export try, so a test sees when the holder frees.
+ * FAKE_HIP_MEMCPY_FAIL=n   the n-th hipMemcpy of the process (1-based) fails,
+ *                          as a copy into a block would on a HIP error. */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -74,7 +76,10 @@ int hipIpcOpenMemHandle(void **p, fake_ipc_handle_t h, unsigned flags) {
 }
 int hipIpcCloseMemHandle(void *p) { return p == g_mapped ? 0 : 1; }
 int hipMemcpy(void *d, const void *s, size_t n, int kind) {
+  static int calls;
   (void)d, (void)s, (void)n, (void)kind;
+  const char *e = getenv("FAKE_HIP_MEMCPY_FAIL");
+  if (e && ++calls == atoi(e)) return 2; /* hipErrorOutOfMemory-like: any failure */
   return 0; /* imported blocks are not backed here */
 }
 int hipDeviceSynchronize(void) { return 0; }

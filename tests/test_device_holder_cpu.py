@@ -20,6 +20,7 @@ import subprocess
 import sys
 import time
 
+import numpy as np
 import pytest
 
 from conftest import REPO
@@ -187,4 +188,36 @@ def test_holder_without_primer_diagnostic(fake_env):
         assert info["export_retries"] == 1 and info["primer_refused"] == 0, (info, r.stderr)
         assert "on block 0" in r.stderr, r.stderr
     finally:
+        assert _destroy(fake_env, key).returncode == 0
+
+
+@pytest.mark.parametrize("fail_at", [1, 2])
+def test_diskdb_failed_copy_ends_the_transfer(fake_env, tmp_path, fail_at):
+    """paf_diskdb into a GPU-resident ring whose copy into block `fail_at`
+    fails (a HIP error): it exits 1 with an ERR line naming the copy, and
+    ends the transfer with the 0-byte end-of-data block where that block
+    was -- the reader gets the blocks copied before and a clean end, never a
+    half-copied block"""
+    key = _key()
+    kf = tmp_path / "in.dada"
+    dada.write_dada_file(str(kf), "x 1\n", np.arange(3 * 8192, dtype=np.uint32).view(np.uint8)[:3 * 8192])
+    hdr = tmp_path / "hdr.txt"
+    hdr.write_text("HDR_SIZE 4096\nNBIT 8\n")
+    assert _create(fake_env, key).returncode == 0
+    out = tmp_path / "out.dada"
+    try:
+        sink = subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{key:x}", "-o", str(out)],
+                                stderr=subprocess.PIPE, text=True, env=fake_env)
+        src = subprocess.run([os.path.join(BIN, "paf_diskdb"), "-a", f"{key:x}", "-b", str(tmp_path), "-c",
+                              "in.dada", "-d", str(hdr), "-e", "1"], capture_output=True, text=True, timeout=60,
+                             env=dict(fake_env, FAKE_HIP_MEMCPY_FAIL=str(fail_at)))
+        _, serr = sink.communicate(timeout=60)
+        assert src.returncode == 1 and "ERR: copy into device block failed" in src.stderr, src.stderr
+        assert sink.returncode == 0, serr
+        assert f"in {fail_at - 1} blocks" in serr, serr  # the blocks before the failed copy, then the end
+        assert os.path.getsize(out) == 4096 + (fail_at - 1) * 8192
+    finally:
+        if sink.poll() is None:
+            sink.kill()
+            sink.wait()
         assert _destroy(fake_env, key).returncode == 0
