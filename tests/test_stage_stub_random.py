@@ -3,7 +3,7 @@
 libpafb2p (tests/c/b2p_cpu_stub.c: exact sums; every call finished on
 return, or a stream model whose work completes up to 2 ms late, drawn per
 example) and libpafdada's sources, between PSRDADA writers in this process
-and `paf_dbdisk`.  Random layouts (int8 / int16 LE, what the stub handles),
+and `paf_dbdisk`.  Random layouts (int8, int16 LE and BMF's int16 BE),
 ring depths, block counts, short last blocks, output pols, sum or mean, and
 every threading mode of the stage:
 
@@ -87,7 +87,8 @@ def cases(draw):
     nframes = draw(st.integers(1, 48))
     if mode == "split":
         nframes = max(nmem, nframes - nframes % nmem)
-    g = npo.Geom(nbit=nbit, nchunk=nchunk, nsamp_df=nsamp_df, nchan_chunk=ncc,
+    g = npo.Geom(nbit=nbit, big_endian=int(nbit == 16 and draw(st.booleans())), nchunk=nchunk,
+                 nsamp_df=nsamp_df, nchan_chunk=ncc,
                  npol_out=draw(st.sampled_from([1, 2])), nsamp_int=nframes * nsamp_df,
                  mean=int(draw(st.booleans())))
     nblk = draw(st.integers(1, 10))
@@ -119,7 +120,8 @@ def test_stage_orchestration_random(stages, tmp_path_factory, case):
     # a longer transfer's writer must not wait on a stage that has left
     nbufs = case["nbufs"] if len(set(nblks)) == 1 else max(case["nbufs"], max(nblks) + 1)
     hdr = (f"HDR_SIZE 4096\nNBIT {g.nbit}\nNDIM 2\nNPOL 2\nNCHAN {g.nchunk * g.nchan_chunk}\n"
-           f"NCHUNK {g.nchunk}\nNCHAN_CHUNK {g.nchan_chunk}\nNSAMP_DF {g.nsamp_df}\nBYTE_ORDER LE\n"
+           f"NCHUNK {g.nchunk}\nNCHAN_CHUNK {g.nchan_chunk}\nNSAMP_DF {g.nsamp_df}\n"
+           f"BYTE_ORDER {'BE' if g.big_endian else 'LE'}\n"
            "TSAMP 0.84375\n")
     for k in keys + [kout]:
         dada.destroy_ring(k)
