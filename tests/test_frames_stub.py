@@ -24,6 +24,8 @@ import time
 
 import numpy as np
 import pytest
+from hypothesis import HealthCheck, assume, given, seed, settings
+from hypothesis import strategies as st
 
 import b2p_oracle as npo
 import oracle_c as co
@@ -231,3 +233,69 @@ def test_frame_hosts_never_fail_silently(exes, tmp_path, host, san):
             _check(g, sp, blocks)  # every block delivered is whole and correct
     assert failed_runs >= len(CALLS[host]), failed_runs
 
+
+
+_SCALE = int(os.environ.get("B2P_HYPOTHESIS_SCALE", "1"))
+_SEED = os.environ.get("B2P_HYPOTHESIS_SEED")
+
+
+@(seed(int(_SEED)) if _SEED else (lambda f: f))
+@settings(max_examples=4 * _SCALE, deadline=None, derandomize=_SEED is None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large,
+                                 HealthCheck.function_scoped_fixture])
+@given(st.sampled_from(["paf_dfdb", "paf_capture"]), st.integers(1, 12), st.integers(1, 48), st.integers(1, 5),
+       st.floats(0.0, 0.3), st.floats(0.05, 1.5), st.sampled_from([1000, 249_990]), st.integers(0, 2 ** 31),
+       st.sampled_from([0, 300, 1500]))
+def test_frame_hosts_random_streams(exes, tmp_path_factory, host, nchunk, block_ndf, nblk, loss, shuffle, ref_idf,
+                                    s, delay):
+    """the random streams tests/test_gpu_stage_random.py sends through the
+    HIP library (chunk counts, block lengths, 0-30 % of frames lost at the
+    source, arrival shuffled within up to 1.5 blocks), here through either
+    host's GPU path on the double under ThreadSanitizer, its queue completing
+    work up to `delay` us late: every spectrum equals the oracle's of its
+    block as the oracle places the stream.  A capture run whose loopback
+    dropped a frame says nothing about the capture and is discarded."""
+    tmp = tmp_path_factory.mktemp("rand")
+    g = npo.Geom(nbit=16, big_endian=1, nchunk=nchunk, nsamp_df=128, nchan_chunk=7, nsamp_int=block_ndf * 128)
+    per_block = block_ndf * nchunk
+    window = max(1, min(int(shuffle * per_block), 200 * nchunk))
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, s, 4, 2)
+    src = tmp / "in.dada"
+    dada.write_dada_file(str(src), "NBIT 16\n", payload)
+    df, ck = tmp / "s.df", tmp / "s.chunks"
+    ref_sec = 27 * 54
+    subprocess.run([os.path.join(BIN, "paf_dfgen"), "-i", str(src), "-o", str(df), "-n", str(nchunk),
+                    "-c", str(ck), "-x", str(ref_idf), "-s", str(ref_sec), "-f", "1300", "-r", str(s % 997),
+                    "-w", str(window), "-l", str(int(loss * 1000))], check=True, capture_output=True)
+    dfs = np.fromfile(df, dtype=np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, dtype=np.uint8)
+    assume(len(dfs) > 0)  # every frame lost at the source: nothing to place
+    h = npo.df_decode(dfs)
+    rel = np.trunc(h["idf"].astype(np.float64) + (h["sec"].astype(np.float64) - ref_sec) / 1.08e-4 - ref_idf)
+    last = int(rel.max()) // block_ndf + 1  # blocks up to the last frame's
+    hdr = tmp / "hdr.txt"
+    hdr.write_text(f"HDR_SIZE 4096\nNBIT 16\nNDIM 2\nNPOL 2\nNCHAN {nchunk * 7}\nNCHUNK {nchunk}\n"
+                   "NCHAN_CHUNK 7\nNSAMP_DF 128\nBYTE_ORDER BE\nTSAMP 0.84375\n")
+    env = dict(os.environ, B2P_STUB_DELAY_US=str(delay), **TSAN_ENV)
+    if host == "paf_dfdb":
+        cmd, start, n_out = ([exes["paf_dfdb"], "-a", "KEY", "-b", str(hdr), "-c", str(df), "-k", str(ck), "-n",
+                              str(nchunk), "-x", str(ref_idf), "-s", str(ref_sec)], None, last)
+    else:
+        port = 28000 + (os.getpid() % 400) * 16 + s % 13
+        cmd = [exes["paf_capture"], "-a", "KEY", "-f", str(hdr), "-c", str(block_ndf), "-n", str(nblk), "-P",
+               str(port), "-N", "3", "-m", "freq:1300", "-x", str(ref_idf), "-s", str(ref_sec), "-t", "1", "-d", "0"]
+        start, n_out = _sender(df, ck, port), min(nblk, last)  # the capture ends with the stream
+    sp, rcs, errs = _chain(tmp, exes, g, cmd, env, start)
+    assert rcs == [0, 0, 0], [e[-800:] for e in errs]
+    if host == "paf_capture":
+        m = re.search(r"capture: (\d+) frames received", errs[2])
+        assert m, errs[2][-800:]
+        assume(int(m.group(1)) == len(dfs))  # the loopback delivered every frame sent
+    assert sp.shape[0] == n_out, errs[2][-800:]
+    idf, sec = ref_idf, ref_sec
+    for b in range(n_out):
+        want = np.zeros(g.block_bytes, np.uint8)
+        co.assemble(dfs, chunk, idf, sec, want, block_ndf, nchunk)
+        assert np.array_equal(sp[b], co.power(g, want).view(np.uint32)), (host, b, errs[2][-600:])
+        gi = idf + block_ndf
+        idf, sec = gi % 250000, sec + (gi // 250000) * 27
