@@ -17,9 +17,13 @@
  * switches, the spill is sorted again against the new reference.
  *
  *   paf_capture -a key -f header_file [-g epoch_file] [-i freq] [-c rbuf_ndf]
- *               [-j seconds | -n blocks] [-I ip] [-P 17100] [-N 6]
+ *               [-j seconds | -n blocks] [-e nic | -I ip] [-P 17100] [-N 6]
  *               [-m ip | -m freq:F0] [-x ref_idf -s ref_sec] [-t idle_s] [-k dir] [-Z]
  *   paf_capture -o frames.df -O chunks.u8 ...      (no GPU: record what arrives)
+ *
+ * Address: -e NIC binds 10.17.<node>.<NIC>, <node> the 8th character of
+ * the host name, as the reference derives it (paf_capture.c:88-90,115-118;
+ * HN_LEN 8, paf_capture.h:5); -I gives the address directly (default any).
  *
  * Chunk of a frame: -m ip (default) derives it from the sender address as
  * acquire_ifreq does (capture.c:570-584); -m freq:F0 uses round(freq - F0)
@@ -84,6 +88,19 @@ static volatile sig_atomic_t g_stop;
 static void on_stop(int sig) {
   (void)sig;
   g_stop = 1;
+}
+
+/* the reference's NIC address: 10.17.<node>.<nic>, node = the host name's
+ * character HN_LEN - 1 (paf_capture.c:115-118; HN_LEN 8, paf_capture.h:5) */
+static int nic_address(int nic, char *ip, size_t len) {
+  char hn[256] = "";
+  if (gethostname(hn, sizeof hn - 1) < 0 || strlen(hn) < 8 || hn[7] < '0' || hn[7] > '9') {
+    fprintf(stderr, "paf_capture: -e %d: host name '%s' has no node digit at its 8th character "
+                    "(the reference's 10.17.<node>.<nic> rule); give the address with -I\n", nic, hn);
+    return -1;
+  }
+  snprintf(ip, len, "10.17.%d.%d", hn[7] - '0', nic);
+  return 0;
 }
 
 static double now_s(void) {
@@ -347,7 +364,9 @@ int main(int argc, char **argv) {
   uint64_t rbuf_ndf = 8192, nblocks = 0, ref_idf = 0, ref_sec = 0;
   int have_ref = 0, have_freq = 0, nrx_req = 0, sod = -1;
   double length = 0, idle_s = 2.0, freq = 0;
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:g:i:j:k:I:P:N:R:m:x:s:n:t:o:O:Zh")) != -1) {
+  int nic = -1;
+  char nic_ip[32] = "";
+  while ((arg = getopt(argc, argv, "a:b:c:d:e:f:g:i:j:k:I:P:N:R:m:x:s:n:t:o:O:Zh")) != -1) {
     switch (arg) {
       case 'a': have_key = sscanf(optarg, "%x", (unsigned *)&key) == 1; break;
       case 'b': /* start of data (paf_capture.c:75-77, capture.c:622-639) */
@@ -366,6 +385,12 @@ int main(int argc, char **argv) {
         break;
       }
       case 'c': rbuf_ndf = strtoull(optarg, NULL, 10); break;
+      case 'e': /* which NIC (paf_capture.c:88-90) */
+        if (sscanf(optarg, "%d", &nic) != 1 || nic < 0 || nic > 255) {
+          fprintf(stderr, "paf_capture: -e takes a NIC number 0..255, not %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        break;
       case 'f': hfile = optarg; break;
       case 'g': efile = optarg; break;
       case 'i':
@@ -392,11 +417,15 @@ int main(int argc, char **argv) {
       default:
         fprintf(stdout,
                 "paf_capture -a key -f header [-g epoch_file] [-i freq] [-b sod] [-d 0] [-c rbuf_ndf] [-j seconds | -n blocks]\n"
-                "            [-I ip] [-P port0] [-N nports] [-R rx_threads] [-m ip|freq:F0] [-x ref_idf -s ref_sec]\n"
+                "            [-e nic | -I ip] [-P port0] [-N nports] [-R rx_threads] [-m ip|freq:F0] [-x ref_idf -s ref_sec]\n"
                 "            [-t idle_s] [-k dir] [-Z]\n"
                 "paf_capture -o frames.df -O chunks.u8 [-I ip] [-P port0] [-N nports] [-m ...] [-t idle_s]\n");
         return EXIT_FAILURE;
     }
+  }
+  if (nic >= 0 && !strcmp(ip, "0.0.0.0")) { /* -I wins over -e */
+    if (nic_address(nic, nic_ip, sizeof nic_ip) < 0) return EXIT_FAILURE;
+    ip = nic_ip;
   }
   const int record = ofile != NULL;
   if ((!record && (!have_key || !hfile)) || (record && !ocfile) || nport < 1 || nport > MAXPORT ||

@@ -140,3 +140,38 @@ def test_capture_refuses_unsupported_record_flags(tmp_path, args, msg):
     r = subprocess.run([os.path.join(BIN, "paf_capture"), "-a", "7e00", "-f", str(hdr)] + args,
                        capture_output=True, text=True, timeout=30)
     assert r.returncode == 1 and msg in r.stderr
+
+
+def test_capture_nic_option_like_the_reference(tmp_path):
+    """-e NIC (paf_capture.c:88-90): the reference binds 10.17.<node>.<NIC>,
+    <node> the 8th character of the host name (:115-118, HN_LEN 8); -I gives
+    the address instead and wins over -e"""
+    import socket
+    hn = socket.gethostname()
+    port = 24500 + (os.getpid() % 500) * 4
+    out, outc = tmp_path / "r.df", tmp_path / "r.chunks"
+    cmd = [os.path.join(BIN, "paf_capture"), "-o", str(out), "-O", str(outc), "-P", str(port), "-N", "1",
+           "-m", "freq:1300", "-t", "0.5"]
+    cap = subprocess.Popen(cmd + ["-e", "3"], stderr=subprocess.PIPE, text=True)
+    try:
+        _, err = cap.communicate(timeout=10)
+    except subprocess.TimeoutExpired:  # the address exists here: bound, waiting for frames
+        cap.kill()
+        _, err = cap.communicate()
+        assert len(hn) >= 8 and hn[7].isdigit(), err
+        return
+    assert cap.returncode == 1
+    if len(hn) >= 8 and hn[7].isdigit():
+        assert f"cannot bind 10.17.{hn[7]}.3:{port}" in err, err
+    else:
+        assert "has no node digit at its 8th character" in err, err
+    # -I wins: the loopback address, one frame stream recorded whole
+    g, _, df, ck = make_stream(tmp_path, nchunk=2, nblk=1)
+    cap = subprocess.Popen(cmd + ["-e", "3", "-I", "127.0.0.1"], stderr=subprocess.PIPE, text=True)
+    time.sleep(0.5)
+    snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-H", "127.0.0.1",
+                          "-P", str(port), "-N", "1", "-r", "100"], capture_output=True, text=True)
+    assert snd.returncode == 0, snd.stderr
+    _, err = cap.communicate(timeout=60)
+    assert cap.returncode == 0, err
+    assert os.path.getsize(out) == os.path.getsize(df), err
