@@ -26,7 +26,10 @@ int main(int argc, char **argv) {
   while ((arg = getopt(argc, argv, "k:b:n:r:dlpH:g:h")) != -1) {
     switch (arg) {
       case 'k':
-        if (sscanf(optarg, "%x", (unsigned *)&key) != 1) return EXIT_FAILURE;
+        if (sscanf(optarg, "%x", (unsigned *)&key) != 1) {
+          fprintf(stderr, "dada_db: could not parse key from %s\n", optarg);
+          return EXIT_FAILURE;
+        }
         break;
       case 'b': bufsz = strtoull(optarg, NULL, 10); break;
       case 'n': nbufs = strtoull(optarg, NULL, 10); break;

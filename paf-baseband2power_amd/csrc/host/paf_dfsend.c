@@ -159,7 +159,10 @@ int main(int argc, char **argv) {
     w[t].chunk = chunk;
     w[t].n = n;
     w[t].dst = dst;
-    if (pthread_create(&w[t].th, NULL, send_main, &w[t]) != 0) return EXIT_FAILURE;
+    if (pthread_create(&w[t].th, NULL, send_main, &w[t]) != 0) {
+      fprintf(stderr, "paf_dfsend: cannot start sender thread %d\n", t);
+      return EXIT_FAILURE;
+    }
   }
   for (int t = 0; t < nthr; t++) {
     pthread_join(w[t].th, NULL);
