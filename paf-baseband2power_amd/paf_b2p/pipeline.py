@@ -73,6 +73,9 @@ def pin_cpus(pin: int | None, r: int, gather: bool = False) -> tuple:
 def _check_pin(pin: int | None, nsub: int, gather: bool) -> None:
     if pin is None:
         return
+    import shutil
+    if not shutil.which("taskset"):
+        raise FileNotFoundError("--pin binds the stages with taskset (util-linux), which is not on PATH")
     want = {c for r in range(nsub) for c in pin_cpus(pin, r, gather)}
     bad = sorted(want - os.sched_getaffinity(0))
     if pin < 0 or bad:
