@@ -104,6 +104,7 @@ def _header(tmp_path, g):
 def _chain(tmp_path, exes, g, producer, env, start_producer=None, stage_env=None, timeout=120):
     """producer -> host ring (as a device ring) -> the stage -> paf_dbdisk;
     returns (spectra, exit codes and stderr of [dbdisk, stage, producer]).
+    start_producer(producer process): called once the three are running.
     stage_env: the stage's own environment (default: the producer's)"""
     kin, kout = _key(), _key()
     for k in (kin, kout):
@@ -121,7 +122,7 @@ def _chain(tmp_path, exes, g, producer, env, start_producer=None, stage_env=None
                  subprocess.Popen([a.replace("KEY", f"{kin:x}") for a in producer],
                                   stderr=subprocess.PIPE, text=True, env=env)]
         if start_producer:
-            start_producer()
+            start_producer(procs[2])
         errs = [None] * 3
         for i in (2, 1, 0):
             errs[i] = procs[i].communicate(timeout=timeout)[1]
@@ -165,7 +166,7 @@ def _capture_cmd(exes, hdr, port, san=""):
 
 
 def _sender(df, ck, port, delay_s=1.5):
-    def go():
+    def go(producer=None):
         time.sleep(delay_s)  # the capture binds its ports and opens its context first
         snd = subprocess.run([os.path.join(BIN, "paf_dfsend"), "-i", str(df), "-k", str(ck), "-P", str(port),
                               "-N", "3", "-r", "50"], capture_output=True, text=True)
@@ -299,3 +300,36 @@ def test_frame_hosts_random_streams(exes, tmp_path_factory, host, nchunk, block_
         assert np.array_equal(sp[b], co.power(g, want).view(np.uint32)), (host, b, errs[2][-600:])
         gi = idf + block_ndf
         idf, sec = gi % 250000, sec + (gi // 250000) * 27
+
+
+def test_capture_sigterm_delivers_the_block_being_filled(exes, tmp_path):
+    """SIGTERM while frames of block 1 are still arriving (the stream has
+    not gone idle): the capture delivers the block being filled -- block 0,
+    whole -- ends the ring's transfer and exits 0; the stage writes its
+    spectrum and ends cleanly (the reference stopped on a quit flag,
+    capture.c:32-39)"""
+    import signal
+    g, df, ck, blocks = _stream(tmp_path, seed=13)
+    dfs = np.fromfile(df, np.uint8).reshape(-1, npo.DF_BYTES)
+    chunk = np.fromfile(ck, np.uint8)
+    h = npo.df_decode(dfs)
+    rel = np.trunc(h["idf"].astype(np.float64) + (h["sec"].astype(np.float64) - REF_SEC) / 1.08e-4 - REF_IDF)
+    keep = rel < BLOCK_NDF * 1.5  # block 0 and half of block 1
+    part_df, part_ck = tmp_path / "part.df", tmp_path / "part.chunks"
+    dfs[keep].tofile(part_df)
+    chunk[keep].tofile(part_ck)
+    hdr = _header(tmp_path, g)
+    port = 29000 + (os.getpid() % 400) * 8
+    env = dict(os.environ, B2P_STUB_DELAY_US="300", **TSAN_ENV)
+    cmd = [exes["paf_capture"], "-a", "KEY", "-f", hdr, "-c", str(BLOCK_NDF), "-P", str(port), "-N", "3",
+           "-m", "freq:1300", "-x", str(REF_IDF), "-s", str(REF_SEC), "-t", "60", "-d", "0"]
+    def start(capture):
+        _sender(part_df, part_ck, port)()
+        time.sleep(1.0)  # every frame sorted; the stream not idle for 60 s
+        capture.send_signal(signal.SIGTERM)
+
+    sp, rcs, errs = _chain(tmp_path, exes, g, cmd, env, start)
+    assert rcs == [0, 0, 0], [e[-800:] for e in errs]
+    assert "stopped by a signal" in errs[2], errs[2][-800:]
+    assert sp.shape[0] == 1, errs[2][-800:]
+    _check(g, sp, blocks)
