@@ -134,12 +134,14 @@ def test_stage_orchestration_random(stages, tmp_path_factory, case):
         args += ["-n", str(nmem), "-G", "copy"]
     if mode == "split":
         args += ["-t", str(nmem), "-G", "copy"]
-    exe = stages["dev" if mode.endswith("_dev") else "host"]
+    # B2P_STAGE_ASAN=1: the AddressSanitizer + UBSan builds (a hunt for
+    # memory the double's late queues touch after the stage let it go)
+    exe = stages[("dev" if mode.endswith("_dev") else "host") + ("_asan" if os.environ.get("B2P_STAGE_ASAN") else "")]
     out = tmp / "power.dada"
     procs, errs = [], []
     try:
         env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",
-                   B2P_STUB_DELAY_US=os.environ.get("B2P_STUB_DELAY_US", str(case["delay_us"])))
+                   B2P_STUB_DELAY_US=os.environ.get("B2P_STUB_DELAY_US", str(case["delay_us"])), **ASAN_ENV)
         procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
                                   stderr=subprocess.PIPE),
                  subprocess.Popen([exe, "-a", f"{base:x}", "-b", f"{kout:x}", "-c", str(tmp), "-d", "0"] + args,
