@@ -1024,8 +1024,14 @@ def main(argv=None) -> int:
         legs = [x for x in a.secondary.split(",") if x]
         if world == 1 and not split and a.config == "c2" and legs and a.secondary_seconds > 0:
             # the other BASELINE layouts and the one the drop-in serves, in the driver's own record
-            res["secondary"] = {x: secondary_leg(x, dev, a.secondary_seconds, max(1, cpu_threads()),
-                                                 not a.no_verify) for x in legs}
+            res["secondary"] = {}
+            for x in legs:
+                try:
+                    res["secondary"][x] = secondary_leg(x, dev, a.secondary_seconds, max(1, cpu_threads()),
+                                                        not a.no_verify)
+                except Exception as e:  # noqa: BLE001 -- the headline line still goes out, naming the leg's error
+                    print(f"bench.py: secondary leg {x} failed: {type(e).__name__}: {e}", file=sys.stderr)
+                    res["secondary"][x] = {"error": f"{type(e).__name__}: {e}", "verified": None}
             if any(v["verified"] is False for v in res["secondary"].values()):
                 res["verified"] = verified = False
         if world == 1 and a.cpu_seconds > 0 and not host_mode:

@@ -53,6 +53,10 @@ class FakeIntegrator:
 
     def __init__(self, geom, device=0, **_):
         self.g = npo.Geom(**{f: int(getattr(geom, f)) for f, _ in geom._fields_ if f != "reserved"})
+        # REHEARSAL_FAIL_NCHAN=N: opening a context of N channels fails, as a
+        # HIP error (out of memory, a lost device) would in one secondary leg
+        if os.environ.get("REHEARSAL_FAIL_NCHAN") == str(self.g.nchunk * self.g.nchan_chunk):
+            raise RuntimeError(f"b2p_open: HIP error (rehearsal: {self.g.nchunk * self.g.nchan_chunk} channels)")
         self.device = device
         self.nout, self.block_bytes = self.g.nout, self.g.block_bytes
         self.info = _Info(device, self.nout)

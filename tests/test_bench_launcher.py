@@ -355,3 +355,22 @@ def test_bench_line_carries_the_secondary_layouts_on_cpu():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--secondary", "c9"], capture_output=True,
                        text=True, timeout=120, env=env, cwd=REPO)
     assert r.returncode == 2 and "unknown layout" in r.stderr
+
+
+def test_a_failed_secondary_leg_keeps_the_headline_line():
+    """a secondary layout whose leg raises (here its context cannot be
+    opened) is reported as that leg's `error`; the headline line still goes
+    out, verified, and bench.py exits 0 -- the driver's record of configs[1]
+    never depends on a secondary leg"""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["REHEARSAL_FAIL_NCHAN"] = "336"  # the BMF leg
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tests", "bench_cpu_rehearsal.py"), "--steps", "4",
+                        "--warmup", "1", "--min-seconds", "0.2", "--bpl1-seconds", "0.1", "--secondary-seconds",
+                        "0.2", "--cpu-seconds", "0"], capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["verified"] is True and d["value"] > 0
+    assert d["secondary"]["bmf"]["verified"] is None and "HIP error" in d["secondary"]["bmf"]["error"]
+    assert d["secondary"]["c5"]["verified"] is True and d["secondary"]["c3"]["verified"] is True
+    assert "secondary leg bmf failed" in r.stderr
