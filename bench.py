@@ -1035,7 +1035,11 @@ def main(argv=None) -> int:
             if any(v["verified"] is False for v in res["secondary"].values()):
                 res["verified"] = verified = False
         if world == 1 and a.cpu_seconds > 0 and not host_mode:
-            res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)
+            try:
+                res["cpu_baseline"] = cpu_baseline(full_geom, a.cpu_seconds)
+            except Exception as e:  # noqa: BLE001 -- the line still goes out, naming the leg's error
+                print(f"bench.py: cpu_baseline failed: {type(e).__name__}: {e}", file=sys.stderr)
+                res["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}", "value": None}
         print(json.dumps(res), flush=True)
     if verified is False:
         print(f"bench.py: rank {rank}: spectra differ from the oracle", file=sys.stderr)
