@@ -41,6 +41,7 @@
  */
 #include <getopt.h>
 #include <inttypes.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -64,6 +65,15 @@ static int ring_device_of(ipcbuf_t *db) {
 }
 
 #define HDR_SIZE DADA_DEFAULT_HEADER_SIZE
+
+/* SIGINT / SIGTERM: the block being assembled is finished and delivered,
+ * then the transfer ends and paf_dfdb exits 0 (as paf_capture stops), so
+ * the stage downstream finishes normally */
+static volatile sig_atomic_t g_stop;
+static void on_stop(int sig) {
+  (void)sig;
+  g_stop = 1;
+}
 
 static double now_s(void) {
   struct timespec t;
@@ -165,6 +175,15 @@ int main(int argc, char **argv) {
     fprintf(stderr, "paf_dfdb: -a, -b and either -c/-k or -R are required (-h for usage)\n");
     return EXIT_FAILURE;
   }
+  {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sigemptyset(&sa.sa_mask);
+    sa.sa_handler = on_stop;
+    sa.sa_flags = SA_RESTART; /* reads and waits carry on; the loops look at g_stop per block */
+    sigaction(SIGINT, &sa, NULL);
+    sigaction(SIGTERM, &sa, NULL);
+  }
   multilog_t *log = multilog_open("paf_dfdb", 0);
   multilog_add(log, stderr);
   FILE *logf = NULL;
@@ -233,7 +252,7 @@ int main(int argc, char **argv) {
       multilog(log, LOG_ERR, "staging block of %" PRIu64 " B: %s", bufsz, b2p_last_error(ctx));
       goto done;
     }
-    for (uint64_t i = 0; i < replay; i++) {
+    for (uint64_t i = 0; i < replay && !g_stop; i++) {
       uint64_t bid;
       char *blk = ipcio_open_block_write(hdu->data_block, &bid);
       if (!blk) {
@@ -280,7 +299,7 @@ int main(int argc, char **argv) {
     int head = 0, live = 0, eof = 0;
     int64_t seen_hi = 0; /* latest block any accepted frame fell in */
     uint64_t placed_all = 0, sent_all = 0, dropped = 0;
-    for (int64_t b = 0;; b++) {
+    for (int64_t b = 0; !g_stop; b++) {
       /* read on until a batch lies wholly past block b+1: no later frame is
        * for block b any more */
       while (!eof) {
@@ -359,6 +378,7 @@ int main(int argc, char **argv) {
                "more than %d blocks out of order)", dropped, NSLOT - 2);
     multilog(log, LOG_INFO, "%" PRIu64 " frames read, %" PRIu64 " placed", sent_all, placed_all);
   }
+  if (g_stop) multilog(log, LOG_INFO, "stopped by a signal after %" PRIu64 " blocks: ending the transfer", nblk);
   const double el = now_s() - t0;
   multilog(log, LOG_INFO, "dfdb: %" PRIu64 " blocks of %" PRIu64 " B in %.3f s (%.2f GB/s of blocks)",
            nblk, bufsz, el, el > 0 ? (double)nblk * bufsz / el / 1e9 : 0.0);

@@ -18,6 +18,11 @@
  * ~10 GB/s on one core and bounds the whole file -> ring -> GPU chain
  * (DESIGN.md section 7); the slices are filled in parallel and the block is
  * closed once all of them have landed, so readers see the same bytes.
+ * SIGINT / SIGTERM stop it as the end of the file would: the blocks read so
+ * far are delivered, the one being read is dropped (the end-of-data block
+ * takes its place), the transfer ends and it exits 0, so the stage
+ * downstream finishes normally (the reference's diskdb had no handler;
+ * killed, it left the transfer open and its reader waiting).
  *
  * -DB2P_PSRDADA builds it against PSRDADA's own headers and the PSRDADA
  * subset the reference calls, as the reference is
@@ -28,6 +33,7 @@
 #include <getopt.h>
 #include <inttypes.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -133,6 +139,14 @@ static int init_diskdb(conf_t *conf) {
   return EXIT_SUCCESS;
 }
 
+/* set by SIGINT / SIGTERM; a read blocked on a stream returns at once (no
+ * SA_RESTART), a wait for a free ring block finishes first */
+static volatile sig_atomic_t g_stop;
+static void on_stop(int sig) {
+  (void)sig;
+  g_stop = 1;
+}
+
 typedef struct slice_t {
   int fd;
   char *dst;
@@ -149,7 +163,7 @@ static void *read_slice(void *arg) {
   while (s->got < s->len) {
     const ssize_t k = pread(s->fd, s->dst + s->got, s->len - s->got, (off_t)(s->off + s->got));
     if (k < 0) {
-      if (errno == EINTR) continue;
+      if (errno == EINTR && !g_stop) continue;
       s->err = errno;
       break;
     }
@@ -216,7 +230,7 @@ static int64_t read_stream(int fd, char *dst, size_t n) {
   while (got < n) {
     const ssize_t k = read(fd, dst + got, n - got);
     if (k < 0) {
-      if (errno == EINTR) continue;
+      if (errno == EINTR && !g_stop) continue;
       return -1;
     }
     if (k == 0) break;
@@ -293,8 +307,13 @@ static int do_diskdb(conf_t *conf) {
    * block ends the transfer, as fread's did (diskdb.cu:103-121) */
   double wait_s = 0, read_s = 0, first_s = 0; /* first_s: the first pass over the ring's blocks */
   const uint64_t nbufs = ipcbuf_get_nbufs((ipcbuf_t *)conf->hdu->data_block);
+  int stopped = 0;
   for (uint64_t off = 0;;) {
     struct timespec a, b, c;
+    if (g_stop) { /* before a block is opened: the transfer ends after the last one */
+      stopped = 1;
+      break;
+    }
     clock_gettime(CLOCK_MONOTONIC, &a);
     char *curbuf = ipcio_open_block_write(conf->hdu->data_block, &block_id);
     if (!curbuf) {
@@ -309,6 +328,10 @@ static int do_diskdb(conf_t *conf) {
     const double rs = (double)(c.tv_sec - b.tv_sec) + (double)(c.tv_nsec - b.tv_nsec) * 1e-9;
     read_s += rs;
     if (nblk < nbufs) first_s += rs;
+    if (g_stop) { /* the block being read is dropped: the end of the transfer takes its place */
+      stopped = 1;
+      break;
+    }
     if (got < 0) {
       multilog(conf->log, LOG_ERR, "read of %s at %" PRIu64 " failed: %s", conf->fname, off, strerror(errno));
       ipcio_close_block_write(conf->hdu->data_block, 0);
@@ -331,6 +354,8 @@ static int do_diskdb(conf_t *conf) {
     if (n < conf->rbufsz) break; /* the short block already ended the transfer */
   }
   free(stage);
+  if (stopped)
+    multilog(conf->log, LOG_INFO, "stopped by a signal after %" PRIu64 " blocks: ending the transfer", nblk);
   clock_gettime(CLOCK_MONOTONIC, &t1);
   double el = (double)(t1.tv_sec - t0.tv_sec) + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-9;
   multilog(conf->log, LOG_INFO,
@@ -396,6 +421,14 @@ int main(int argc, char **argv) {
   FILE *lf = logname[0] ? fopen(logname, "ab") : NULL;
   multilog_add(conf.log, lf ? lf : stderr);
 
+  {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sigemptyset(&sa.sa_mask);
+    sa.sa_handler = on_stop; /* no SA_RESTART: a read blocked on a stream returns EINTR */
+    sigaction(SIGINT, &sa, NULL);
+    sigaction(SIGTERM, &sa, NULL);
+  }
   int rc = init_diskdb(&conf);
   if (rc == EXIT_SUCCESS) rc = do_diskdb(&conf);
   destroy_diskdb(&conf);

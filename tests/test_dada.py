@@ -389,6 +389,48 @@ def test_diskdb_reads_a_fifo_and_a_growing_file_to_their_end(tmp_path, ring):
     assert b"".join(seen2) == payload.tobytes()
 
 
+def test_diskdb_stops_cleanly_on_sigterm(tmp_path, ring):
+    """SIGTERM while paf_diskdb waits on its input (a FIFO that has delivered
+    a block and a half): the whole block goes out, the half block is dropped
+    -- the end of data takes its place -- the transfer ends and paf_diskdb
+    exits 0, so the reader downstream finishes normally"""
+    import signal
+    bufsz = 1 << 16
+    hdr = tmp_path / "header.txt"
+    hdr.write_text(TEMPLATE)
+    payload = np.random.default_rng(11).integers(0, 256, 3 * bufsz, dtype=np.uint8)
+    whole = tmp_path / "whole.dada"
+    dada.write_dada_file(str(whole), "FILE_HEADER_IS_SKIPPED 1\n", payload)
+    blob = whole.read_bytes()
+    k = ring(4, bufsz)
+    fifo = tmp_path / "obs.fifo"
+    os.mkfifo(fifo)
+    out = tmp_path / "out.dada"
+    sink = subprocess.Popen([f"{BIN}/paf_dbdisk", "-k", f"{k:x}", "-o", str(out)], stderr=subprocess.PIPE)
+    p = run_diskdb(k, str(fifo), str(hdr), threads=2)
+    f = open(fifo, "wb")
+    try:
+        f.write(blob[: 4096 + bufsz + bufsz // 2])
+        f.flush()
+        t_end = time.time() + 30
+        while (not out.exists() or out.stat().st_size < 4096 + bufsz) and time.time() < t_end:
+            time.sleep(0.02)
+        time.sleep(0.2)  # the half block read, paf_diskdb waiting for the rest
+        assert p.poll() is None
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(30) == 0, p.stderr.read()
+        assert sink.wait(30) == 0, sink.stderr.read()
+    finally:
+        f.close()
+        for q in (p, sink):
+            if q.poll() is None:
+                q.kill()
+                q.wait()
+    assert b"stopped by a signal after 1 blocks" in p.stderr.read()
+    _, data = dada.read_dada_file(str(out))
+    assert data.tobytes() == payload[:bufsz].tobytes()
+
+
 def test_diskdb_rejects_bad_thread_count(tmp_path):
     r = subprocess.run([f"{BIN}/paf_diskdb", "-a", "dada", "-c", "x", "-d", "y", "-T", "0"],
                        capture_output=True, text=True)

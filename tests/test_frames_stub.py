@@ -67,13 +67,13 @@ def exes(tmp_path_factory):
     return out
 
 
-def _stream(tmp_path, lost=0, seed=3):
-    """a BMF frame stream of NBLK blocks (paf_dfgen: frames shuffled within a
+def _stream(tmp_path, lost=0, seed=3, nblk=NBLK):
+    """a BMF frame stream of nblk blocks (paf_dfgen: frames shuffled within a
     window, `lost` frames left out), its frames and chunk indices, and the
     blocks the oracle assembles from it"""
     g = npo.Geom(nbit=16, big_endian=1, nchunk=NCHUNK, nsamp_df=128, nchan_chunk=7,
                  nsamp_int=BLOCK_NDF * 128)
-    payload = co.fill_synthetic(g, g.block_bytes * NBLK, 20181105, 4, seed)
+    payload = co.fill_synthetic(g, g.block_bytes * nblk, 20181105, 4, seed)
     src = tmp_path / "in.dada"
     dada.write_dada_file(str(src), "NBIT 16\n", payload)
     df, ck = tmp_path / "s.df", tmp_path / "s.chunks"
@@ -83,7 +83,7 @@ def _stream(tmp_path, lost=0, seed=3):
     dfs = np.fromfile(df, np.uint8).reshape(-1, npo.DF_BYTES)
     chunk = np.fromfile(ck, np.uint8)
     blocks, idf, sec = [], REF_IDF, REF_SEC
-    for b in range(NBLK):
+    for b in range(nblk):
         want = np.zeros(g.block_bytes, np.uint8)  # lost frames read as zeros
         co.assemble(dfs, chunk, idf, sec, want, BLOCK_NDF, NCHUNK)
         if not lost:
@@ -332,4 +332,52 @@ def test_capture_sigterm_delivers_the_block_being_filled(exes, tmp_path):
     assert rcs == [0, 0, 0], [e[-800:] for e in errs]
     assert "stopped by a signal" in errs[2], errs[2][-800:]
     assert sp.shape[0] == 1, errs[2][-800:]
+    _check(g, sp, blocks)
+
+
+def test_dfdb_sigterm_delivers_the_block_in_hand(exes, tmp_path):
+    """SIGTERM while paf_dfdb waits for a free ring block (the ring full, no
+    reader yet): once a block frees, the one it was waiting to fill is
+    assembled and delivered, then the transfer ends and paf_dfdb exits 0;
+    the stage downstream integrates exactly those blocks, each equal to the
+    oracle's"""
+    import signal
+    g, df, ck, blocks = _stream(tmp_path, seed=17, nblk=6)  # stopped after 3 of the 6
+    kin, kout = _key(), _key()
+    for k in (kin, kout):
+        dada.destroy_ring(k)
+    dada.create_ring(kin, 2, g.block_bytes)
+    dada.create_ring(kout, 8, g.nout * 4)
+    out = tmp_path / "power.dada"
+    env = dict(os.environ, B2P_STUB_DELAY_US="300", **TSAN_ENV)
+    procs = []
+    try:
+        dfdb = subprocess.Popen([exes["paf_dfdb"], "-a", f"{kin:x}", "-b", _header(tmp_path, g), "-c", str(df),
+                                 "-k", str(ck), "-n", str(NCHUNK), "-x", str(REF_IDF), "-s", str(REF_SEC)],
+                                stderr=subprocess.PIPE, text=True, env=env)
+        procs.append(dfdb)
+        time.sleep(1.5)  # blocks 0 and 1 fill the ring; block 2 waits for a free slot
+        assert dfdb.poll() is None
+        dfdb.send_signal(signal.SIGTERM)
+        time.sleep(0.3)
+        procs += [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                   stderr=subprocess.PIPE, text=True),
+                  subprocess.Popen([exes["paf_baseband2power"], "-a", f"{kin:x}", "-b", f"{kout:x}", "-c",
+                                    str(tmp_path), "-d", "0", "-f", "header"], stderr=subprocess.PIPE, text=True,
+                                   env=env)]
+        errs = [p.communicate(timeout=60)[1] for p in procs]
+        rcs = [p.returncode for p in procs]
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for k in (kin, kout):
+            dada.destroy_ring(k)
+    assert rcs == [0, 0, 0], [e[-800:] for e in errs]
+    m = re.search(r"stopped by a signal after (\d+) blocks", errs[0])
+    assert m and 1 <= int(m.group(1)) < 6, errs[0][-800:]  # (3 when the ring filled before the signal)
+    sp = data.view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == int(m.group(1))
     _check(g, sp, blocks)
