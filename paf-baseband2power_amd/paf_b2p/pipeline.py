@@ -186,25 +186,7 @@ def run(conf_path: str, directory: str, gpu: int, datafile: str, nsub: int = 1,
                 _bin("paf_diskdb", bin_dir), "-a", f"{kin:x}", "-b", os.path.dirname(os.path.abspath(dfile)),
                 "-c", os.path.basename(dfile), "-d", hdr, "-e", str(c["diskdb_sod"])]),
                 stderr=subprocess.PIPE))
-        t_end = time.time() + timeout
-        failed = None
-        while any(p.poll() is None for p in procs):
-            for p in procs:
-                if p.poll() not in (None, 0):
-                    failed = p
-            if failed or time.time() > t_end:
-                break
-            time.sleep(0.05)
-        if failed is None:
-            failed = next((p for p in procs if p.poll() not in (None, 0)), None)
-        if failed is not None or any(p.poll() is None for p in procs):
-            for p in procs:  # stop the rest (exact PIDs we started)
-                if p.poll() is None:
-                    p.kill()
-                    p.wait()
-            msgs = [f"{p.args[0]}: rc={p.returncode} {p.stderr.read().decode(errors='replace')[-400:]}"
-                    for p in procs]
-            raise RuntimeError("pipeline failed:\n" + "\n".join(msgs))
+        _wait_all(procs, timeout)
         return outs
     finally:
         for k in keys:  # paf-baseband2power.py:129-130
@@ -220,14 +202,28 @@ def _resolve_header(c, conf_path, hfname):
     return hdr
 
 
-def _wait_all(procs, timeout):
+def _wait_all(procs, timeout, grace=30.0):
+    """until every stage has ended; the first failure (or the timeout) stops
+    the rest.  Ctrl-C reaches the stages too (one process group): they end
+    their transfers and exit, which is waited for (up to `grace` s) before
+    the rings go, so the spectra written so far stay whole"""
     t_end = time.time() + timeout
     failed = None
-    while any(p.poll() is None for p in procs):
-        failed = next((p for p in procs if p.poll() not in (None, 0)), None)
-        if failed or time.time() > t_end:
-            break
-        time.sleep(0.05)
+    try:
+        while any(p.poll() is None for p in procs):
+            failed = next((p for p in procs if p.poll() not in (None, 0)), None)
+            if failed or time.time() > t_end:
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        t_grace = time.time() + grace
+        for p in procs:
+            try:
+                p.wait(max(0.0, t_grace - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        raise
     failed = failed or next((p for p in procs if p.poll() not in (None, 0)), None)
     if failed is not None or any(p.poll() is None for p in procs):
         for p in procs:  # stop the rest (exact PIDs we started)

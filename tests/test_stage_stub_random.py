@@ -639,3 +639,68 @@ def test_pipeline_memcheck_runs_the_stage_on_the_debug_library(stages, tmp_path)
     assert (tmp_path / "ldpath").read_text().split(":")[0].strip() == dbg
     sp = dada.read_dada_file(outs[0])[1].view(np.uint32).reshape(-1, g.nout)
     assert sp.shape[0] == 1 and np.array_equal(sp[0], co.power(g, p).view(np.uint32))
+
+
+def test_pipeline_ctrl_c_lets_the_stages_finish(stages, tmp_path):
+    """Ctrl-C on `python -m paf_b2p.pipeline` (SIGINT to its process group,
+    as a terminal sends it): the launcher waits for the stages, which got the
+    same signal -- paf_diskdb ends its transfer, the stage ends its output
+    transfer -- then removes the rings; the spectra written so far are in
+    the file, whole, and no process of the run is left"""
+    import signal
+    import sys
+    import textwrap
+    g = npo.Geom(nbit=8, nchan_chunk=64, nsamp_int=1 << 10)
+    hfile = tmp_path / "hdr.txt"
+    hfile.write_text("HEADER DADA\nHDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 64\nTSAMP 0.84375\n")
+    block = co.fill_synthetic(g, g.block_bytes, 20181105, 0, 0)
+    fifo = tmp_path / "obs.fifo"
+    os.mkfifo(fifo)
+    kin, kout = _key(), _key()
+    from test_gpu_pipeline import write_conf
+    conf = tmp_path / "p.conf"
+    write_conf(conf, 1 << 10, 1, 256, 64, kin, kout, str(hfile))
+    script = tmp_path / "run.py"
+    script.write_text(textwrap.dedent(f"""\
+        import sys
+        sys.path.insert(0, {os.path.join(REPO, "paf-baseband2power_amd")!r})
+        from paf_b2p import pipeline
+        pipeline.run({str(conf)!r}, {str(tmp_path / "out")!r}, 0, {str(fifo)!r}, timeout=120,
+                     stage_exe={stages["host"]!r})
+        """))
+    run = subprocess.Popen([sys.executable, str(script)], stderr=subprocess.PIPE, text=True,
+                           start_new_session=True)
+    out = tmp_path / "out" / "power.dada"
+    t_end = time.time() + 30
+    while True:  # the write end opens once paf_diskdb has the read end open
+        try:
+            fd = os.open(fifo, os.O_WRONLY | os.O_NONBLOCK)
+            break
+        except OSError:
+            assert run.poll() is None and time.time() < t_end, run.communicate()[1][-2000:]
+            time.sleep(0.05)
+    os.set_blocking(fd, True)
+    f = os.fdopen(fd, "wb")
+    try:
+        f.write(b"H" * 4096 + block.tobytes() + block.tobytes()[: g.block_bytes // 2])
+        f.flush()
+        t_end = time.time() + 30
+        while (not out.exists() or out.stat().st_size < 4096 + g.nout * 4) and time.time() < t_end:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        assert run.poll() is None
+        os.killpg(run.pid, signal.SIGINT)
+        _, err = run.communicate(timeout=60)
+    finally:
+        f.close()
+        if run.poll() is None:
+            os.killpg(run.pid, signal.SIGKILL)
+            run.wait()
+    assert "KeyboardInterrupt" in err, err[-2000:]
+    with pytest.raises(ProcessLookupError):  # every process of the run has ended
+        os.killpg(run.pid, 0)
+    log = (tmp_path / "out" / "paf_baseband2power.log").read_text()
+    assert "FINISH PAF_PROCESS: 1 integrations, 0 skipped, ok" in log, log[-800:]  # stopped, not failed
+    sp = dada.read_dada_file(str(out))[1].view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == 1 and np.array_equal(sp[0], co.power(g, block).view(np.uint32))
+    assert not dada.destroy_ring(kin) and not dada.destroy_ring(kout)  # the launcher removed them
