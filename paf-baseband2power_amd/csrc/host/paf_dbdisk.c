@@ -10,11 +10,14 @@
  *   exits after the first end of data, where dada_dbdisk without -s waits
  *   for the next transfer)
  *   -o file  explicit output path (instead of the DADA naming rule)
+ * SIGINT / SIGTERM: the block being written is finished, the file closed,
+ * exit 0 (a wait for the next block gives up at once).
  */
 #include <errno.h>
 #include <fcntl.h>
 #include <getopt.h>
 #include <sched.h>
+#include <signal.h>
 #include <inttypes.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +26,13 @@
 #include <unistd.h>
 
 #include "b2p_dada.h"
+
+static volatile sig_atomic_t g_stop;
+static void on_stop(int sig) {
+  (void)sig;
+  g_stop = 1;
+  dada_interrupt_waits(); /* a reader waiting for its next block gives up */
+}
 
 /* every byte of buf to fd (a block reaches the file when it leaves the ring,
  * as in dada_dbdisk: no stdio buffer holding small spectra back) */
@@ -72,6 +82,15 @@ int main(int argc, char **argv) {
     fprintf(stderr, "paf_dbdisk: %s exists; -W overwrites\n", ofile);
     return EXIT_FAILURE;
   }
+  {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sigemptyset(&sa.sa_mask);
+    sa.sa_handler = on_stop;
+    sa.sa_flags = SA_RESTART; /* a write in progress completes */
+    sigaction(SIGINT, &sa, NULL);
+    sigaction(SIGTERM, &sa, NULL);
+  }
   multilog_t *log = multilog_open("paf_dbdisk", 0);
   multilog_add(log, stderr);
   if (core >= 0) {
@@ -110,7 +129,7 @@ int main(int argc, char **argv) {
   ipcbuf_t *db = &hdu->data_block->buf;
   char *stage = NULL; /* a GPU-resident ring's blocks come back through host */
   if (ipcbuf_get_device(db) >= 0 && !(stage = malloc(ipcbuf_get_bufsz(db)))) rc = EXIT_FAILURE;
-  for (; rc == EXIT_SUCCESS;) {
+  for (; rc == EXIT_SUCCESS && !g_stop;) {
     uint64_t bytes = 0, bid = 0;
     char *b = ipcio_open_block_read(hdu->data_block, &bytes, &bid);
     if (!b) break;
@@ -126,6 +145,7 @@ int main(int argc, char **argv) {
     if (bytes) nblk++; /* a 0-byte block only carries the end of data */
   }
   free(stage);
+  if (g_stop) multilog(log, LOG_INFO, "dbdisk: stopped by a signal after %" PRIu64 " blocks", nblk);
   if (close(fd) < 0) rc = EXIT_FAILURE;
   multilog(log, LOG_INFO, "dbdisk: %s: %" PRIu64 " B in %" PRIu64 " blocks", ofile, total, nblk);
   dada_hdu_unlock_read(hdu);

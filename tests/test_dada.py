@@ -431,6 +431,32 @@ def test_diskdb_stops_cleanly_on_sigterm(tmp_path, ring):
     assert data.tobytes() == payload[:bufsz].tobytes()
 
 
+def test_dbdisk_stops_cleanly_on_sigterm(tmp_path, ring):
+    """SIGTERM while paf_dbdisk waits for the next block (the writer idle,
+    its transfer open): the wait gives up, the file keeps every block so
+    far, paf_dbdisk exits 0"""
+    import signal
+    k = ring(4, 1344)
+    out = tmp_path / "power.dada"
+    sink = subprocess.Popen([f"{BIN}/paf_dbdisk", "-k", f"{k:x}", "-o", str(out)], stderr=subprocess.PIPE)
+    try:
+        with dada.Hdu(k, "W") as w:
+            w.write_header(TEMPLATE)
+            for n in (1, 2):
+                w.write_block(bytes([n]) * 1344)
+            t_end = time.time() + 10
+            while (not out.exists() or out.stat().st_size < 4096 + 2 * 1344) and time.time() < t_end:
+                time.sleep(0.01)
+            sink.send_signal(signal.SIGTERM)
+            assert sink.wait(10) == 0, sink.stderr.read()
+    finally:
+        if sink.poll() is None:
+            sink.kill()
+            sink.wait()
+    assert b"stopped by a signal after 2 blocks" in sink.stderr.read()
+    assert dada.read_dada_file(str(out))[1].tobytes() == b"\1" * 1344 + b"\2" * 1344
+
+
 def test_diskdb_rejects_bad_thread_count(tmp_path):
     r = subprocess.run([f"{BIN}/paf_diskdb", "-a", "dada", "-c", "x", "-d", "y", "-T", "0"],
                        capture_output=True, text=True)
