@@ -257,6 +257,37 @@ def kernel_sources_sha() -> str:
     return h.hexdigest()
 
 
+def device_code_sha(lib: str | None = None) -> str | None:
+    """sha256 of the gfx950 code objects the library carries (its ELF
+    section .hip_fatbin): what the GPU runs.  A change to the host half of
+    KERNEL_SOURCES (b2p_ctx.hip) changes kernel_sources_sha but not this;
+    None if the library has no such section"""
+    import hashlib
+    import struct
+    if lib is None:
+        sys.path.insert(0, PKG)
+        from paf_b2p import _lib
+        lib = _lib.LIB_PATH
+    try:
+        data = open(lib, "rb").read()
+    except OSError:
+        return None
+    if data[:4] != b"\x7fELF" or data[4] != 2:  # ELF64 only
+        return None
+    shoff = struct.unpack_from("<Q", data, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def section(i):  # sh_name, sh_type, sh_flags, sh_addr, sh_offset, sh_size, ...
+        return struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize)
+    names = section(shstrndx)[4]
+    for i in range(shnum):
+        sh = section(i)
+        name = data[names + sh[0]: data.index(b"\0", names + sh[0])]
+        if name == b".hip_fatbin":
+            return hashlib.sha256(data[sh[4]: sh[4] + sh[5]]).hexdigest()
+    return None
+
+
 def pmc_traffic(config: str, bytes_per_launch: float):
     """HBM bytes per launch from the committed rocprofv3 PMC summary for this
     config (profiles/pmc_<config>.json, written by tools/pmc_summary.py from
@@ -276,6 +307,8 @@ def pmc_traffic(config: str, bytes_per_launch: float):
         sha = d.get("kernel_sources_sha256")
         prov = {"measured_commit": d.get("commit"), "kernel_sources_commit": d.get("kernel_sources_commit"),
                 "stale": sha != kernel_sources_sha() if sha else None}
+        if d.get("device_code_sha256"):  # the code objects measured vs the ones this run loads
+            prov["device_code_match"] = d["device_code_sha256"] == device_code_sha()
         if prov["stale"] is None:
             prov["note"] = "summary predates source stamping: freshness unknown"
         if prov["stale"]:
@@ -998,7 +1031,8 @@ def main(argv=None) -> int:
                 {"same_as_headline": True, "blocks_per_launch": 1} if bpl == 1 else None),
             "cpu_baseline": None,
             "provenance": {"kernel_sources_sha256": kernel_sources_sha(),
-                           "kernel_sources": list(KERNEL_SOURCES)},
+                           "kernel_sources": list(KERNEL_SOURCES),
+                           "device_code_sha256": device_code_sha()},
         }
         if host_mode and h2d:
             # PCIe-bound: the ceiling is the bare H2D stream measured above;

@@ -182,7 +182,8 @@ int b2p_set_stream(b2p_ctx_t *ctx, void *hip_stream);
  *  - the memory must stay allocated while registered;
  *  - unregister: first drains the context's streams (a b2p_finish_async into
  *    the range may still be landing); work the caller enqueued elsewhere on
- *    the range must be complete; any context may release a range;
+ *    the range must be complete; any context may release a range; a base
+ *    that is not registered is B2P_EINVAL;
  *  - b2p_close releases every range its context registered and the caller
  *    left registered. */
 int b2p_register_host(b2p_ctx_t *ctx, void *base, size_t bytes);

@@ -519,27 +519,34 @@ static int flush_pending(b2p_ctx_t *c);
 // caller had unregistered, and possibly freed, it.  Work the caller
 // enqueued on other contexts or streams that touches the range must be
 // complete before this call.
-static int unregister_locked(b2p_ctx_t *c, const char *base) {
+// The drain runs without g_reg_mu: it waits on this context's streams only,
+// and holding the process-wide lock across it stalled every other
+// context's register / unregister (and, in the debug build, its host pushes,
+// dbg_check_host_range) for as long (advisor, round 5).  The range stays in
+// g_regs until it is unregistered, so no overlapping registration can slip
+// in meanwhile.
+static int drain_for_unregister(b2p_ctx_t *c) {
   if (!c->failed && c->pend.valid) {
     const int rf = flush_pending(c);
     if (rf != B2P_OK) return rf;
   }
   if (c->stream) CK(c, hipStreamSynchronize(c->stream));
   if (c->copy_stream) CK(c, hipStreamSynchronize(c->copy_stream));
-  CK(c, hipHostUnregister(const_cast<char *>(base)));
   return B2P_OK;
 }
 
 int b2p_unregister_host(b2p_ctx_t *c, void *base) {
   if (!c || !base) return B2P_EINVAL;
   CK(c, hipSetDevice(c->device));
-  std::lock_guard<std::mutex> lk(g_reg_mu);
+  const int rc = drain_for_unregister(c);
+  if (rc != B2P_OK) return rc;
   const char *b = static_cast<const char *>(base);
-  int rc = unregister_locked(c, b);
-  if (rc == B2P_OK)
-    g_regs.erase(std::remove_if(g_regs.begin(), g_regs.end(), [b](const HostReg &r) { return r.base == b; }),
-                 g_regs.end());
-  return rc;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = std::find_if(g_regs.begin(), g_regs.end(), [b](const HostReg &r) { return r.base == b; });
+  if (it == g_regs.end()) return set_err(c, B2P_EINVAL, "host range %p is not registered", base);
+  CK(c, hipHostUnregister(const_cast<char *>(b)));
+  g_regs.erase(it);
+  return B2P_OK;
 }
 
 static hipEvent_t pool_event(b2p_ctx_t *c) {

@@ -374,3 +374,25 @@ def test_a_failed_secondary_leg_keeps_the_headline_line():
     assert d["secondary"]["bmf"]["verified"] is None and "HIP error" in d["secondary"]["bmf"]["error"]
     assert d["secondary"]["c5"]["verified"] is True and d["secondary"]["c3"]["verified"] is True
     assert "secondary leg bmf failed" in r.stderr
+
+
+def test_device_code_sha_is_the_code_object_section():
+    """bench.py's provenance names the sha256 of the library's gfx950 code
+    objects (.hip_fatbin), read by a small ELF parse: the same bytes
+    llvm-objcopy extracts"""
+    import hashlib
+    import shutil
+    import tempfile
+    sys.path.insert(0, REPO)
+    import bench
+    sha = bench.device_code_sha()
+    assert sha and len(sha) == 64
+    objcopy = shutil.which("llvm-objcopy") or "/opt/rocm/lib/llvm/bin/llvm-objcopy"
+    if not os.path.exists(objcopy):
+        pytest.skip("no llvm-objcopy")
+    from paf_b2p import _lib
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "fatbin")
+        subprocess.run([objcopy, "--dump-section", f".hip_fatbin={out}", _lib.LIB_PATH, os.path.join(d, "x")],
+                       check=True)
+        assert hashlib.sha256(open(out, "rb").read()).hexdigest() == sha

@@ -12,8 +12,9 @@ coalesced streaming read on gfx950, so it is doubled.
 
 Provenance: the summary records the sha256 of the integrate kernel's sources
 (bench.KERNEL_SOURCES) the passes ran -- read from the profiled bench.py's own
-JSON line (--bench-log; the GPU box has no git) or else hashed here -- plus
-the git commit and the last commit that touched those sources.  bench.py
+JSON line (--bench-log; the GPU box has no git) or else hashed here -- and of
+the library's gfx950 code objects (bench.device_code_sha), plus the git
+commit and the last commit that touched those sources.  bench.py
 marks the traffic it quotes STALE when today's sources hash differently.
 """
 from __future__ import annotations
@@ -62,12 +63,15 @@ def main():
     sys.path.insert(0, REPO)
     import bench
     sha, sha_from = bench.kernel_sources_sha(), "hashed by tools/pmc_summary.py at summary time"
+    dev_sha = bench.device_code_sha()  # the code objects of the library in this tree
     for path in filter(None, [a.bench_log]):
         for ln in open(path):
             if ln.startswith("{"):
-                got = (json.loads(ln).get("provenance") or {}).get("kernel_sources_sha256")
-                if got:
-                    sha, sha_from = got, f"from the profiled run's JSON line ({os.path.relpath(path, REPO)})"
+                prov = json.loads(ln).get("provenance") or {}
+                if prov.get("kernel_sources_sha256"):
+                    sha, sha_from = prov["kernel_sources_sha256"], \
+                        f"from the profiled run's JSON line ({os.path.relpath(path, REPO)})"
+                dev_sha = prov.get("device_code_sha256") or dev_sha
 
     def git(*args):
         r = subprocess.run(["git", "-C", REPO, *args], capture_output=True, text=True)
@@ -95,6 +99,7 @@ def main():
         "kernel_sources_sha256": sha,
         "kernel_sources_sha256_from": sha_from,
         "kernel_sources_match_tree": sha == bench.kernel_sources_sha(),
+        "device_code_sha256": dev_sha,
         "commit": git("rev-parse", "HEAD"),
         "kernel_sources_commit": git("log", "-1", "--format=%H", "--", *bench.KERNEL_SOURCES),
     }
