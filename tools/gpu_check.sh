@@ -167,14 +167,14 @@ for s in $STEPS; do
             -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     pmc) # 12 steps: every launch carries bench.py's default 4 blocks (c2); no one-per-launch leg
          run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
-            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 &&
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 --secondary-seconds 0 &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \
-            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 ;;
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --bpl1-seconds 0 --secondary-seconds 0 ;;
     pmc1) # the one-block launch shape (MULTI=false) of configs[1]
          run pmc_fetch_bpl1 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_bpl1" -o run \
-            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --blocks-per-launch 1 &&
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --blocks-per-launch 1 --secondary-seconds 0 &&
          run pmc_write_bpl1 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_bpl1" -o run \
-            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --blocks-per-launch 1 ;;
+            -- python3 bench.py --steps 12 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify --blocks-per-launch 1 --secondary-seconds 0 ;;
     pmc5) run pmc_fetch_c5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch_c5" -o run \
             -- python3 bench.py --config c5 --steps 6 --warmup 2 --cpu-seconds 0 --min-seconds 0 --no-verify &&
          run pmc_write_c5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_c5" -o run \

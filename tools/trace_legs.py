@@ -8,7 +8,9 @@ together under one kernel name, so its figure matches neither.  The bench
 line lists its integrate launches in issue order per phase
 (roofline.launch_phases); this slices the trace's integrate dispatches
 (ordered by dispatch id) by those counts and reports each leg's launch
-durations, and for the headline the HBM fraction they imply.
+durations, and for the headline the HBM fraction they imply.  The secondary
+layouts (`secondary` in the line) follow, each as its warm-up region and its
+timed launches, with their own HBM fractions.
 
   tools/trace_legs.py --trace gpurun_out/prof/run_kernel_trace.csv \\
       --bench-log gpurun_out/prof.log [--out profiles/r04_c2_kernel_legs.json]
@@ -30,9 +32,20 @@ def legs(trace_path: str, line: dict) -> dict:
     names = [r["Kernel_Name"] for r in rows]
     rf = line["roofline"]
     phases = rf.get("launch_phases") or []
-    want = sum(c for _, c in phases)
+    # the secondary legs (bench.py secondary_leg) run after those phases, in
+    # the line's order: one untimed warm-up region, then the timed regions
+    sec = []
+    for name, v in (line.get("secondary") or {}).items():
+        r = v.get("roofline") or {}
+        timed = (r.get("hbm") or {}).get("launches_timed") if r.get("bound") == "pcie" else r.get("launches_timed")
+        if timed and v.get("timed_regions"):
+            sec.append((f"secondary.{name}", timed // v["timed_regions"], timed, r))
+    want = sum(c for _, c in phases) + sum(w + t for _, w, t, _ in sec)
     out = {"trace": trace_path, "integrate_dispatches": len(dur), "launches_in_bench_line": want,
            "counts_agree": len(dur) == want, "legs": {}}
+    phases = list(phases)
+    for name, w, t, _ in sec:
+        phases += [(name + "_warmup", w), (name, t)]
     i = 0
     for name, c in phases:
         d = dur[i:i + c]
@@ -50,6 +63,12 @@ def legs(trace_path: str, line: dict) -> dict:
         h["frac_of_8TBps"] = round(b / (h["avg_us"] * 1e-6) / 1e9 / rf["peak"], 4)
         h["bench_line_avg_launch_us"] = rf["avg_launch_us"]
         h["bench_line_kernel_only_us"] = rf.get("kernel_only_us")
+    for name, _, _, r in sec:
+        leg = out["legs"].get(name)
+        if leg and r.get("bound") == "hbm":
+            b = r["algorithmic_bytes_per_launch"]
+            leg["frac_of_8TBps"] = round(b / (leg["avg_us"] * 1e-6) / 1e9 / r["peak"], 4)
+            leg["bench_line_avg_launch_us"] = r.get("avg_launch_us")
     one = out["legs"].get("one_per_launch")
     if one:
         b1 = line["config"]["bytes_per_integration"]
