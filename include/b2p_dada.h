@@ -138,6 +138,14 @@ uint64_t ipcbuf_get_eodack_iread(ipcbuf_t *id, int iread);
 int ipcbuf_get_reader_conn(ipcbuf_t *id);
 int ipcbuf_get_reader_conn_iread(ipcbuf_t *id, int iread);
 int ipcbuf_get_read_semaphore_count(ipcbuf_t *id); /* free reader slots */
+/* Extensions (not in PSRDADA), for a reader watching its writer: 1 if a
+ * writer holds the ring's write lock, 0 if none, -1 on error; 1 while a
+ * transfer is open (its start of data written, its end-of-data block not
+ * yet), 0 if not, -1 on error.  A writer that died mid-transfer shows as an
+ * open transfer with no writer (its lock is undone by the kernel); a new
+ * writer may still take the lock and go on with that transfer. */
+int ipcbuf_get_writer_conn(ipcbuf_t *id);
+int ipcbuf_get_transfer_open(ipcbuf_t *id);
 /* byte positions in this process's transfer */
 uint64_t ipcbuf_tell(ipcbuf_t *id, uint64_t bufnum);
 int64_t ipcbuf_tell_write(ipcbuf_t *id);

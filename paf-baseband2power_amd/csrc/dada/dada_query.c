@@ -40,6 +40,23 @@ int ipcbuf_get_reader_conn_iread(ipcbuf_t *id, int iread) { return (int)sem_coun
 int ipcbuf_get_reader_conn(ipcbuf_t *id) { return ipcbuf_get_reader_conn_iread(id, -1); }
 
 /* free reader slots (the connect set's READ count, @0x405780) */
+/* ---- extensions (not in PSRDADA): a reader watching its writer ----
+ * A writer holds the write lock (SEM_WRITE, taken with SEM_UNDO) for the
+ * whole of its transfer, and the sync segment's w_state is ST_WRITING from
+ * the start of data until the end-of-data block is marked filled.  A writer
+ * that dies mid-transfer releases the lock (the kernel undoes it) but leaves
+ * the transfer open: a reader sees an open transfer with no writer. */
+int ipcbuf_get_writer_conn(ipcbuf_t *id) {
+  if (!id || id->semid_connect < 0) return -1;
+  const int v = semctl(id->semid_connect, SEM_WRITE, GETVAL);
+  return v < 0 ? -1 : v == 0;
+}
+
+int ipcbuf_get_transfer_open(ipcbuf_t *id) {
+  if (!id || !id->sync) return -1;
+  return __atomic_load_n(&id->sync->w_state, __ATOMIC_ACQUIRE) != 0;
+}
+
 int ipcbuf_get_read_semaphore_count(ipcbuf_t *id) {
   return id && id->semid_connect >= 0 ? semctl(id->semid_connect, SEM_READ, GETVAL) : -1;
 }

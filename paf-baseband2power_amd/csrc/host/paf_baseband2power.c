@@ -83,6 +83,7 @@ typedef struct conf_t { /* baseband2power.cuh:18-23, plus options */
   int coll_timeout_s; /* -T: RCCL set-up / collective time limit */
   int sync;  /* -S: one block per launch, waited for (the unpipelined baseline) */
   int trace; /* -V: log every launch / round */
+  double writer_grace_s; /* -W: a transfer left open by a writer that went away ends the run after this */
 } conf_t;
 
 typedef struct sub_t { /* one sub-band: ring + GPU context + worker thread */
@@ -128,6 +129,9 @@ static void usage(void) {
           " -S  GPU-resident rings: one block per launch, each waited for before the next\n"
           "     (no launches in flight, no batching of queued blocks; a diagnostic baseline)\n"
           " -V  Log every integrate launch / gathered round\n"
+          " -W  Seconds an input transfer may stay open with no writer attached and nothing\n"
+          "     to read before the run ends with an error (a writer that died mid-transfer;\n"
+          "     default 0: wait for a writer to take the transfer on, as PSRDADA allows)\n"
           " -h  show help\n");
 }
 
@@ -135,7 +139,7 @@ static void usage(void) {
  * cleanly (unlock_write writes its end of data, so the sink finishes).
  * Ring waits in progress give up (dada_interrupt_waits); worker threads
  * blocked in one are woken with SIGUSR2 by the main thread. */
-static volatile sig_atomic_t g_stop;
+static atomic_int g_stop; /* lock-free: set by the signal handler, read by every thread */
 /* a member's input ring failed under it (next_block): every other member
  * waiting on its own ring is woken the same way, so the run ends instead of
  * waiting for blocks that are not coming */
@@ -324,6 +328,26 @@ static char *next_block(dada_hdu_t *h, uint64_t *bytes, int *failed) {
  * the run fails */
 #define HAVE_READ_FAILED (-2)
 
+#if DEVICE_RINGS
+/* -W S: the stage notices a writer that went away mid-transfer.  An input
+ * transfer that is open, with no writer holding the ring and no block
+ * waiting for this reader, for S seconds in a row, means the writer died
+ * (the kernel undid its write lock) and no other writer took the transfer
+ * on -- PSRDADA lets one, hence the grace period.  The run then ends as on
+ * a failed read: an ERR line, every member woken, exit 1.  Only shared ring
+ * state is read here (semaphores, the sync segment), never a member's
+ * ipcbuf_t fields that its thread changes. */
+typedef struct watch_t {
+  struct shared_t *sh;
+  dada_hdu_t *ring[MAX_SUB];
+  key_t key[MAX_SUB];
+  int nring;
+  double grace_s;
+  pthread_t main_th;
+  atomic_int stop;
+} watch_t;
+#endif
+
 /* ---- the integration loop, one thread per sub-band ---------------------- */
 
 typedef struct shared_t {
@@ -395,6 +419,37 @@ static int write_output(shared_t *sh, const float *spec) {
   if (sh->nblocks == kWarm) sh->t_warm = sh->t_last;
   return 0;
 }
+
+#if DEVICE_RINGS
+static void *watch_writers(void *arg) {
+  watch_t *w = (watch_t *)arg;
+  double since[MAX_SUB];
+  for (int r = 0; r < w->nring; r++) since[r] = -1;
+  while (!w->stop && !g_stop && !g_abort) {
+    const double t = now_s();
+    for (int r = 0; r < w->nring; r++) {
+      ipcbuf_t *db = data_buf(w->ring[r]);
+      const int open = ipcbuf_get_transfer_open(db), conn = ipcbuf_get_writer_conn(db);
+      const uint64_t waiting = ipcbuf_get_nfull_iread(db, db->iread);
+      if (open != 1 || conn != 0 || waiting) {
+        since[r] = -1;
+      } else if (since[r] < 0) {
+        since[r] = t;
+      } else if (t - since[r] >= w->grace_s) {
+        multilog(w->sh->log, LOG_ERR, "input ring %x: its writer went away without ending the transfer "
+                 "(open, no writer, nothing to read for %.1f s)", (unsigned)w->key[r], t - since[r]);
+        w->sh->failed = 1;
+        g_abort = 1;
+        dada_interrupt_waits();
+        pthread_kill(w->main_th, SIGUSR2); /* the main thread may be the reader (run_device_pipelined) */
+        return NULL;
+      }
+    }
+    usleep(50000);
+  }
+  return NULL;
+}
+#endif
 
 static void *worker(void *arg) {
   worker_t *w = (worker_t *)arg;
@@ -786,10 +841,10 @@ static void run_device_pipelined(shared_t *sh) {
     const void *blks[B2P_MAX_BLOCKS];
     uint64_t bytes = 0, bid = 0;
     char *blk = NULL;
-    if (!g_stop && !ipcbuf_eod(&in->buf)) {
+    if (!g_stop && !g_abort && !ipcbuf_eod(&in->buf)) {
       errno = 0;
       blk = ipcio_open_block_read(in, &bytes, &bid);
-      if (!blk && errno && !g_stop) { /* not an end of data: the ring failed under the stage */
+      if (!blk && errno && !g_stop && !g_abort) { /* not an end of data: the ring failed under the stage */
         multilog(sh->log, LOG_ERR, "reading input ring %x failed (%s)", (unsigned)s->key, strerror(errno));
         sh->failed = 1;
       }
@@ -992,7 +1047,7 @@ int main(int argc, char *argv[]) {
   strcpy(conf.dir, ".");
   int have_in = 0, have_out = 0;
 
-  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:G:T:mSVh")) != -1) {
+  while ((arg = getopt(argc, argv, "a:b:c:d:f:p:n:t:G:T:W:mSVh")) != -1) {
     switch (arg) {
       case 'h':
         usage();
@@ -1029,6 +1084,18 @@ int main(int argc, char *argv[]) {
         }
         break;
       case 'T': conf.coll_timeout_s = atoi(optarg); break;
+      case 'W':
+        if (sscanf(optarg, "%lf", &conf.writer_grace_s) != 1 || conf.writer_grace_s < 0) {
+          fprintf(stderr, "-W takes seconds >= 0, not %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+#if !DEVICE_RINGS
+        if (conf.writer_grace_s > 0) {
+          fprintf(stderr, "-W needs libpafdada's writer queries (not in PSRDADA)\n");
+          return EXIT_FAILURE;
+        }
+#endif
+        break;
       default: usage(); return EXIT_FAILURE;
     }
   }
@@ -1316,6 +1383,23 @@ int main(int argc, char *argv[]) {
              sh.gather_dev ? ", queued blocks in rounds of up to b2p_blocks_per_launch" : "");
   }
 
+#if DEVICE_RINGS
+  watch_t watch = {0};
+  pthread_t watch_th;
+  int watching = 0;
+  if (conf.writer_grace_s > 0) {
+    watch.sh = &sh;
+    watch.nring = split ? 1 : nmem;
+    for (int r = 0; r < watch.nring; r++) {
+      watch.ring[r] = sub[r].in;
+      watch.key[r] = sub[r].key;
+    }
+    watch.grace_s = conf.writer_grace_s;
+    watch.main_th = pthread_self();
+    watching = pthread_create(&watch_th, NULL, watch_writers, &watch) == 0;
+    if (!watching) multilog(log, LOG_WARNING, "-W: cannot start the writer watch; running without it");
+  }
+#endif
   {
 #if DEVICE_RINGS
     if (!split && nmem == 1 && !sh.grouped && sub[0].ondev && !conf.sync) {
@@ -1355,6 +1439,10 @@ int main(int argc, char *argv[]) {
   }
 #if DEVICE_RINGS
 joined:
+  if (watching) {
+    watch.stop = 1;
+    pthread_join(watch_th, NULL);
+  }
 #endif
   status = sh.failed ? EXIT_FAILURE : EXIT_SUCCESS;
 

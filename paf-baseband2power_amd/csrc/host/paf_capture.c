@@ -84,7 +84,7 @@ static int ring_device_of(ipcbuf_t *db) {
 /* SIGINT / SIGTERM: stop receiving, deliver the block being filled and end
  * the ring's transfer cleanly (the reference's capture stopped on a quit
  * flag polled without atomics, capture.c:32-39, 443-446) */
-static volatile sig_atomic_t g_stop;
+static atomic_int g_stop; /* lock-free: set by the signal handler, read by every thread */
 static void on_stop(int sig) {
   (void)sig;
   g_stop = 1;

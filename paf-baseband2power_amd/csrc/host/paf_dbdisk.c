@@ -19,6 +19,7 @@
 #include <sched.h>
 #include <signal.h>
 #include <inttypes.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -27,7 +28,7 @@
 
 #include "b2p_dada.h"
 
-static volatile sig_atomic_t g_stop;
+static atomic_int g_stop; /* lock-free: set by the signal handler, read by every thread */
 static void on_stop(int sig) {
   (void)sig;
   g_stop = 1;

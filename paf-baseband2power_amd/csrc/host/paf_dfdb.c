@@ -42,6 +42,7 @@
 #include <getopt.h>
 #include <inttypes.h>
 #include <signal.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -69,7 +70,7 @@ static int ring_device_of(ipcbuf_t *db) {
 /* SIGINT / SIGTERM: the block being assembled is finished and delivered,
  * then the transfer ends and paf_dfdb exits 0 (as paf_capture stops), so
  * the stage downstream finishes normally */
-static volatile sig_atomic_t g_stop;
+static atomic_int g_stop; /* lock-free: set by the signal handler, read by every thread */
 static void on_stop(int sig) {
   (void)sig;
   g_stop = 1;

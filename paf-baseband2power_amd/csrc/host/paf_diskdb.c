@@ -34,6 +34,7 @@
 #include <inttypes.h>
 #include <pthread.h>
 #include <signal.h>
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -141,7 +142,7 @@ static int init_diskdb(conf_t *conf) {
 
 /* set by SIGINT / SIGTERM; a read blocked on a stream returns at once (no
  * SA_RESTART), a wait for a free ring block finishes first */
-static volatile sig_atomic_t g_stop;
+static atomic_int g_stop; /* lock-free: set by the signal handler, read by every thread */
 static void on_stop(int sig) {
   (void)sig;
   g_stop = 1;

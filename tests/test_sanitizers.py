@@ -229,3 +229,69 @@ def test_read_depth_survives_a_view_under_asan(tmp_path):
     r = subprocess.run([str(exe), "7c50"], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "errors 0" in r.stdout
+
+
+@pytest.mark.parametrize("as_device", [False, True])
+def test_stage_stop_signal_under_tsan(tmp_path, as_device):
+    """SIGTERM to the stage while its -n 2 members wait on their rings, under
+    ThreadSanitizer: the flag the handler sets is read by every member
+    thread (a C11 atomic since round 6: as a volatile sig_atomic_t it was a
+    data race TSan reported), the waits give up, the output transfer ends,
+    exit 0 with every spectrum so far"""
+    import signal
+    import sys
+    import time
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_c as co
+    import b2p_oracle as npo
+    from paf_b2p import dada
+    exe = _stage_tsan(tmp_path, as_device=as_device)
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=128)
+    base = 0x6e00 + (os.getpid() % 64) * 0x40 + (0x20 if as_device else 0)
+    keys, kout = [base, base + 0x10], base + 4
+    for k in keys + [kout]:
+        dada.destroy_ring(k)
+    for k in keys:
+        dada.create_ring(k, 4, g.block_bytes)
+    dada.create_ring(kout, 8, 2 * g.nout * 4)
+    blocks = [co.fill_synthetic(g, g.block_bytes, 29, r, 0) for r in range(2)]
+    out = tmp_path / "power.dada"
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1", B2P_STUB_DELAY_US="300")
+    procs, writers = [], []
+    try:
+        procs = [subprocess.Popen([os.path.join(dada.BIN_DIR, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([exe, "-a", f"{base:x}", "-b", f"{kout:x}", "-c", str(tmp_path), "-d", "0",
+                                   "-f", "int8:16", "-n", "2", "-G", "copy"], stderr=subprocess.PIPE, text=True,
+                                  env=env)]
+        for k, b in zip(keys, blocks):  # one block each; the transfers stay open
+            w = dada.Hdu(k, "W")
+            writers.append(w)
+            w.write_header("HDR_SIZE 4096\nTSAMP 0.84375\n")
+            w.write_block(b.tobytes())
+        t_end = time.time() + 30
+        while (not out.exists() or out.stat().st_size < 4096 + 2 * g.nout * 4) and time.time() < t_end:
+            time.sleep(0.05)
+        time.sleep(0.3)
+        procs[1].send_signal(signal.SIGTERM)
+        _, err = procs[1].communicate(timeout=30)
+        _, derr = procs[0].communicate(timeout=30)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for w in writers:
+            try:
+                w.close()
+            except OSError:
+                pass
+        for k in keys + [kout]:
+            dada.destroy_ring(k)
+    assert "WARNING: ThreadSanitizer" not in err, err[-4000:]
+    assert procs[1].returncode == 0 and procs[0].returncode == 0, (err[-1500:], derr)
+    sp = dada.read_dada_file(str(out))[1].view(np.uint32).reshape(-1, 2, g.nout)
+    assert sp.shape[0] == 1
+    for r in range(2):
+        assert np.array_equal(sp[0, r], co.power(g, blocks[r]).view(np.uint32))

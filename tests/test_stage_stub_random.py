@@ -704,3 +704,114 @@ def test_pipeline_ctrl_c_lets_the_stages_finish(stages, tmp_path):
     sp = dada.read_dada_file(str(out))[1].view(np.uint32).reshape(-1, g.nout)
     assert sp.shape[0] == 1 and np.array_equal(sp[0], co.power(g, block).view(np.uint32))
     assert not dada.destroy_ring(kin) and not dada.destroy_ring(kout)  # the launcher removed them
+
+
+_WRITER = """
+import sys, time
+sys.path.insert(0, {pkg!r})
+import numpy as np
+from paf_b2p import dada
+key, nblk, header, path = int(sys.argv[1], 16), int(sys.argv[2]), sys.argv[3] == "1", sys.argv[4]
+data = np.fromfile(path, dtype=np.uint8)
+w = dada.Hdu(key, "W")
+if header:
+    w.write_header(open(path + ".hdr").read())
+for b in np.split(data, nblk):
+    w.write_block(b.tobytes())
+if sys.argv[5] == "hold":
+    print("written", flush=True)
+    time.sleep(120)  # the transfer stays open until this process is killed
+w.close()            # the end of data
+"""
+
+
+@pytest.mark.parametrize("mode,grace,resume", [("single", 1.0, False), ("single_dev", 1.0, False),
+                                               ("gathered", 1.0, False), ("single", 0, False),
+                                               ("single_dev", 4.0, True)])
+def test_stage_notices_a_writer_that_went_away(stages, tmp_path, mode, grace, resume):
+    """-W S: a writer killed mid-transfer (SIGKILL: no end of data; the kernel
+    undoes its write lock) leaves the stage's transfer open with no writer.
+    After S s of that the stage logs "its writer went away", wakes every
+    member and exits 1, the spectra of the blocks it had written and whole.
+    Without -W it waits (PSRDADA lets a new writer take an open transfer
+    on); and a writer that does so within the grace period carries the run
+    to its normal end"""
+    import signal
+    import sys
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=128)
+    rings = 2 if mode == "gathered" else 1
+    blocks = [[co.fill_synthetic(g, g.block_bytes, 61, r, b) for b in range(3)] for r in range(rings)]
+    hdr = ("HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 16\nNCHUNK 1\nNCHAN_CHUNK 16\nNSAMP_DF 1\n"
+           "BYTE_ORDER LE\nTSAMP 0.84375\n")
+    base, kout = _key(), _key()
+    keys = [base + 0x10 * r for r in range(rings)]
+    for k in keys + [kout]:
+        dada.destroy_ring(k)
+    for k in keys:
+        dada.create_ring(k, 6, g.block_bytes)
+    dada.create_ring(kout, 8, rings * g.nout * 4)
+    script = tmp_path / "writer.py"
+    script.write_text(_WRITER.format(pkg=PKG))
+    files = []
+    for r in range(rings):
+        f = tmp_path / f"in{r}.u8"
+        np.concatenate([b.reshape(-1).view(np.uint8) for b in blocks[r][:2]]).tofile(f)
+        (tmp_path / f"in{r}.u8.hdr").write_text(hdr)
+        files.append(f)
+    args = ["-f", "header"] + (["-n", "2", "-G", "copy"] if mode == "gathered" else []) \
+        + (["-W", str(grace)] if grace else [])
+    out = tmp_path / "power.dada"
+    procs, writers = [], []
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([stages["dev" if mode.endswith("_dev") else "host"], "-a", f"{base:x}", "-b",
+                                   f"{kout:x}", "-c", str(tmp_path), "-d", "0"] + args,
+                                  stderr=subprocess.PIPE, text=True)]
+        for k, f in zip(keys, files):  # two blocks each, the transfers left open
+            writers.append(subprocess.Popen([sys.executable, str(script), f"{k:x}", "2", "1", str(f), "hold"],
+                                            stdout=subprocess.PIPE, text=True))
+        for w in writers:
+            assert w.stdout.readline().strip() == "written"
+        t_end = time.time() + 30
+        while (not out.exists() or out.stat().st_size < 4096 + 2 * rings * g.nout * 4) and time.time() < t_end:
+            time.sleep(0.05)
+        writers[0].send_signal(signal.SIGKILL)  # ring 0's writer dies mid-transfer
+        writers[0].wait()
+        t_kill = time.time()
+        if resume:  # a new writer takes the open transfer on: one more block, then the end of data
+            time.sleep(0.5)
+            f3 = tmp_path / "in0b.u8"
+            blocks[0][2].reshape(-1).view(np.uint8).tofile(f3)
+            assert subprocess.run([sys.executable, str(script), f"{keys[0]:x}", "1", "0", str(f3), "end"],
+                                  timeout=30).returncode == 0
+        if grace and not resume:
+            _, err = procs[1].communicate(timeout=30)
+            assert procs[1].returncode == 1, err
+            assert time.time() - t_kill >= grace - 0.1  # not before the grace period
+            assert f"input ring {keys[0]:x}: its writer went away" in err and "] ERR: " in err, err
+        elif resume:
+            _, err = procs[1].communicate(timeout=30)
+            assert procs[1].returncode == 0, err
+        else:  # no -W: still waiting for a writer
+            time.sleep(2.0)
+            assert procs[1].poll() is None
+            procs[1].send_signal(signal.SIGTERM)
+            _, err = procs[1].communicate(timeout=30)
+            assert procs[1].returncode == 0, err
+        _, derr = procs[0].communicate(timeout=30)
+        assert procs[0].returncode == 0, derr
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs + writers:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for k in keys + [kout]:
+            dada.destroy_ring(k)
+    sp = data.view(np.uint32).reshape(-1, rings, g.nout)
+    n = 3 if resume else 2
+    assert sp.shape[0] == n, (sp.shape, err[-1500:])
+    for b in range(n):
+        for r in range(rings):
+            assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=1).view(np.uint32)), (b, r)
