@@ -108,3 +108,73 @@ def test_stage_input_ring_removed_under_it_gpu(gpu, tmp_path, mode):
     for b in range(nblk):
         for r in range(onsub):
             assert np.array_equal(sp[b, r], co.power(g, blocks[r][b], nthreads=1).view(np.uint32)), (b, r)
+
+
+_WRITER = """
+import sys, time
+sys.path.insert(0, {pkg!r})
+import numpy as np
+from paf_b2p import dada
+key, path = int(sys.argv[1], 16), sys.argv[2]
+w = dada.Hdu(key, "W")
+w.write_header(open(path + ".hdr").read())
+for b in np.split(np.fromfile(path, dtype=np.uint8), 2):
+    w.write_block(b.tobytes())
+print("written", flush=True)
+time.sleep(120)  # the transfer stays open until this process is killed
+"""
+
+
+@pytest.mark.parametrize("device", [-1, 0])
+def test_stage_notices_a_dead_writer_gpu(gpu, tmp_path, device):
+    """-W 1 on the GPU: the ring's writer is killed mid-transfer (SIGKILL;
+    on a GPU-resident ring its imported blocks go with it, the holder keeps
+    them for the stage); the stage logs "its writer went away" after the
+    grace second and exits 1, both spectra written and equal to the
+    oracle's"""
+    import signal
+    import sys
+    g = npo.Geom(nbit=8, nchunk=1, nsamp_df=1, nchan_chunk=16, npol_out=1, nsamp_int=128)
+    blocks = [co.fill_synthetic(g, g.block_bytes, 83, 0, b) for b in range(2)]
+    kout, kin = fresh_key(), fresh_key()
+    dada.create_ring(kin, 4, g.block_bytes, device=device)
+    dada.create_ring(kout, 8, g.nout * 4)
+    f = tmp_path / "in.u8"
+    np.concatenate([b.reshape(-1).view(np.uint8) for b in blocks]).tofile(f)
+    (tmp_path / "in.u8.hdr").write_text("HDR_SIZE 4096\nNBIT 8\nNDIM 2\nNPOL 2\nNCHAN 16\nNCHUNK 1\n"
+                                        "NCHAN_CHUNK 16\nNSAMP_DF 1\nBYTE_ORDER LE\nTSAMP 0.84375\n")
+    script = tmp_path / "writer.py"
+    script.write_text(_WRITER.format(pkg=os.path.dirname(BIN)))
+    out = tmp_path / "power.dada"
+    procs, writer = [], None
+    try:
+        procs = [subprocess.Popen([os.path.join(BIN, "paf_dbdisk"), "-k", f"{kout:x}", "-o", str(out)],
+                                  stderr=subprocess.PIPE, text=True),
+                 subprocess.Popen([os.path.join(BIN, "paf_baseband2power"), "-a", f"{kin:x}", "-b", f"{kout:x}",
+                                   "-c", str(tmp_path), "-d", "0", "-f", "header", "-W", "1"],
+                                  stderr=subprocess.PIPE, text=True)]
+        writer = subprocess.Popen([sys.executable, str(script), f"{kin:x}", str(f)], stdout=subprocess.PIPE,
+                                  text=True)
+        assert writer.stdout.readline().strip() == "written"
+        t_end = time.time() + 60
+        while (not out.exists() or out.stat().st_size < 4096 + 2 * g.nout * 4) and time.time() < t_end:
+            time.sleep(0.05)
+        writer.send_signal(signal.SIGKILL)
+        writer.wait()
+        _, err = procs[1].communicate(timeout=60)
+        _, derr = procs[0].communicate(timeout=60)
+        assert procs[1].returncode == 1, err
+        assert procs[0].returncode == 0, derr
+        _, data = dada.read_dada_file(str(out))
+    finally:
+        for p in procs + ([writer] if writer else []):
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        dada.destroy_ring(kin)
+        dada.destroy_ring(kout)
+    assert f"input ring {kin:x}: its writer went away" in err, err
+    sp = data.view(np.uint32).reshape(-1, g.nout)
+    assert sp.shape[0] == 2
+    for b in range(2):
+        assert np.array_equal(sp[b], co.power(g, blocks[b], nthreads=1).view(np.uint32)), b
