@@ -38,7 +38,7 @@ HOST = os.path.join(PKG, "csrc", "host")
 STUB = os.path.join(REPO, "tests", "c", "b2p_cpu_stub.c")
 DADA_SRC = [os.path.join(PKG, "csrc", "dada", f)
             for f in ("dada_ring.c", "dada_query.c", "dada_device.c", "ascii_header.c", "df_header.c")]
-_KEY = [0x4c00 + (os.getpid() % 64) * 0x40]
+_KEY = [0x8000 + (os.getpid() % 64) * 0x40]  # a key window of its own (holder tests use 0x4c00..)
 NCHUNK, BLOCK_NDF, NBLK = 4, 32, 3
 REF_IDF, REF_SEC = 249990, 54  # the stream crosses a 27-s period
 TSAN_ENV = {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1",
